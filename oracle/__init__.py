@@ -1,0 +1,143 @@
+"""ctypes wrapper over oracle/build/libcpt_oracle.so — TEST INFRASTRUCTURE ONLY.
+
+The oracle is the CPU restatement of the reference integrator (oracle/cpt_oracle.cpp).
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module; the product package (cpppathtracer_amd) never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "libcpt_oracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its Makefile (g++ is in the image and on the GPU box)."""
+    if force or not os.path.exists(LIB_PATH) or (
+        os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "cpt_oracle.cpp"))
+    ):
+        subprocess.run(["make", "-s", "-C", _HERE, "-B" if force else "all"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        i32, u64, f32, f64 = ctypes.c_int, ctypes.c_uint64, ctypes.c_float, ctypes.c_double
+        L.or_abi_version.restype = i32
+        L.or_sizeof.argtypes = [i32]
+        L.or_sizeof.restype = i32
+        for n in ("or_pow",):
+            getattr(L, n).argtypes = [f64, f64]
+            getattr(L, n).restype = f64
+        for n in ("or_log", "or_exp", "or_atan"):
+            getattr(L, n).argtypes = [f64]
+            getattr(L, n).restype = f64
+        L.or_powf.argtypes = [f32, f32]
+        L.or_powf.restype = f32
+        for n in ("or_sinf", "or_cosf", "or_asinf", "or_atanf"):
+            getattr(L, n).argtypes = [f32]
+            getattr(L, n).restype = f32
+        L.or_math_batch.argtypes = [i32, P, P, P, ctypes.c_long]
+        L.or_math_batch.restype = None
+        L.or_curand_init.argtypes = [u64, u64, P]
+        L.or_curand_init.restype = None
+        L.or_xorwow_next.argtypes = [P]
+        L.or_xorwow_next.restype = ctypes.c_uint32
+        L.or_uniform.argtypes = [P]
+        L.or_uniform.restype = f32
+        L.or_seq_jump_matrix_pow4.argtypes = [i32, P]
+        L.or_seq_jump_matrix_pow4.restype = None
+        L.or_init_rng.argtypes = [u64, i32, P, i32, P, i32]
+        L.or_init_rng.restype = None
+        L.or_camera_get_copy.argtypes = [P]
+        L.or_camera_get_copy.restype = None
+        L.or_build_bvh.argtypes = [P, i32, P, P, i32]
+        L.or_build_bvh.restype = i32
+        L.or_render.argtypes = [P, i32, P, P, i32, i32, i32, P, i32, i32, i32, P, P, P, P, P, i32, i32]
+        L.or_render.restype = i32
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def math_batch(op: int, a, b=None):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    b = np.ascontiguousarray(b if b is not None else np.zeros_like(a), dtype=np.float32)
+    out = np.empty_like(a)
+    lib().or_math_batch(op, _ptr(a), _ptr(b), _ptr(out), a.size)
+    return out
+
+
+def curand_init(seed: int, subsequence: int) -> np.ndarray:
+    out = np.zeros(6, dtype=np.uint32)
+    lib().or_curand_init(seed, subsequence, _ptr(out))
+    return out
+
+
+def seq_jump_matrix_pow4(t: int) -> np.ndarray:
+    out = np.zeros(800, dtype=np.uint32)
+    lib().or_seq_jump_matrix_pow4(t, _ptr(out))
+    return out
+
+
+def init_rng(seed: int, width: int, rows, threads: int = 1) -> np.ndarray:
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    out = np.zeros((6, rows.size * width), dtype=np.uint32)
+    lib().or_init_rng(seed, width, _ptr(rows), rows.size, _ptr(out), threads)
+    return out
+
+
+def camera_get_copy(cam):
+    """MotionalCamera::GetCopy on a CAMERA_DTYPE scalar/0-d array; returns the updated copy."""
+    c = np.array(cam, copy=True)
+    lib().or_camera_get_copy(_ptr(c))
+    return c
+
+
+def build_bvh(objs):
+    objs = np.ascontiguousarray(objs)
+    cap = max(1, 2 * len(objs))
+    box = np.zeros((cap, 6), dtype=np.float32)
+    link = np.zeros((cap, 4), dtype=np.int32)
+    m = lib().or_build_bvh(_ptr(objs), len(objs), _ptr(box), _ptr(link), cap)
+    return box[:m], link[:m]
+
+
+def render(objs, cam, env, rows, spp, max_depth, rng, accum=None, want_aux=False, accumulate=False,
+           threads=1):
+    """Run `spp` passes of the reference integrator over `rows` (global row indices).
+
+    rng: uint32 [6, n_rows*W] planar XORWOW state, advanced in place.
+    Returns (accum [n_rows*W, 4] float32, stats dict, normal or None, depth or None).
+    """
+    objs = np.ascontiguousarray(objs)
+    cam = np.ascontiguousarray(cam)
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    W = int(cam["width"])
+    npix = rows.size * W
+    assert rng.dtype == np.uint32 and rng.shape == (6, npix) and rng.flags.c_contiguous
+    if accum is None:
+        accum = np.zeros((npix, 4), dtype=np.float32)
+    normal = np.zeros((npix, 3), dtype=np.float32) if want_aux else None
+    depth = np.zeros(npix, dtype=np.float32) if want_aux else None
+    stats = np.zeros(5, dtype=np.uint64)
+    env_ptr = _ptr(env.rgba) if env is not None else None
+    ew, eh, ec = (env.width, env.height, env.valid_cols) if env is not None else (1, 1, 0)
+    rc = lib().or_render(_ptr(objs), len(objs), _ptr(cam), env_ptr, ew, eh, ec, _ptr(rows), rows.size, spp,
+                         max_depth, _ptr(rng), _ptr(accum), _ptr(normal), _ptr(depth), _ptr(stats),
+                         1 if accumulate else 0, threads)
+    if rc != 0:
+        raise ValueError(f"or_render failed: {rc}")
+    st = dict(zip(("segments", "nodes", "prims", "hits", "misses"), (int(x) for x in stats)))
+    return accum, st, normal, depth

@@ -1,0 +1,1117 @@
+// cpt_oracle.cpp — TEST INFRASTRUCTURE ONLY (the parity checker / CPU baseline).
+//
+// Scalar C++ restatement of DearPoca/CppPathTracer's per-pixel Monte-Carlo integrator
+// (reference @ /root/reference).  Only tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg may load this library.  The product (cpppathtracer_amd/, libcpt.so)
+// never includes, links or calls anything under oracle/.
+//
+// Parity status:
+//   * The reference ships no tests, fixtures or golden vectors and
+//     cannot be compiled here (CUDA 11.7 + cuRAND + OpenCV + Win32).  Pinned in-container:
+//       - XORWOW transition and the 2^67 subsequence jump: checked against rocRAND's
+//         precomputed tables (tests/test_oracle_rng.py);
+//       - the sky texture bytes (PIL decode == lossless PNG decode, tools/make_sky_fixture.py).
+//     UNPINNED (no reference artefact exists): cuRAND's curand_init salts/multipliers and
+//     uniform mapping (recalled from the public curand_kernel.h), CUDA libdevice
+//     transcendental rounding, NVIDIA TMU bilinear weight quantisation.  These are defined
+//     here as documented deterministic choices and the HIP path must match them bit-exactly.
+//
+// Build: see oracle/Makefile (g++ -O2 -ffp-contract=off; no fast-math, no FMA contraction).
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------------------------------
+// Reference POD layouts (restated; byte offsets checked by static_asserts and by tests).
+// ---------------------------------------------------------------------------------------
+struct f3 { float x, y, z; };                                   // CUDA float3, 12 B
+
+struct Material {                                               // material.h:17-35 (40 B)
+    int32_t type;            // MaterialType::Enum  @0
+    uint8_t have_tex;        // bool                @4
+    uint8_t pad_[3];
+    union { f3 kd; uint64_t tex; } u;  //           @8 (16 B, align 8)
+    float refractive_index;  //                     @24
+    float emit_intensity;    //                     @28
+    float smoothness;        //                     @32
+    float reflectivity;      //                     @36
+};
+static_assert(sizeof(Material) == 40, "Material layout");
+
+struct Object {                                                 // object.h:17-32 (72 B)
+    int32_t type;            // PrimitiveType::Enum @0
+    int32_t pad_;
+    Material material;       //                     @8
+    f3 center;               //                     @48
+    float radius;            //                     @60
+    float y_pos;             //                     @64
+    float height;            //                     @68
+};
+static_assert(sizeof(Object) == 72, "Object layout");
+
+struct Camera {                                                 // motional_camera.h:8-24 (136 B)
+    f3 vup;                  // @0
+    int32_t width, height;   // @12, @16
+    uint32_t cur_sample_idx; // @20
+    f3 origin, look_at;      // @24, @36
+    float view_fov, dist_to_focus, lens_radius, move_speed;  // @48..@60
+    f3 u, v, w;              // @64, @76, @88
+    f3 top_left, horizontal, vertical;                       // @100, @112, @124
+};
+static_assert(sizeof(Camera) == 136, "MotionalCamera layout");
+
+enum { PRIM_SPHERE = 0, PRIM_PLATFORM = 1, PRIM_CYLINDER = 2 };          // object.h:7-15
+enum { MAT_DIFFUSE = 0, MAT_METAL = 1, MAT_MIRROR = 2, MAT_GLASS = 3 };  // material.h:5-15
+
+const float DEFAULT_RAY_TMAX = 1e30f;   // ray_tracing_common.h:11
+const float BOUNCE_RAY_TMIN = 2e-5f;    // ray_tracing_common.h:12
+const uint32_t MAX_RECURSION_DEPTH_SET = 32;  // path_tracer.h:13
+const double REF_PI = 3.14159265358979323846;  // ray_tracing_math.hpp:11-13 (M_PI, double)
+
+// MIN/MAX/ABS are ternary macros in the reference (ray_tracing_math.hpp:15-26): NaN-sensitive.
+inline float MIN_(float a, float b) { return a < b ? a : b; }
+inline float MAX_(float a, float b) { return a > b ? a : b; }
+inline float ABS_(float a) { return a >= 0 ? a : -a; }
+
+// ---------------------------------------------------------------------------------------
+// helper_math.h host-path semantics (Common/helper_math.h, lines cited per op).
+// ---------------------------------------------------------------------------------------
+inline f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+inline f3 mk1(float s) { return f3{s, s, s}; }                                  // :135-138
+inline f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+inline f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+inline f3 mul(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+inline f3 mul(float s, f3 a) { return mk(s * a.x, s * a.y, s * a.z); }          // :834-837
+inline f3 mul(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+inline f3 divs(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }         // :1013-1016
+inline f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
+inline float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }      // :1264-1267
+inline float length(f3 v) { return sqrtf(dot(v, v)); }                          // :1307-1310
+inline f3 normalize(f3 v) { float inv = 1.0f / sqrtf(dot(v, v)); return mul(v, inv); }  // :1325-1329, host rsqrtf :78-81
+inline f3 cross(f3 a, f3 b) {                                                   // :1436-1439
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+inline f3 reflect(f3 i, f3 n) { return sub(i, mul(mul(2.0f, n), dot(n, i))); }   // :1427-1430
+
+// ---------------------------------------------------------------------------------------
+// Deterministic transcendentals ("detmath").  The reference calls CUDA libdevice pow / sinf /
+// cosf / asinf / atanf (material.cu:24-25,44-46,70,78,86,105; path_tracer.cu:119;
+// ray_tracing_math.hpp:68).  libdevice is not available, so the reference semantics are
+// defined here as: evaluate in double with these exact operation sequences (error well
+// under 1e-15 relative), then round as the C++ expression does.  The HIP kernels implement
+// the identical sequences; with FMA contraction off on both sides the results are equal
+// bit for bit.  Accuracy vs glibc is checked by tests/test_oracle_math.py.
+// ---------------------------------------------------------------------------------------
+inline uint64_t dbits(double x) { uint64_t u; std::memcpy(&u, &x, 8); return u; }
+inline double bitsd(uint64_t u) { double x; std::memcpy(&x, &u, 8); return x; }
+
+const double LN2_HI = 6.93147180369123816490e-01;   // 0x3fe62e42fee00000 (trailing zeros)
+const double LN2_LO = 1.90821492927058770002e-10;   // 0x3dea39ef35793c76
+const double INV_LN2 = 1.44269504088896338700e+00;
+const double SQRT2 = 1.41421356237309514547e+00;
+
+double dm_log(double x) {
+    if (!(x > 0.0)) {                       // x <= 0 or NaN
+        if (x == 0.0) return -INFINITY;
+        return NAN;
+    }
+    if (x == INFINITY) return INFINITY;
+    uint64_t u = dbits(x);
+    int e = (int)((u >> 52) & 0x7ff);
+    if (e == 0) {                           // subnormal: scale by 2^54
+        x = x * 18014398509481984.0;
+        u = dbits(x);
+        e = (int)((u >> 52) & 0x7ff) - 54;
+    }
+    e -= 1023;
+    double m = bitsd((u & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL);  // [1,2)
+    if (m > SQRT2) { m = m * 0.5; e += 1; }
+    double f = m - 1.0;
+    double s = f / (2.0 + f);
+    double s2 = s * s;
+    // 2*atanh(s) = 2s(1 + s2/3 + s2^2/5 + ...), |s| <= 0.1716, 12 terms
+    double p = 1.0 / 25.0;
+    p = 1.0 / 23.0 + s2 * p;
+    p = 1.0 / 21.0 + s2 * p;
+    p = 1.0 / 19.0 + s2 * p;
+    p = 1.0 / 17.0 + s2 * p;
+    p = 1.0 / 15.0 + s2 * p;
+    p = 1.0 / 13.0 + s2 * p;
+    p = 1.0 / 11.0 + s2 * p;
+    p = 1.0 / 9.0 + s2 * p;
+    p = 1.0 / 7.0 + s2 * p;
+    p = 1.0 / 5.0 + s2 * p;
+    p = 1.0 / 3.0 + s2 * p;
+    double r = 2.0 * s + 2.0 * s * (s2 * p);
+    double de = (double)e;
+    return de * LN2_HI + (r + de * LN2_LO);
+}
+
+double dm_ldexp(double x, int k) {
+    // x in [0.5, 2], k in [-1100, 1100]; two-step scaling keeps every step exact until the
+    // final (possibly subnormal) multiply.
+    if (k > 1023) { x = x * bitsd(0x7fe0000000000000ULL); k -= 1023; if (k > 1023) k = 1023; }
+    if (k < -1022) { x = x * bitsd(0x0010000000000000ULL); k += 1022; if (k < -1022) k = -1022; }
+    return x * bitsd((uint64_t)(k + 1023) << 52);
+}
+
+double dm_exp(double x) {
+    if (x != x) return x;
+    if (x > 709.782712893384) return INFINITY;
+    if (x < -745.1332191019412) return 0.0;
+    double k = floor(x * INV_LN2 + 0.5);
+    double r = (x - k * LN2_HI) - k * LN2_LO;   // |r| <= 0.3466
+    // Taylor to r^13
+    double p = 1.0 / 6227020800.0;              // 1/13!
+    p = 1.0 / 479001600.0 + r * p;              // 1/12!
+    p = 1.0 / 39916800.0 + r * p;
+    p = 1.0 / 3628800.0 + r * p;
+    p = 1.0 / 362880.0 + r * p;
+    p = 1.0 / 40320.0 + r * p;
+    p = 1.0 / 5040.0 + r * p;
+    p = 1.0 / 720.0 + r * p;
+    p = 1.0 / 120.0 + r * p;
+    p = 1.0 / 24.0 + r * p;
+    p = 1.0 / 6.0 + r * p;
+    p = 0.5 + r * p;
+    p = 1.0 + r * p;
+    p = 1.0 + r * p;
+    return dm_ldexp(p, (int)k);
+}
+
+// pow(double, double) with the C99 special cases the integrator can reach.
+double dm_pow(double x, double y) {
+    if (y == 0.0) return 1.0;
+    if (x == 1.0) return 1.0;
+    if (x != x || y != y) return NAN;
+    if (x == 0.0) return y > 0.0 ? 0.0 : INFINITY;
+    if (x < 0.0) {
+        double yi = floor(y);
+        if (yi != y) return NAN;
+        double m = dm_exp(y * dm_log(-x));
+        double half = y * 0.5;
+        return (floor(half) != half) ? -m : m;   // odd integer exponent keeps the sign
+    }
+    if (x == INFINITY) return y > 0.0 ? INFINITY : 0.0;
+    return dm_exp(y * dm_log(x));
+}
+
+float dm_powf(float x, float y) { return (float)dm_pow((double)x, (double)y); }
+
+// pi/2 split (fdlibm constants): PIO2_1 has 33 significant bits.
+const double PIO2_1 = 1.57079632673412561417e+00;
+const double PIO2_2 = 6.07710050650619224932e-11;
+const double PIO2_3 = 2.02226624879595063154e-21;
+const double TWO_OVER_PI = 6.36619772367581382433e-01;
+
+double dm_sin_poly(double r) {   // |r| <= pi/4, Taylor to r^19
+    double r2 = r * r;
+    double p = -1.0 / 121645100408832000.0;     // -1/19!
+    p = 1.0 / 355687428096000.0 + r2 * p;       // 1/17!
+    p = -1.0 / 1307674368000.0 + r2 * p;        // -1/15!
+    p = 1.0 / 6227020800.0 + r2 * p;            // 1/13!
+    p = -1.0 / 39916800.0 + r2 * p;             // -1/11!
+    p = 1.0 / 362880.0 + r2 * p;
+    p = -1.0 / 5040.0 + r2 * p;
+    p = 1.0 / 120.0 + r2 * p;
+    p = -1.0 / 6.0 + r2 * p;
+    return r + r * (r2 * p);
+}
+
+double dm_cos_poly(double r) {   // |r| <= pi/4, Taylor to r^20
+    double r2 = r * r;
+    double p = 1.0 / 2432902008176640000.0;     // 1/20!
+    p = -1.0 / 6402373705728000.0 + r2 * p;     // -1/18!
+    p = 1.0 / 20922789888000.0 + r2 * p;        // 1/16!
+    p = -1.0 / 87178291200.0 + r2 * p;          // -1/14!
+    p = 1.0 / 479001600.0 + r2 * p;             // 1/12!
+    p = -1.0 / 3628800.0 + r2 * p;
+    p = 1.0 / 40320.0 + r2 * p;
+    p = -1.0 / 720.0 + r2 * p;
+    p = 1.0 / 24.0 + r2 * p;
+    p = -0.5 + r2 * p;
+    return 1.0 + r2 * p;
+}
+
+// Shared range reduction; returns quadrant in *q.
+double dm_reduce(double x, int* q) {
+    double k = floor(x * TWO_OVER_PI + 0.5);
+    double r = ((x - k * PIO2_1) - k * PIO2_2) - k * PIO2_3;
+    double km = k - 4.0 * floor(k * 0.25);     // k mod 4 in [0,4)
+    *q = (int)km;
+    return r;
+}
+
+float dm_sinf(float xf) {
+    double x = (double)xf;
+    if (x != x || x == INFINITY || x == -INFINITY) return NAN;
+    int q;
+    double r = dm_reduce(x, &q);
+    double s;
+    switch (q) {
+        case 0: s = dm_sin_poly(r); break;
+        case 1: s = dm_cos_poly(r); break;
+        case 2: s = -dm_sin_poly(r); break;
+        default: s = -dm_cos_poly(r); break;
+    }
+    return (float)s;
+}
+
+float dm_cosf(float xf) {
+    double x = (double)xf;
+    if (x != x || x == INFINITY || x == -INFINITY) return NAN;
+    int q;
+    double r = dm_reduce(x, &q);
+    double c;
+    switch (q) {
+        case 0: c = dm_cos_poly(r); break;
+        case 1: c = -dm_sin_poly(r); break;
+        case 2: c = -dm_cos_poly(r); break;
+        default: c = dm_sin_poly(r); break;
+    }
+    return (float)c;
+}
+
+const double PI_2_D = 1.57079632679489655800e+00;  // pi/2 rounded to double
+
+double dm_atan(double t) {
+    if (t != t) return t;
+    double sgn = 1.0;
+    double a = t;
+    if (a < 0.0) { a = -a; sgn = -1.0; }
+    if (a == INFINITY) return sgn * PI_2_D;
+    bool inv = false;
+    if (a > 1.0) { a = 1.0 / a; inv = true; }
+    // two argument halvings: atan(a) = 2 atan(a / (1 + sqrt(1 + a^2)))
+    a = a / (1.0 + sqrt(1.0 + a * a));
+    a = a / (1.0 + sqrt(1.0 + a * a));       // a <= tan(pi/16) ~ 0.1989
+    double a2 = a * a;
+    double p = -1.0 / 27.0;
+    p = 1.0 / 25.0 + a2 * p;
+    p = -1.0 / 23.0 + a2 * p;
+    p = 1.0 / 21.0 + a2 * p;
+    p = -1.0 / 19.0 + a2 * p;
+    p = 1.0 / 17.0 + a2 * p;
+    p = -1.0 / 15.0 + a2 * p;
+    p = 1.0 / 13.0 + a2 * p;
+    p = -1.0 / 11.0 + a2 * p;
+    p = 1.0 / 9.0 + a2 * p;
+    p = -1.0 / 7.0 + a2 * p;
+    p = 1.0 / 5.0 + a2 * p;
+    p = -1.0 / 3.0 + a2 * p;
+    double r = 4.0 * (a + a * (a2 * p));
+    if (inv) r = PI_2_D - r;
+    return sgn * r;
+}
+
+float dm_atanf(float x) { return (float)dm_atan((double)x); }
+
+float dm_asinf(float xf) {
+    double x = (double)xf;
+    if (x != x) return NAN;
+    if (x > 1.0 || x < -1.0) return NAN;
+    if (x == 1.0) return (float)PI_2_D;
+    if (x == -1.0) return (float)(-PI_2_D);
+    return (float)dm_atan(x / sqrt((1.0 - x) * (1.0 + x)));
+}
+
+// ---------------------------------------------------------------------------------------
+// cuRAND XORWOW restatement (ray_tracing_math.hpp:82-104 call sites; the algorithm lives in
+// CUDA 11.7 curand_kernel.h, not present here).  State: v[5], d.  Layout in this library's
+// buffers is planar [6][npix]: v0..v4, d.
+// ---------------------------------------------------------------------------------------
+struct Xorwow { uint32_t v[5]; uint32_t d; };
+
+inline uint32_t xorwow_next(Xorwow& s) {                       // curand(): xorshift + Weyl
+    uint32_t t = s.v[0] ^ (s.v[0] >> 2);
+    s.v[0] = s.v[1]; s.v[1] = s.v[2]; s.v[2] = s.v[3]; s.v[3] = s.v[4];
+    s.v[4] = (s.v[4] ^ (s.v[4] << 4)) ^ (t ^ (t << 1));
+    s.d += 362437u;
+    return s.v[4] + s.d;
+}
+
+// curand_uniform: x * CURAND_2POW32_INV + CURAND_2POW32_INV/2, in (0, 1].
+// 2.3283064e-10f rounds to exactly 2^-32, so the product is exact and FMA contraction
+// (nvcc default) cannot change the result.
+inline float uniform(Xorwow& s) {
+    uint32_t x = xorwow_next(s);
+    return (float)x * 2.3283064e-10f + (2.3283064e-10f / 2.0f);
+}
+
+// Linear part of one XORWOW step as a 160x160 GF(2) matrix stored column-wise in rocRAND's
+// layout m[(word*32 + bit)*5 + k] (rocrand_xorwow.h:51-65): column (word,bit) = A * e(word,bit).
+struct BitMat { uint32_t m[800]; };
+
+void matvec(const BitMat& M, const uint32_t in[5], uint32_t out[5]) {
+    uint32_t r[5] = {0, 0, 0, 0, 0};
+    for (int i = 0; i < 5; ++i)
+        for (int j = 0; j < 32; ++j)
+            if (in[i] & (1u << j))
+                for (int k = 0; k < 5; ++k) r[k] ^= M.m[(i * 32 + j) * 5 + k];
+    std::memcpy(out, r, sizeof(r));
+}
+
+BitMat matmul(const BitMat& A, const BitMat& B) {   // A*B
+    BitMat C;
+    for (int c = 0; c < 160; ++c) matvec(A, &B.m[c * 5], &C.m[c * 5]);
+    return C;
+}
+
+struct JumpTables {
+    BitMat seq[64];     // seq[t] = A^(2^67 * 2^t)
+};
+
+const JumpTables& jump_tables() {
+    static JumpTables* tbl = nullptr;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        tbl = new JumpTables;
+        BitMat A;
+        for (int c = 0; c < 160; ++c) {
+            Xorwow s{};
+            s.v[c / 32] = 1u << (c % 32);
+            xorwow_next(s);
+            std::memcpy(&A.m[c * 5], s.v, 20);
+        }
+        BitMat P = A;
+        for (int i = 0; i < 67; ++i) P = matmul(P, P);      // A^(2^67)
+        tbl->seq[0] = P;
+        for (int t = 1; t < 64; ++t) tbl->seq[t] = matmul(tbl->seq[t - 1], tbl->seq[t - 1]);
+    });
+    return *tbl;
+}
+
+// curand_init(seed, subsequence, offset=0, &state) — curand_kernel.h (CUDA 11.7)
+// _curand_init_scratch.  Salts / multipliers recalled from the public header (UNPINNED).
+Xorwow curand_init(uint64_t seed, uint64_t subsequence) {
+    uint32_t s0 = (uint32_t)seed ^ 0xaad26b49u;
+    uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+    uint32_t t0 = 1099087573u * s0;
+    uint32_t t1 = 2591861531u * s1;
+    Xorwow st;
+    st.d = 6615241u + t1 + t0;
+    st.v[0] = 123456789u + t0;
+    st.v[1] = 362436069u ^ t0;
+    st.v[2] = 521288629u + t1;
+    st.v[3] = 88675123u ^ t1;
+    st.v[4] = 5783321u + t0;
+    const JumpTables& J = jump_tables();
+    for (int t = 0; t < 64; ++t)
+        if ((subsequence >> t) & 1ull) matvec(J.seq[t], st.v, st.v);
+    // d unchanged: 2^67 * k steps of the Weyl sequence are 0 mod 2^32.
+    return st;
+}
+
+// ---------------------------------------------------------------------------------------
+// Environment texture: PocaTextureUtils::GetTexture2D (textures.cu:68-71) over the cudaArray
+// filled by AddTexByFile (textures.cu:14-62): uchar4, normalized coords, Mirror addressing,
+// Linear filter, NormalizedFloat read.  Only `valid_cols` columns hold data (textures.cu:32-33
+// copies width BYTES per row); the rest are read as 0 (UNPINNED: uninitialised in CUDA).
+// Bilinear weights are quantised to 1/256 with round-to-nearest (CUDA guide: 9-bit fixed
+// point, 8 fractional bits; rounding mode UNPINNED).
+// ---------------------------------------------------------------------------------------
+struct Env {
+    const uint8_t* rgba;   // valid_cols x h, row pitch valid_cols*4
+    int w, h, valid_cols;
+};
+
+inline int mirror_index(int i, int n) {
+    int period = 2 * n;
+    int m = i % period;
+    if (m < 0) m += period;
+    if (m >= n) m = period - 1 - m;
+    return m;
+}
+
+inline void texel(const Env& e, int i, int j, float out[3]) {
+    int x = mirror_index(i, e.w), y = mirror_index(j, e.h);
+    if (x >= e.valid_cols || e.rgba == nullptr) { out[0] = out[1] = out[2] = 0.0f; return; }
+    const uint8_t* p = e.rgba + ((size_t)y * e.valid_cols + x) * 4;
+    out[0] = (float)p[0] / 255.0f;
+    out[1] = (float)p[1] / 255.0f;
+    out[2] = (float)p[2] / 255.0f;
+}
+
+f3 tex2d(const Env& e, float u, float v) {
+    float x = u * (float)e.w - 0.5f;
+    float y = v * (float)e.h - 0.5f;
+    if (!(x > -1e7f && x < 1e7f && y > -1e7f && y < 1e7f)) return mk1(0.0f);  // NaN/huge guard
+    float fx = floorf(x), fy = floorf(y);
+    float a = floorf((x - fx) * 256.0f + 0.5f) * 0.00390625f;
+    float b = floorf((y - fy) * 256.0f + 0.5f) * 0.00390625f;
+    int i0 = (int)fx, j0 = (int)fy;
+    float t00[3], t10[3], t01[3], t11[3];
+    texel(e, i0, j0, t00);
+    texel(e, i0 + 1, j0, t10);
+    texel(e, i0, j0 + 1, t01);
+    texel(e, i0 + 1, j0 + 1, t11);
+    float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    float r[3];
+    for (int c = 0; c < 3; ++c) r[c] = ((w00 * t00[c] + w10 * t10[c]) + w01 * t01[c]) + w11 * t11[c];
+    return mk(r[0], r[1], r[2]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Scene BVH — SceneBVH::Divide / BuildBVHInCpu (bvh.cu:31-95), node = bvh.h:32-38.
+// ---------------------------------------------------------------------------------------
+struct Node {
+    f3 bmin, bmax;
+    bool is_object;
+    int left, right;
+    int obj;          // index into the object array (the reference stores a by-value copy)
+};
+
+f3 aabb_max(const Object& o) {                                  // object.cu:134-151
+    float tol = BOUNCE_RAY_TMIN * 5.f;
+    switch (o.type) {
+        case PRIM_SPHERE: return add(o.center, mk1(ABS_(o.radius)));
+        case PRIM_PLATFORM: return mk(DEFAULT_RAY_TMAX * 5, o.y_pos + tol, DEFAULT_RAY_TMAX * 5);
+        case PRIM_CYLINDER:
+            return mk(o.center.x + ABS_(o.radius), o.center.y + o.height / 2 + tol, o.center.z + ABS_(o.radius));
+        default: return mk1(0.0f);   // reference: uninitialised
+    }
+}
+
+f3 aabb_min(const Object& o) {                                  // object.cu:153-170
+    float tol = BOUNCE_RAY_TMIN * 5.f;
+    switch (o.type) {
+        case PRIM_SPHERE: return sub(o.center, mk1(ABS_(o.radius)));
+        case PRIM_PLATFORM: return mk(-DEFAULT_RAY_TMAX * 5, o.y_pos - tol, -DEFAULT_RAY_TMAX * 5);
+        case PRIM_CYLINDER:
+            return mk(o.center.x - ABS_(o.radius), o.center.y - o.height / 2 - tol, o.center.z - ABS_(o.radius));
+        default: return mk1(0.0f);
+    }
+}
+
+struct Bvh {
+    std::vector<Node> nodes;
+    const Object* objs;
+};
+
+// std::sort in the reference (bvh.cu:67-80) is unstable; ties between equal centroids are
+// implementation-defined.  The restatement uses stable_sort (documented tie rule; the test
+// scenes have no centroid ties).
+int divide(Bvh& bvh, std::vector<int>& idx, int l, int r) {      // bvh.cu:31-90
+    if (l >= r) return -1;
+    int ret = (int)bvh.nodes.size();
+    bvh.nodes.push_back(Node{});
+    const Object* O = bvh.objs;
+    f3 lmin = aabb_min(O[idx[l]]), lmax = aabb_max(O[idx[l]]);
+    if (l == r - 1) {
+        Node& n = bvh.nodes[ret];
+        n.left = n.right = -1;
+        n.bmin = lmin; n.bmax = lmax;
+        n.is_object = true;
+        n.obj = idx[l];
+        return ret;
+    }
+    float minx = lmin.x, miny = lmin.y, minz = lmin.z;
+    float maxx = lmax.x, maxy = lmax.y, maxz = lmax.z;
+    for (int i = l + 1; i < r; ++i) {
+        f3 cmin = aabb_min(O[idx[i]]), cmax = aabb_max(O[idx[i]]);
+        minx = MIN_(minx, cmin.x); miny = MIN_(miny, cmin.y); minz = MIN_(minz, cmin.z);
+        maxx = MAX_(maxx, cmax.x); maxy = MAX_(maxy, cmax.y); maxz = MAX_(maxz, cmax.z);
+    }
+    float span_x = maxx - minx, span_y = maxy - miny, span_z = maxz - minz;
+    int axis = (span_x >= span_y && span_x >= span_z) ? 0 : (span_y >= span_z ? 1 : 2);
+    auto centroid = [&](int k) {
+        f3 a = aabb_min(O[k]), b = aabb_max(O[k]);
+        float lo = axis == 0 ? a.x : axis == 1 ? a.y : a.z;
+        float hi = axis == 0 ? b.x : axis == 1 ? b.y : b.z;
+        return (lo + hi) / 2;
+    };
+    std::stable_sort(idx.begin() + l, idx.begin() + r, [&](int a, int b) { return centroid(a) < centroid(b); });
+    int mid = (l + r) / 2;
+    int left = divide(bvh, idx, l, mid);
+    int right = divide(bvh, idx, mid, r);
+    Node& n = bvh.nodes[ret];
+    n.left = left; n.right = right;
+    n.bmin = mk(minx, miny, minz);
+    n.bmax = mk(maxx, maxy, maxz);
+    n.is_object = false;
+    n.obj = -1;
+    return ret;
+}
+
+void build_bvh(Bvh& bvh, const Object* objs, int n) {
+    bvh.objs = objs;
+    bvh.nodes.clear();
+    std::vector<int> idx(n);
+    for (int i = 0; i < n; ++i) idx[i] = i;
+    divide(bvh, idx, 0, n);
+}
+
+// ---------------------------------------------------------------------------------------
+// Ray / intersection (ray_tracing_common.h:14-35, object.cu:10-128)
+// ---------------------------------------------------------------------------------------
+struct Ray { f3 origin, dir; float tmin, tmax; };
+struct Attr { f3 normal, hit_pos; };
+
+bool sphere_test(const Object& s, Ray& ray, Attr& attr) {        // object.cu:10-35
+    f3 A_C = sub(ray.origin, s.center);
+    f3 B = ray.dir;
+    float a = dot(B, B);
+    float b = dot(A_C, B);
+    float c = dot(A_C, A_C) - s.radius * s.radius;
+    float disc = b * b - a * c;
+    if (disc > 0) {
+        float temp = (-b - sqrtf(disc)) / a;
+        if (temp < ray.tmax && temp > ray.tmin) {
+            ray.tmax = temp;
+            attr.hit_pos = add(ray.origin, mul(temp, ray.dir));
+            f3 normal = sub(attr.hit_pos, s.center);
+            attr.normal = divs(normal, s.radius);
+            return true;
+        }
+        temp = (-b + sqrtf(disc)) / a;
+        if (temp < ray.tmax && temp > ray.tmin) {
+            ray.tmax = temp;
+            attr.hit_pos = add(ray.origin, mul(temp, ray.dir));
+            attr.normal = normalize(sub(attr.hit_pos, s.center));
+            return true;
+        }
+    }
+    return false;
+}
+
+bool platform_test(const Object& p, Ray& ray, Attr& attr) {      // object.cu:37-48
+    if ((ray.origin.y < p.y_pos && ray.dir.y > 0.f) || (ray.origin.y > p.y_pos && ray.dir.y < 0.f)) {
+        float temp = (p.y_pos - ray.origin.y) / ray.dir.y;
+        if (temp < ray.tmax && temp > ray.tmin) {
+            ray.tmax = temp;
+            attr.hit_pos = add(ray.origin, mul(temp, ray.dir));
+            attr.normal = normalize(mk(0, -ray.dir.y, 0));
+            return true;
+        }
+    }
+    return false;
+}
+
+bool cap_test(const Object& cy, Ray& ray, Attr& attr, float ypos) {  // object.cu:52-77 (one cap)
+    if ((ray.origin.y < ypos && ray.dir.y > 0.f) || (ray.origin.y > ypos && ray.dir.y < 0.f)) {
+        float temp = (ypos - ray.origin.y) / ray.dir.y;
+        f3 hit_pos = add(ray.origin, mul(temp, ray.dir));
+        if (temp < ray.tmax && temp > ray.tmin &&
+            sqrtf((hit_pos.x - cy.center.x) * (hit_pos.x - cy.center.x) +
+                  (hit_pos.z - cy.center.z) * (hit_pos.z - cy.center.z)) < cy.radius) {
+            ray.tmax = temp;
+            attr.hit_pos = hit_pos;
+            attr.normal = normalize(mk(0, -ray.dir.y, 0));
+            return true;
+        }
+    }
+    return false;
+}
+
+bool cylinder_test(const Object& cy, Ray& ray, Attr& attr) {     // object.cu:50-112
+    bool ret = false;
+    float upper = cy.center.y + cy.height / 2;
+    if (cap_test(cy, ray, attr, upper)) ret = true;
+    float lower = cy.center.y - cy.height / 2;
+    if (cap_test(cy, ray, attr, lower)) ret = true;
+    float dx = ray.dir.x, dz = ray.dir.z, r = cy.radius;
+    float cx = ray.origin.x - cy.center.x;
+    float cz = ray.origin.z - cy.center.z;
+    float a = dx * dx + dz * dz;
+    float b = cx * dx + cz * dz;
+    float c = cx * cx + cz * cz - r * r;
+    float disc = b * b - a * c;
+    if (disc > 0.f) {
+        float temp = (-b - sqrtf(disc)) / a;
+        f3 hit_pos = add(ray.origin, mul(temp, ray.dir));
+        if (temp < ray.tmax && temp > ray.tmin && hit_pos.y > lower && hit_pos.y < upper) {
+            ray.tmax = temp;
+            attr.hit_pos = hit_pos;
+            attr.normal = normalize(mk(hit_pos.x - cy.center.x, 0.f, hit_pos.z - cy.center.z));
+            ret = true;
+        }
+        temp = (-b + sqrtf(disc)) / a;
+        hit_pos = add(ray.origin, mul(temp, ray.dir));
+        if (temp < ray.tmax && temp > ray.tmin && hit_pos.y > lower && hit_pos.y < upper) {
+            ray.tmax = temp;
+            attr.hit_pos = hit_pos;
+            attr.normal = normalize(mk(hit_pos.x - cy.center.x, 0.f, hit_pos.z - cy.center.z));
+            ret = true;
+        }
+    }
+    return ret;
+}
+
+bool intersection_test(const Object& o, Ray& ray, Attr& attr) {  // object.cu:114-128
+    switch (o.type) {
+        case PRIM_SPHERE: return sphere_test(o, ray, attr);
+        case PRIM_PLATFORM: return platform_test(o, ray, attr);
+        case PRIM_CYLINDER: return cylinder_test(o, ray, attr);
+        default: return false;
+    }
+}
+
+struct Stats { uint64_t segments, nodes, prims, hits, misses; };
+
+// SceneBVH::TraceRay (bvh.cu:167-205): DFS, explicit stack, leaf test before slab test,
+// left pushed before right (right popped first), ray taken BY VALUE.
+bool trace_ray(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st) {
+    if (bvh.nodes.empty()) return false;
+    int stack[512];
+    int top = 0;
+    stack[top++] = 0;
+    bool ret = false;
+    while (top > 0) {
+        int ni = stack[--top];
+        if (ni == -1) continue;
+        const Node& n = bvh.nodes[ni];
+        st.nodes++;
+        if (n.is_object) {
+            st.prims++;
+            if (intersection_test(bvh.objs[n.obj], ray, attr)) { hit_obj = n.obj; ret = true; }
+        }
+        float local_tmin = -DEFAULT_RAY_TMAX * 2, local_tmax = DEFAULT_RAY_TMAX * 2;
+        if (ray.dir.x != 0.f) {
+            float t0 = (n.bmin.x - ray.origin.x) / ray.dir.x;
+            float t1 = (n.bmax.x - ray.origin.x) / ray.dir.x;
+            local_tmin = MAX_(local_tmin, MIN_(t0, t1));
+            local_tmax = MIN_(local_tmax, MAX_(t0, t1));
+        }
+        if (ray.dir.y != 0.f) {
+            float t0 = (n.bmin.y - ray.origin.y) / ray.dir.y;
+            float t1 = (n.bmax.y - ray.origin.y) / ray.dir.y;
+            local_tmin = MAX_(local_tmin, MIN_(t0, t1));
+            local_tmax = MIN_(local_tmax, MAX_(t0, t1));
+        }
+        if (ray.dir.z != 0.f) {
+            float t0 = (n.bmin.z - ray.origin.z) / ray.dir.z;
+            float t1 = (n.bmax.z - ray.origin.z) / ray.dir.z;
+            local_tmin = MAX_(local_tmin, MIN_(t0, t1));
+            local_tmax = MIN_(local_tmax, MAX_(t0, t1));
+        }
+        if (local_tmin > local_tmax || local_tmin > ray.tmax || local_tmax < ray.tmin) continue;
+        if (top + 2 > 512) return ret;   // reference would overflow; unreachable for sane trees
+        stack[top++] = n.left;
+        stack[top++] = n.right;
+    }
+    return ret;
+}
+
+// ---------------------------------------------------------------------------------------
+// Shading (material.cu).  Payload mirrors RayPayload (ray_tracing_common.h:21-30).
+// ---------------------------------------------------------------------------------------
+struct Payload {
+    Ray ray;
+    f3 radiance, attenuation, hit_pos, bounce_dir;
+    uint32_t depth;
+};
+
+// to_world (ray_tracing_math.hpp:51-63)
+f3 to_world(f3 a, f3 N) {
+    f3 B, C;
+    if (fabsf(N.x) > fabsf(N.y)) {
+        float invLen = 1.0f / sqrtf(N.x * N.x + N.z * N.z);
+        C = mk(N.z * invLen, 0.0f, -N.x * invLen);
+    } else {
+        float invLen = 1.0f / sqrtf(N.y * N.y + N.z * N.z);
+        C = mk(0.f, N.z * invLen, -N.y * invLen);
+    }
+    B = cross(C, N);
+    return add(add(mul(a.x, B), mul(a.y, C)), mul(a.z, N));
+}
+
+// schlick (ray_tracing_math.hpp:65-69).  pow(float, int) resolves to CUDA's float overload
+// in device code (UNPINNED: ISO C++ would promote to double).
+float schlick(float cosine, float ref_idx) {
+    float r0 = (1 - ref_idx) / (1 + ref_idx);
+    r0 *= r0;
+    return r0 + (1 - r0) * dm_powf(1 - cosine, 5.0f);
+}
+
+// refract (ray_tracing_math.hpp:71-80): discriminant in double (1.0 literal), stored float.
+bool refract(f3 v, f3 n, float ni_over_nt, f3& refracted) {
+    f3 uv = normalize(v);
+    float dt = dot(uv, n);
+    float discriminant = (float)(1.0 - (double)(ni_over_nt * ni_over_nt * (1 - dt * dt)));
+    if (discriminant > 0) {
+        refracted = normalize(sub(mul(ni_over_nt, sub(uv, mul(n, dt))), mul(n, sqrtf(discriminant))));
+        return true;
+    }
+    return false;
+}
+
+// Shared lobe: z = pow(x1, 1/alpha) (double pow), r = sqrtf(1 - z^2), phi = 2*M_PI*x2 (double).
+inline f3 lobe(float x_1, float x_2, double inv_alpha) {
+    float z = (float)dm_pow((double)x_1, inv_alpha);
+    float r = sqrtf(1.0f - z * z);
+    float phi = (float)(2 * REF_PI * (double)x_2);
+    return mk(r * dm_cosf(phi), r * dm_sinf(phi), z);
+}
+
+void diffuse_shader(const Material& m, Payload& p, f3 position, f3 normal, f3 in_ray_dir, Xorwow& rng) {  // :20-38
+    (void)in_ray_dir;
+    float x_1 = uniform(rng), x_2 = uniform(rng);
+    f3 localRay = lobe(x_1, x_2, 1.0 / 2);
+    p.bounce_dir = to_world(localRay, normal);
+    float cosalpha = dot(normal, p.bounce_dir);
+    p.attenuation = cosalpha > 0.0f ? m.u.kd : mk(0.0f, 0.0f, 0.0f);
+    p.radiance = mul(m.emit_intensity, m.u.kd);
+    p.hit_pos = position;
+}
+
+void mirror_shader(const Material& m, Payload& p, f3 position, f3 normal, f3 in_ray_dir, Xorwow& rng) {  // :40-64
+    float s = m.smoothness;
+    float alpha = dm_powf(1000.0f, s);
+    float x_1 = uniform(rng), x_2 = uniform(rng);
+    f3 localRay = lobe(x_1, x_2, 1.0 / (double)alpha);
+    f3 reflect_dir = reflect(in_ray_dir, normal);
+    f3 wo = to_world(localRay, reflect_dir);
+    float cosalpha = dot(normal, wo);
+    p.attenuation = cosalpha > 0.0f ? m.u.kd : mk(0.0f, 0.0f, 0.0f);
+    p.bounce_dir = wo;
+    p.radiance = mul(m.emit_intensity, m.u.kd);
+    p.hit_pos = position;
+}
+
+void metal_shader(const Material& m, Payload& p, f3 position, f3 normal, f3 in_ray_dir, Xorwow& rng) {  // :66-99
+    float x_1 = uniform(rng), x_2 = uniform(rng);
+    float s = m.smoothness;
+    float alpha = dm_powf(1000.0f, s);
+    float reflectivity = m.reflectivity;
+    if (uniform(rng) < reflectivity) {
+        f3 localRay = lobe(x_1, x_2, 1.0 / (double)alpha);
+        p.bounce_dir = to_world(localRay, reflect(in_ray_dir, normal));
+    } else {
+        f3 localRay = lobe(x_1, x_2, 1.0 / 2.0);
+        p.bounce_dir = to_world(localRay, normal);
+    }
+    p.attenuation = dot(p.bounce_dir, normal) < 0 ? mk(0.0f, 0.0f, 0.0f) : m.u.kd;
+    p.radiance = mul(m.emit_intensity, m.u.kd);
+    p.hit_pos = position;
+}
+
+void glass_shader(const Material& m, Payload& p, f3 position, f3 normal, f3 in_ray_dir, Xorwow& rng) {  // :101-143
+    float x_1 = uniform(rng), x_2 = uniform(rng);
+    float alpha = dm_powf(1000.0f, m.smoothness);
+    f3 localRay = lobe(x_1, x_2, 1.0 / (double)alpha);
+    f3 outward_normal, refracted = mk1(0.0f);
+    float ni_over_nt, reflect_prob, cosine;
+    in_ray_dir = normalize(in_ray_dir);
+    if (dot(in_ray_dir, normal) > 0) {
+        outward_normal = neg(normal);
+        ni_over_nt = m.refractive_index;
+        cosine = dot(in_ray_dir, normal);
+        cosine = sqrtf(1 - m.refractive_index * m.refractive_index * (1 - cosine * cosine));
+    } else {
+        outward_normal = normal;
+        ni_over_nt = 1.f / m.refractive_index;
+        cosine = -dot(in_ray_dir, normal);
+    }
+    if (refract(in_ray_dir, outward_normal, ni_over_nt, refracted)) reflect_prob = schlick(cosine, m.refractive_index);
+    else reflect_prob = 1.0f;
+    if (uniform(rng) < reflect_prob) p.bounce_dir = to_world(localRay, reflect(in_ray_dir, normal));
+    else p.bounce_dir = to_world(localRay, refracted);
+    p.attenuation = m.u.kd;
+    p.radiance = mul(m.emit_intensity, m.u.kd);
+    p.hit_pos = position;
+}
+
+// Material::EvalAttenuationAndCreateRay (material.cu:145-163) — note the Metal/Mirror swap.
+void eval_material(const Material& m, Payload& p, f3 position, f3 normal, f3 in_ray_dir, Xorwow& rng) {
+    switch (m.type) {
+        case MAT_DIFFUSE: diffuse_shader(m, p, position, normal, in_ray_dir, rng); break;
+        case MAT_METAL: mirror_shader(m, p, position, normal, in_ray_dir, rng); break;
+        case MAT_MIRROR: metal_shader(m, p, position, normal, in_ray_dir, rng); break;
+        case MAT_GLASS: glass_shader(m, p, position, normal, in_ray_dir, rng); break;
+        default: diffuse_shader(m, p, position, normal, in_ray_dir, rng);
+    }
+}
+
+// Miss (path_tracer.cu:117-122)
+void miss(const Env& env, Payload& p) {
+    f3 d = normalize(p.ray.dir);
+    float v = (float)((double)dm_asinf(d.z) / REF_PI + 0.5);
+    float u = (float)((double)(dm_atanf(d.y / d.x) / 2) / REF_PI);
+    p.radiance = tex2d(env, u, v);
+    p.depth = MAX_RECURSION_DEPTH_SET;
+}
+
+// MotionalCamera::RayGen (motional_camera.cu:202-213); the three draws are taken left to
+// right (argument evaluation order of make_float3 is unspecified; nvcc evaluates L->R).
+Ray ray_gen(const Camera& c, int x, int y, Xorwow& rng) {
+    float r1 = uniform(rng), r2 = uniform(rng), r3 = uniform(rng);
+    f3 rd = mul(c.lens_radius, mk(r1, r2, r3));
+    f3 offset = add(mul(c.u, rd.x), mul(c.v, rd.y));
+    float dx = float(x) / float(c.width);
+    float dy = float(y) / float(c.height);
+    Ray ray;
+    ray.origin = add(c.origin, offset);
+    ray.dir = normalize(sub(sub(add(add(c.top_left, mul(dx, c.horizontal)), mul(dy, c.vertical)), c.origin), offset));
+    ray.tmin = 0.f;
+    ray.tmax = DEFAULT_RAY_TMAX;
+    return ray;
+}
+
+struct PassOut { f3 radiance, normal; float depth; };
+
+// SamplePixel body (path_tracer.cu:124-175) for one pixel and one pass.
+PassOut sample_pixel(const Bvh& bvh, const Env& env, const Camera& cam, uint32_t max_depth, int x, int y,
+                     Xorwow& rng, Stats& st) {
+    f3 radiance = mk1(0.f), normals = mk1(0.f);
+    float depth = 0.0f;
+    Payload p;
+    std::memset(&p, 0, sizeof(p));
+    p.ray = ray_gen(cam, x, y, rng);
+    f3 attenuation = mk1(1.f);
+    p.depth = 0;
+    bool first = false;
+    while (p.depth < max_depth) {
+        Attr attr;
+        std::memset(&attr, 0, sizeof(attr));
+        int hit_obj = -1;
+        st.segments++;
+        bool ret = trace_ray(bvh, p.ray, attr, hit_obj, st);
+        if (ret) {
+            st.hits++;
+            // Object::ClosetHit (object.cu:130-132)
+            eval_material(bvh.objs[hit_obj].material, p, attr.hit_pos, attr.normal, p.ray.dir, rng);
+        } else {
+            st.misses++;
+            attr.hit_pos = add(p.ray.origin, mul(DEFAULT_RAY_TMAX, p.ray.dir));
+            attr.normal = neg(p.ray.dir);
+            miss(env, p);
+        }
+        radiance = add(radiance, mul(attenuation, p.radiance));
+        attenuation = mul(attenuation, p.attenuation);
+        if (!first) {
+            normals = add(normals, attr.normal);
+            depth += p.ray.tmax;
+            first = true;
+        }
+        p.ray.origin = p.hit_pos;
+        p.ray.dir = normalize(p.bounce_dir);
+        p.ray.tmin = BOUNCE_RAY_TMIN;
+        p.ray.tmax = DEFAULT_RAY_TMAX;
+        p.depth++;
+    }
+    return PassOut{radiance, normals, depth};
+}
+
+struct RenderJob {
+    const Bvh* bvh;
+    Env env;
+    Camera cam;
+    const int32_t* rows;
+    int n_rows;
+    int spp;
+    uint32_t max_depth;
+    uint32_t* rng;      // planar [6][npix]
+    float* accum;       // [npix][4]
+    float* normal;      // [npix][3] or null
+    float* depthbuf;    // [npix] or null
+    int accumulate;
+};
+
+void render_rows(const RenderJob& J, int thread, int nthreads, Stats& st) {
+    const int W = J.cam.width;
+    const size_t npix = (size_t)J.n_rows * W;
+    for (int ri = thread; ri < J.n_rows; ri += nthreads) {
+        int y = J.rows[ri];
+        for (int x = 0; x < W; ++x) {
+            size_t pix = (size_t)ri * W + x;
+            Xorwow s;
+            for (int k = 0; k < 5; ++k) s.v[k] = J.rng[k * npix + pix];
+            s.d = J.rng[5 * npix + pix];
+            float* a = J.accum + pix * 4;
+            f3 sum = J.accumulate ? mk(a[0], a[1], a[2]) : mk1(0.0f);
+            float cnt = J.accumulate ? a[3] : 0.0f;
+            PassOut last{};
+            for (int sidx = 0; sidx < J.spp; ++sidx) {
+                last = sample_pixel(*J.bvh, J.env, J.cam, J.max_depth, x, y, s, st);
+                sum = add(sum, last.radiance);
+                cnt += 1.0f;
+            }
+            a[0] = sum.x; a[1] = sum.y; a[2] = sum.z; a[3] = cnt;
+            if (J.normal && J.spp > 0) {
+                J.normal[pix * 3 + 0] = last.normal.x;
+                J.normal[pix * 3 + 1] = last.normal.y;
+                J.normal[pix * 3 + 2] = last.normal.z;
+            }
+            if (J.depthbuf && J.spp > 0) J.depthbuf[pix] = last.depth;
+            for (int k = 0; k < 5; ++k) J.rng[k * npix + pix] = s.v[k];
+            J.rng[5 * npix + pix] = s.d;
+        }
+    }
+}
+
+}  // namespace
+
+// =======================================================================================
+// extern "C" surface for tests / bench cpu_baseline (ctypes).
+// =======================================================================================
+extern "C" {
+
+int or_abi_version(void) { return 1; }
+
+int or_sizeof(int which) {
+    switch (which) {
+        case 0: return (int)sizeof(Material);
+        case 1: return (int)sizeof(Object);
+        case 2: return (int)sizeof(Camera);
+        default: return -1;
+    }
+}
+
+// --- detmath KAT surface -------------------------------------------------------------
+double or_pow(double x, double y) { return dm_pow(x, y); }
+double or_log(double x) { return dm_log(x); }
+double or_exp(double x) { return dm_exp(x); }
+double or_atan(double x) { return dm_atan(x); }
+float or_powf(float x, float y) { return dm_powf(x, y); }
+float or_sinf(float x) { return dm_sinf(x); }
+float or_cosf(float x) { return dm_cosf(x); }
+float or_asinf(float x) { return dm_asinf(x); }
+float or_atanf(float x) { return dm_atanf(x); }
+
+// Vectorised forms (op: 0 powf(a,b) 1 sinf 2 cosf 3 asinf 4 atanf 5 pow(a,b) as float of double).
+void or_math_batch(int op, const float* a, const float* b, float* out, long n) {
+    for (long i = 0; i < n; ++i) {
+        switch (op) {
+            case 0: out[i] = dm_powf(a[i], b[i]); break;
+            case 1: out[i] = dm_sinf(a[i]); break;
+            case 2: out[i] = dm_cosf(a[i]); break;
+            case 3: out[i] = dm_asinf(a[i]); break;
+            case 4: out[i] = dm_atanf(a[i]); break;
+            case 5: out[i] = (float)dm_pow((double)a[i], 1.0 / (double)b[i]); break;
+            default: out[i] = NAN;
+        }
+    }
+}
+
+// --- RNG -------------------------------------------------------------------------------
+void or_curand_init(uint64_t seed, uint64_t subsequence, uint32_t out6[6]) {
+    Xorwow s = curand_init(seed, subsequence);
+    std::memcpy(out6, s.v, 20);
+    out6[5] = s.d;
+}
+
+uint32_t or_xorwow_next(uint32_t st6[6]) {
+    Xorwow s;
+    std::memcpy(s.v, st6, 20);
+    s.d = st6[5];
+    uint32_t r = xorwow_next(s);
+    std::memcpy(st6, s.v, 20);
+    st6[5] = s.d;
+    return r;
+}
+
+float or_uniform(uint32_t st6[6]) {
+    Xorwow s;
+    std::memcpy(s.v, st6, 20);
+    s.d = st6[5];
+    float r = uniform(s);
+    std::memcpy(st6, s.v, 20);
+    st6[5] = s.d;
+    return r;
+}
+
+// A^(2^67 * 4^t) in rocRAND layout (compare: h_xorwow_sequence_jump_matrices[t]).
+void or_seq_jump_matrix_pow4(int t, uint32_t out[800]) {
+    const JumpTables& J = jump_tables();
+    std::memcpy(out, J.seq[2 * t].m, sizeof(uint32_t) * 800);
+}
+
+// InitCuRand (path_tracer.cu:36-42): per pixel curand_init(seed, (x<<32)|y, 0).
+void or_init_rng(uint64_t seed, int width, const int32_t* rows, int n_rows, uint32_t* rng_planar, int nthreads) {
+    jump_tables();
+    const size_t npix = (size_t)n_rows * width;
+    if (nthreads < 1) nthreads = 1;
+    auto work = [&](int t) {
+        for (int ri = t; ri < n_rows; ri += nthreads)
+            for (int x = 0; x < width; ++x) {
+                Xorwow s = curand_init(seed, ((uint64_t)x << 32) | (uint64_t)(uint32_t)rows[ri]);
+                size_t pix = (size_t)ri * width + x;
+                for (int k = 0; k < 5; ++k) rng_planar[k * npix + pix] = s.v[k];
+                rng_planar[5 * npix + pix] = s.d;
+            }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+}
+
+// --- Camera ---------------------------------------------------------------------------
+// MotionalCamera::GetCopy (motional_camera.cu:177-200): basis + corner vectors; increments
+// cur_sample_idx.  theta uses the double M_PI; tan of a float resolves to tanf.
+void or_camera_get_copy(void* cam_inout) {
+    Camera& c = *reinterpret_cast<Camera*>(cam_inout);
+    float theta = (float)((double)c.view_fov * REF_PI / 180);
+    float aspect = float(c.width) / float(c.height);
+    float half_height = tanf(theta / 2);
+    float half_width = aspect * half_height;
+    c.w = normalize(sub(c.origin, c.look_at));
+    c.u = normalize(cross(c.vup, c.w));
+    c.v = cross(c.w, c.u);
+    c.dist_to_focus = length(sub(c.origin, c.look_at));
+    // top_left = origin - hw*d*u + hh*d*v - d*w, evaluated left to right:
+    c.top_left = sub(add(sub(c.origin, mul(half_width * c.dist_to_focus, c.u)), mul(half_height * c.dist_to_focus, c.v)),
+                     mul(c.dist_to_focus, c.w));
+    c.horizontal = mul(2 * half_width * c.dist_to_focus, c.u);
+    c.vertical = mul(-2 * half_height * c.dist_to_focus, c.v);
+    c.cur_sample_idx++;
+}
+
+// --- BVH (topology export for tests) ----------------------------------------------------
+// out: per node {bmin xyz, bmax xyz} floats (6) and {is_object, left, right, obj} ints (4).
+int or_build_bvh(const void* objs, int n, float* out_box, int32_t* out_link, int cap) {
+    Bvh b;
+    build_bvh(b, reinterpret_cast<const Object*>(objs), n);
+    int m = (int)b.nodes.size();
+    for (int i = 0; i < m && i < cap; ++i) {
+        const Node& nd = b.nodes[i];
+        float* bx = out_box + i * 6;
+        bx[0] = nd.bmin.x; bx[1] = nd.bmin.y; bx[2] = nd.bmin.z;
+        bx[3] = nd.bmax.x; bx[4] = nd.bmax.y; bx[5] = nd.bmax.z;
+        int32_t* l = out_link + i * 4;
+        l[0] = nd.is_object; l[1] = nd.left; l[2] = nd.right; l[3] = nd.obj;
+    }
+    return m;
+}
+
+// --- Integrator -------------------------------------------------------------------------
+// Renders `spp` passes of SamplePixel for every pixel of the given rows.  rng_planar is
+// [6][n_rows*W] (in/out), accum is [n_rows*W][4] rgb-sum + pass count (in/out when
+// accumulate != 0).  stats5 (optional) receives segments, node visits, primitive tests,
+// hits, misses.  Returns 0 on success.
+int or_render(const void* objs, int n_objs, const void* camera, const uint8_t* env_rgba, int env_w, int env_h,
+              int env_valid_cols, const int32_t* rows, int n_rows, int spp, int max_depth, uint32_t* rng_planar,
+              float* accum, float* normal_out, float* depth_out, uint64_t* stats5, int accumulate, int nthreads) {
+    if (max_depth < 0 || max_depth > (int)MAX_RECURSION_DEPTH_SET) return -1;
+    Bvh bvh;
+    build_bvh(bvh, reinterpret_cast<const Object*>(objs), n_objs);
+    RenderJob J;
+    J.bvh = &bvh;
+    J.env = Env{env_rgba, env_w, env_h, env_valid_cols};
+    std::memcpy(&J.cam, camera, sizeof(Camera));
+    J.rows = rows; J.n_rows = n_rows; J.spp = spp; J.max_depth = (uint32_t)max_depth;
+    J.rng = rng_planar; J.accum = accum; J.normal = normal_out; J.depthbuf = depth_out;
+    J.accumulate = accumulate;
+    if (nthreads < 1) nthreads = 1;
+    std::vector<Stats> st(nthreads, Stats{0, 0, 0, 0, 0});
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back([&, t] { render_rows(J, t, nthreads, st[t]); });
+    render_rows(J, 0, nthreads, st[0]);
+    for (auto& x : th) x.join();
+    if (stats5) {
+        Stats s{0, 0, 0, 0, 0};
+        for (auto& x : st) { s.segments += x.segments; s.nodes += x.nodes; s.prims += x.prims; s.hits += x.hits; s.misses += x.misses; }
+        stats5[0] = s.segments; stats5[1] = s.nodes; stats5[2] = s.prims; stats5[3] = s.hits; stats5[4] = s.misses;
+    }
+    return 0;
+}
+
+}  // extern "C"
