@@ -1,0 +1,244 @@
+"""Benchmark of the integrator hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4] [--spp S]
+
+One step = one full render of the configured workload (all `spp` SamplePixel passes for
+every pixel of the image; each pass continues the pixel's XORWOW stream, exactly like the
+reference's progressive passes) with inputs already resident in HBM, plus — for N > 1 — the
+RCCL gather of the fp32 framebuffer tiles into rank 0.  Multi-GPU: one process per GPU
+(torchrun), the image rows are dealt in interleaved 16-row blocks (row tiling, strong
+scaling: the total image is fixed).
+
+Rank 0 prints one JSON line with `roofline` (algorithmic bytes of SURVEY.md §8(d) ÷ the
+kernel's HIP-event time) and `cpu_baseline` (the scalar oracle on a bounded sample of the
+same workload on the host cores).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "Mpaths/sec (pixels×spp/s) at 1920×1080; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def byte_model(st, paths):
+    """B_read = sum_segments[76 + 32 n_node + 32 n_prim + (hit ? 40 : 16)] + 16 P."""
+    return (76 * st["segments"] + 32 * st["nodes"] + 32 * st["prims"] + 40 * st["hits"] + 16 * st["misses"]
+            + 16 * paths)
+
+
+def partition_rows(height, world, rank, block=16):
+    """Interleaved row blocks: block b = rows [16b, 16b+16) goes to rank b % world."""
+    ys = np.arange(height, dtype=np.int32)
+    return ys[(ys // block) % world == rank]
+
+
+def cpu_baseline(cfg, objs, sky, cam, seconds_hint=15.0, threads=None):
+    """The oracle (scalar C++ restatement, test infrastructure) on a bounded sample: 16 rows
+    spread over the image, full width, `spp_sample` passes (a pixel's passes are sequential, so
+    the sample takes the first passes of every sampled pixel)."""
+    import oracle
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    W, H = cfg["width"], cfg["height"]
+    rows = np.linspace(0, H - 1, 16).astype(np.int32)
+    # calibrate with a short run, then size the sample to ~seconds_hint
+    spp_probe = 2
+    rng = oracle.init_rng(cfg["seed"], W, rows, threads=threads)
+    t = time.perf_counter()
+    oracle.render(objs, cam, sky, rows, spp_probe, cfg["depth"], rng, threads=threads)
+    dt = max(time.perf_counter() - t, 1e-3)
+    spp_sample = int(max(2, min(cfg["spp"], spp_probe * seconds_hint / dt)))
+    rng = oracle.init_rng(cfg["seed"], W, rows, threads=threads)
+    t = time.perf_counter()
+    oracle.render(objs, cam, sky, rows, spp_sample, cfg["depth"], rng, threads=threads)
+    dt = time.perf_counter() - t
+    paths = rows.size * W * spp_sample
+    return {
+        "value": round(paths / dt / 1e6, 4),
+        "unit": "Mpaths/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{rows.size} rows evenly spaced x {W} px x first {spp_sample} of {cfg['spp']} spp of "
+                  f"{cfg['name']} ({paths} paths, {dt:.1f} s, std::thread over rows)",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--spp", type=int, default=None, help="override the config's spp")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--traffic-json", default=None,
+                    help="per-launch HBM traffic measured by rocprofv3 PMC (profiles/*.json) for this config")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from cpppathtracer_amd import Renderer, camera_get_copy, scenes, texture_io
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    cfg = dict(scenes.CONFIGS[args.config])
+    cfg["name"] = args.config
+    if args.spp:
+        cfg["spp"] = args.spp
+    if args.width:
+        cfg["width"] = args.width
+    if args.height:
+        cfg["height"] = args.height
+    cfg["seed"] = args.seed
+    W, H, spp, depth = cfg["width"], cfg["height"], cfg["spp"], cfg["depth"]
+    objs = scenes.SCENES[cfg["scene"]]()
+    sky = texture_io.load_cptex()
+    cam = camera_get_copy(scenes.camera_for(W, H))
+    rows = partition_rows(H, world, rank)
+
+    r = Renderer(torch.cuda.current_device())
+    stream = torch.cuda.current_stream()
+    r.set_stream(stream.cuda_stream)          # our kernels and torch's collectives share one stream
+    r.set_scene(objs)
+    r.set_env(sky)
+    r.set_frame(W, H, rows)
+    t_init = time.perf_counter()
+    r.init_rng(cfg["seed"])
+    torch.cuda.synchronize()
+    t_init = time.perf_counter() - t_init
+
+    npix_local = rows.size * W
+    max_rows = int(max(partition_rows(H, world, k).size for k in range(world)))
+    send = torch.zeros((max_rows * W, 4), dtype=torch.float32, device=dev)
+    gathered = torch.zeros((world * max_rows * W, 4), dtype=torch.float32, device=dev) if world > 1 else None
+
+    def step():
+        r.render(cam, spp, depth)
+        if world > 1:
+            r.copy_accum_device(send.data_ptr(), npix_local * 16)
+            dist.all_gather_into_tensor(gathered, send)
+
+    # Counting pass (same config, same pixels) for the algorithmic byte model; not timed.
+    r.reset_stats()
+    r.render(cam, spp, depth, stats=True)
+    torch.cuda.synchronize()
+    st_local = r.stats()
+    st_vec = torch.tensor([st_local[k] for k in ("segments", "nodes", "prims", "hits", "misses")],
+                          dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(st_vec)
+    st = dict(zip(("segments", "nodes", "prims", "hits", "misses"), (int(x) for x in st_vec.tolist())))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    kernel_ms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kernel_ms.append(None)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    # kernel time of the last step's render, from HIP events recorded around the launch on the
+    # launch stream (same stream as above)
+    last_kernel_ms = r.last_render_ms()
+    # per-step kernel times: re-time each step individually (untimed region) for the average
+    ks = []
+    for _ in range(max(1, min(args.steps, 3))):
+        r.render(cam, spp, depth)
+        ks.append(r.last_render_ms())
+    avg_kernel_ms = float(np.mean(ks))
+
+    t = torch.tensor([elapsed, avg_kernel_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, avg_kernel_ms_max = t.tolist()
+
+    if rank == 0:
+        paths_total = W * H * spp
+        value = paths_total * args.steps / elapsed / 1e6
+        # algorithmic bytes of one launch on rank 0's pixels: scale whole-image counts by the
+        # pixel share (interleaved blocks keep the shares statistically equal)
+        share = npix_local / float(W * H)
+        bytes_launch = byte_model(st, paths_total) * share
+        achieved = bytes_launch / (avg_kernel_ms / 1e3) / 1e9
+        traffic = None
+        if args.traffic_json and os.path.exists(args.traffic_json):
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("config") == args.config and tj.get("n_rows") == int(rows.size):
+                traffic = tj.get("hbm_bytes_per_launch")
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mpaths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic procedural scene, sky.png fixture)",
+            "config": {
+                "workload": f"{args.config}: {cfg['scene']} {W}x{H} {spp}spp depth {depth}",
+                "width": W, "height": H, "spp": spp, "max_depth": depth, "seed": cfg["seed"],
+                "rows_rendered": H, "path": "megakernel",
+                "parallelism": f"row-tiled x{world} (interleaved 16-row blocks)" + (", RCCL all-gather" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "k_megakernel",
+                "kernel_avg_ms": round(avg_kernel_ms, 3),
+                "bytes_per_launch": int(bytes_launch),
+                "byte_model": "SURVEY.md 8(d): 76 S + 32 nodes + 32 prims + 40 hits + 16 misses + 16 P",
+                "counts": st,
+            },
+            "rng_init_ms": round(t_init * 1e3, 2),
+        }
+        if not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(cfg, objs, sky, cam, seconds_hint=args.cpu_seconds)
+            except Exception as e:  # the baseline must never sink the GPU measurement
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,78 @@
+"""Builds libcpt.so (the HIP kernels + C-ABI + C++ API) in-tree for gfx950 with hipcc.
+
+hipcc cross-compiles without a GPU, so this runs in the build container; the resulting .so
+travels to the GPU box with the repo snapshot.
+"""
+import os
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libcpt.so")
+
+SOURCES = [
+    os.path.join(CSRC, "cpt_kernels.hip"),
+    os.path.join(CSRC, "cpt_capi.cpp"),
+    os.path.join(CSRC, "cpt_api.cpp"),
+]
+HEADERS = [
+    os.path.join(CSRC, "cpt_device.hpp"),
+    os.path.join(CSRC, "cpt_internal.hpp"),
+    os.path.join(REPO_DIR, "include", "cpt.h"),
+]
+
+# Float semantics: no FMA contraction, IEEE f32 div/sqrt, no fast math,
+# f32 denormals kept — each expression rounds exactly as written, as in the CPU oracle.
+HIPCC_FLAGS = [
+    "--offload-arch=gfx950",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-shared",
+    "-ffp-contract=off",
+    "-fno-fast-math",
+    "-fhip-fp32-correctly-rounded-divide-sqrt",
+    "-fno-gpu-flush-denormals-to-zero",
+    "-Wall",
+    "-Wno-unused-function",
+]
+
+
+def _hipcc():
+    for p in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if p and (os.path.isabs(p) and os.path.exists(p) or not os.path.isabs(p)):
+            return p
+    return "hipcc"
+
+
+def _extra_sources():
+    return [s for s in SOURCES if os.path.exists(s)]
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    deps = _extra_sources() + [h for h in HEADERS if os.path.exists(h)]
+    deps += [os.path.join(REPO_DIR, "include", "cpppathtracer", f)
+             for f in os.listdir(os.path.join(REPO_DIR, "include", "cpppathtracer"))] if os.path.isdir(
+        os.path.join(REPO_DIR, "include", "cpppathtracer")) else []
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return LIB_PATH
+    tmp = LIB_PATH + ".tmp"
+    cmd = [_hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO_DIR, "include"), "-o", tmp, *_extra_sources()]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

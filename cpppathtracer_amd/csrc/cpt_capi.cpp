@@ -1,0 +1,853 @@
+// cpt_capi.cpp — implementation of the C-ABI in include/cpt.h.
+//
+// Owns the per-context device memory, builds the reference's median-split BVH on the host
+// (bvh.cu:31-120) and linearises it into the skip-link order the kernels walk, computes the
+// XORWOW jump tables (GF(2) matrix powers), and launches the kernels on one HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/cpt.h"
+#include "cpt_internal.hpp"
+
+static_assert(sizeof(cpt_material) == 40, "cpt_material must match Material (40 B)");
+static_assert(sizeof(cpt_object) == 72, "cpt_object must match Object (72 B)");
+static_assert(sizeof(cpt_camera) == 136, "cpt_camera must match MotionalCamera (136 B)");
+static_assert(offsetof(cpt_object, center) == 48, "Object::center_ offset");
+static_assert(offsetof(cpt_material, refractive_index) == 24, "Material::refractive_index_ offset");
+
+namespace {
+
+using cpt::Mat;
+using cpt::Node;
+using cpt::Prim;
+
+std::string g_create_error;
+
+// ------------------------------------------------------------------------------------
+// Host BVH: SceneBVH::Divide (bvh.cu:31-90) and the skip-link linearisation.
+// ------------------------------------------------------------------------------------
+struct F3 { float x, y, z; };
+
+inline float MIN_(float a, float b) { return a < b ? a : b; }   // ray_tracing_math.hpp:19-21
+inline float MAX_(float a, float b) { return a > b ? a : b; }   // ray_tracing_math.hpp:15-17
+inline float ABS_(float a) { return a >= 0 ? a : -a; }          // ray_tracing_math.hpp:23-25
+
+// Object::GetAABBMax / GetAABBMin (object.cu:134-170)
+F3 aabb_max(const cpt_object& o) {
+    const float tol = 2e-5f * 5.f;
+    switch (o.type) {
+        case CPT_PRIM_SPHERE: {
+            float r = ABS_(o.radius);
+            return F3{o.center.x + r, o.center.y + r, o.center.z + r};
+        }
+        case CPT_PRIM_PLATFORM: return F3{1e30f * 5, o.y_pos + tol, 1e30f * 5};
+        case CPT_PRIM_CYLINDER:
+            return F3{o.center.x + ABS_(o.radius), o.center.y + o.height / 2 + tol, o.center.z + ABS_(o.radius)};
+        default: return F3{0, 0, 0};
+    }
+}
+
+F3 aabb_min(const cpt_object& o) {
+    const float tol = 2e-5f * 5.f;
+    switch (o.type) {
+        case CPT_PRIM_SPHERE: {
+            float r = ABS_(o.radius);
+            return F3{o.center.x - r, o.center.y - r, o.center.z - r};
+        }
+        case CPT_PRIM_PLATFORM: return F3{-1e30f * 5, o.y_pos - tol, -1e30f * 5};
+        case CPT_PRIM_CYLINDER:
+            return F3{o.center.x - ABS_(o.radius), o.center.y - o.height / 2 - tol, o.center.z - ABS_(o.radius)};
+        default: return F3{0, 0, 0};
+    }
+}
+
+struct BNode {            // bvh.h:32-38, object stored as an index
+    F3 bmin, bmax;
+    bool is_object;
+    int left, right, obj, parent;
+};
+
+struct HostBvh {
+    std::vector<BNode> nodes;          // Divide creation order (reference order)
+    std::vector<int> leaf_of_object;   // object index -> node
+};
+
+int divide(HostBvh& b, const std::vector<cpt_object>& objs, std::vector<int>& idx, int l, int r) {
+    if (l >= r) return -1;
+    int ret = (int)b.nodes.size();
+    b.nodes.push_back(BNode{});
+    F3 lmin = aabb_min(objs[idx[l]]), lmax = aabb_max(objs[idx[l]]);
+    if (l == r - 1) {
+        BNode& n = b.nodes[ret];
+        n.left = n.right = -1;
+        n.bmin = lmin; n.bmax = lmax;
+        n.is_object = true;
+        n.obj = idx[l];
+        b.leaf_of_object[idx[l]] = ret;
+        return ret;
+    }
+    float minx = lmin.x, miny = lmin.y, minz = lmin.z, maxx = lmax.x, maxy = lmax.y, maxz = lmax.z;
+    for (int i = l + 1; i < r; ++i) {
+        F3 a = aabb_min(objs[idx[i]]), c = aabb_max(objs[idx[i]]);
+        minx = MIN_(minx, a.x); miny = MIN_(miny, a.y); minz = MIN_(minz, a.z);
+        maxx = MAX_(maxx, c.x); maxy = MAX_(maxy, c.y); maxz = MAX_(maxz, c.z);
+    }
+    float sx = maxx - minx, sy = maxy - miny, sz = maxz - minz;
+    int axis = (sx >= sy && sx >= sz) ? 0 : (sy >= sz ? 1 : 2);
+    // Centroids precomputed once per split (the reference recomputes them in the comparator);
+    // stable order for equal centroids (std::sort's tie order is implementation-defined).
+    std::vector<std::pair<float, int>> keyed;
+    keyed.reserve(r - l);
+    for (int i = l; i < r; ++i) {
+        F3 a = aabb_min(objs[idx[i]]), c = aabb_max(objs[idx[i]]);
+        float lo = axis == 0 ? a.x : axis == 1 ? a.y : a.z;
+        float hi = axis == 0 ? c.x : axis == 1 ? c.y : c.z;
+        keyed.emplace_back((lo + hi) / 2, idx[i]);
+    }
+    std::stable_sort(keyed.begin(), keyed.end(),
+                     [](const std::pair<float, int>& p, const std::pair<float, int>& q) { return p.first < q.first; });
+    for (int i = l; i < r; ++i) idx[i] = keyed[i - l].second;
+    int mid = (l + r) / 2;
+    int left = divide(b, objs, idx, l, mid);
+    int right = divide(b, objs, idx, mid, r);
+    BNode& n = b.nodes[ret];
+    n.left = left; n.right = right;
+    n.bmin = F3{minx, miny, minz};
+    n.bmax = F3{maxx, maxy, maxz};
+    n.is_object = false;
+    n.obj = -1;
+    b.nodes[left].parent = ret;
+    b.nodes[right].parent = ret;
+    return ret;
+}
+
+void build_host_bvh(HostBvh& b, const std::vector<cpt_object>& objs) {
+    b.nodes.clear();
+    b.leaf_of_object.assign(objs.size(), -1);
+    if (objs.empty()) return;
+    b.nodes.reserve(2 * objs.size());
+    std::vector<int> idx(objs.size());
+    for (size_t i = 0; i < objs.size(); ++i) idx[i] = (int)i;
+    divide(b, objs, idx, 0, (int)objs.size());
+    b.nodes[0].parent = -1;
+}
+
+// Right-first preorder = the order the reference's stack DFS pops nodes (left pushed first,
+// bvh.cu:201-202).  skip[i] = position after node i's subtree.
+void linearise(const HostBvh& b, std::vector<Node>& out, std::vector<int>& pos_of_node) {
+    out.clear();
+    pos_of_node.assign(b.nodes.size(), -1);
+    if (b.nodes.empty()) return;
+    struct Frame { int node; int stage; };
+    std::vector<Frame> st;
+    st.push_back({0, 0});
+    out.reserve(b.nodes.size());
+    while (!st.empty()) {
+        Frame& f = st.back();
+        const BNode& n = b.nodes[f.node];
+        if (f.stage == 0) {
+            pos_of_node[f.node] = (int)out.size();
+            Node g;
+            g.bmin_x = n.bmin.x; g.bmin_y = n.bmin.y; g.bmin_z = n.bmin.z;
+            g.bmax_x = n.bmax.x; g.bmax_y = n.bmax.y; g.bmax_z = n.bmax.z;
+            g.prim = n.is_object ? n.obj : -1;
+            g.miss = -1;
+            out.push_back(g);
+            if (n.is_object) {
+                out[pos_of_node[f.node]].miss = (int)out.size();
+                st.pop_back();
+                continue;
+            }
+            f.stage = 1;
+            st.push_back({n.right, 0});
+        } else if (f.stage == 1) {
+            f.stage = 2;
+            st.push_back({n.left, 0});
+        } else {
+            out[pos_of_node[f.node]].miss = (int)out.size();
+            st.pop_back();
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// XORWOW jump tables: jumps[t] = A^(2^67 * 2^t), 160x160 over GF(2), column-major
+// (column c = A^k e_c as 5 words), the layout rocRAND uses (rocrand_xorwow.h:51-65).
+// ------------------------------------------------------------------------------------
+struct BitMat { uint32_t m[800]; };
+
+void xorshift_step(uint32_t v[5]) {   // linear part of curand() (d excluded)
+    uint32_t t = v[0] ^ (v[0] >> 2);
+    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+    v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+}
+
+void bm_apply(const BitMat& M, const uint32_t in[5], uint32_t out[5]) {
+    uint32_t r[5] = {0, 0, 0, 0, 0};
+    for (int c = 0; c < 160; ++c)
+        if ((in[c >> 5] >> (c & 31)) & 1u)
+            for (int k = 0; k < 5; ++k) r[k] ^= M.m[c * 5 + k];
+    std::memcpy(out, r, sizeof(r));
+}
+
+BitMat bm_square(const BitMat& M) {
+    BitMat R;
+    for (int c = 0; c < 160; ++c) bm_apply(M, &M.m[c * 5], &R.m[c * 5]);
+    return R;
+}
+
+const std::vector<uint32_t>& jump_tables() {
+    static std::vector<uint32_t> tbl;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        BitMat A;
+        for (int c = 0; c < 160; ++c) {
+            uint32_t v[5] = {0, 0, 0, 0, 0};
+            v[c >> 5] = 1u << (c & 31);
+            xorshift_step(v);
+            std::memcpy(&A.m[c * 5], v, 20);
+        }
+        for (int i = 0; i < 67; ++i) A = bm_square(A);
+        tbl.resize(64 * 800);
+        for (int t = 0; t < 64; ++t) {
+            std::memcpy(&tbl[(size_t)t * 800], A.m, sizeof(A.m));
+            A = bm_square(A);
+        }
+    });
+    return tbl;
+}
+
+// curand_init's seed scrambling (curand_kernel.h, CUDA 11.7).
+void curand_seed_state(uint64_t seed, uint32_t out[6]) {
+    uint32_t s0 = (uint32_t)seed ^ 0xaad26b49u;
+    uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+    uint32_t t0 = 1099087573u * s0;
+    uint32_t t1 = 2591861531u * s1;
+    out[0] = 123456789u + t0;
+    out[1] = 362436069u ^ t0;
+    out[2] = 521288629u + t1;
+    out[3] = 88675123u ^ t1;
+    out[4] = 5783321u + t0;
+    out[5] = 6615241u + t1 + t0;
+}
+
+}  // namespace
+
+// ======================================================================================
+// Context
+// ======================================================================================
+struct cpt_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t user_stream = nullptr;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    bool have_timing = false;
+    std::string err;
+
+    // scene
+    std::vector<cpt_object> objs;
+    HostBvh bvh;
+    std::vector<Node> lin;
+    std::vector<int> pos_of_node;
+    std::vector<Prim> prims_h;
+    std::vector<Mat> mats_h;
+    Node* d_nodes = nullptr;
+    Prim* d_prims = nullptr;
+    Mat* d_mats = nullptr;
+    size_t cap_nodes = 0, cap_prims = 0, cap_mats = 0;
+    bool scene_set = false;
+
+    // environment
+    uint32_t* d_env = nullptr;
+    int env_w = 1, env_h = 1, env_cols = 0;
+    size_t cap_env = 0;
+
+    // frame
+    int width = 0, height = 0, n_rows = 0;
+    std::vector<int32_t> rows_h;
+    int32_t* d_rows = nullptr;
+    uint32_t* d_rng = nullptr;
+    float4* d_accum = nullptr;
+    float* d_normal = nullptr;
+    float* d_depth = nullptr;
+    bool frame_set = false, rng_set = false;
+
+    // rng init
+    uint32_t* d_jumps = nullptr;
+    uint32_t* d_scratch_w = nullptr;
+    uint32_t* d_scratch_m = nullptr;
+
+    unsigned long long* d_stats = nullptr;
+    float last_kernel_ms = 0.f;
+    int last_launches = 0;
+
+    hipStream_t stream() const { return user_stream ? user_stream : own_stream; }
+};
+
+namespace {
+
+int fail(cpt_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    else g_create_error = buf;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                             \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess)                                                                          \
+            return fail((ctx), e_ == hipErrorOutOfMemory ? CPT_ERR_OUT_OF_MEMORY : CPT_ERR_HIP,        \
+                        "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__);           \
+    } while (0)
+
+template <typename T>
+int ensure(cpt_ctx* c, T** ptr, size_t* cap, size_t count) {
+    if (*ptr && *cap >= count) return CPT_OK;
+    if (*ptr) { (void)hipFree(*ptr); *ptr = nullptr; *cap = 0; }
+    if (count == 0) return CPT_OK;
+    HIP_TRY(c, hipMalloc((void**)ptr, count * sizeof(T)));
+    *cap = count;
+    return CPT_OK;
+}
+
+void free_frame(cpt_ctx* c) {
+    (void)hipFree(c->d_rows); c->d_rows = nullptr;
+    (void)hipFree(c->d_rng); c->d_rng = nullptr;
+    (void)hipFree(c->d_accum); c->d_accum = nullptr;
+    (void)hipFree(c->d_normal); c->d_normal = nullptr;
+    (void)hipFree(c->d_depth); c->d_depth = nullptr;
+    (void)hipFree(c->d_scratch_w); c->d_scratch_w = nullptr;
+    (void)hipFree(c->d_scratch_m); c->d_scratch_m = nullptr;
+    c->frame_set = c->rng_set = false;
+}
+
+Prim to_prim(const cpt_object& o, int mat_index) {
+    Prim p;
+    p.cx = o.center.x; p.cy = o.center.y; p.cz = o.center.z;
+    p.radius = o.radius;
+    p.y_pos = o.y_pos;
+    p.height = o.height;
+    p.type = o.type;
+    p.material = mat_index;
+    return p;
+}
+
+Mat to_mat(const cpt_material& m) {
+    Mat g;
+    g.kd_x = m.u.kd.x; g.kd_y = m.u.kd.y; g.kd_z = m.u.kd.z;
+    g.emit = m.emit_intensity;
+    g.ior = m.refractive_index;
+    g.smoothness = m.smoothness;
+    g.reflectivity = m.reflectivity;
+    g.type = m.type;
+    g.inv_alpha = 0.0;   // filled on the device (k_prepare_materials)
+    g.pad_ = 0.0;
+    return g;
+}
+
+int upload_scene(cpt_ctx* c) {
+    HIP_TRY(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = ensure(c, &c->d_nodes, &c->cap_nodes, std::max<size_t>(1, c->lin.size()))) != CPT_OK) return rc;
+    if ((rc = ensure(c, &c->d_prims, &c->cap_prims, std::max<size_t>(1, c->prims_h.size()))) != CPT_OK) return rc;
+    if ((rc = ensure(c, &c->d_mats, &c->cap_mats, std::max<size_t>(1, c->mats_h.size()))) != CPT_OK) return rc;
+    hipStream_t s = c->stream();
+    if (!c->lin.empty())
+        HIP_TRY(c, hipMemcpyAsync(c->d_nodes, c->lin.data(), c->lin.size() * sizeof(Node), hipMemcpyHostToDevice, s));
+    if (!c->prims_h.empty())
+        HIP_TRY(c, hipMemcpyAsync(c->d_prims, c->prims_h.data(), c->prims_h.size() * sizeof(Prim), hipMemcpyHostToDevice, s));
+    if (!c->mats_h.empty()) {
+        HIP_TRY(c, hipMemcpyAsync(c->d_mats, c->mats_h.data(), c->mats_h.size() * sizeof(Mat), hipMemcpyHostToDevice, s));
+        HIP_TRY(c, cpt::launch_prepare_materials(c->d_mats, (int)c->mats_h.size(), s));
+    }
+    HIP_TRY(c, hipStreamSynchronize(s));
+    c->scene_set = true;
+    return CPT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpt_abi_version(void) { return CPT_ABI_VERSION; }
+
+const char* cpt_status_string(int status) {
+    switch (status) {
+        case CPT_OK: return "ok";
+        case CPT_ERR_INVALID_ARG: return "invalid argument";
+        case CPT_ERR_NO_DEVICE: return "no HIP device";
+        case CPT_ERR_HIP: return "HIP runtime error";
+        case CPT_ERR_OUT_OF_MEMORY: return "out of device memory";
+        case CPT_ERR_STATE: return "invalid state";
+        case CPT_ERR_UNSUPPORTED: return "unsupported";
+        default: return "unknown status";
+    }
+}
+
+int cpt_get_device_count(int* count) {
+    if (!count) return CPT_ERR_INVALID_ARG;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    *count = (e == hipSuccess) ? n : 0;
+    return CPT_OK;
+}
+
+int cpt_create(int device, cpt_ctx** out) {
+    if (!out) return fail(nullptr, CPT_ERR_INVALID_ARG, "cpt_create: out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return fail(nullptr, CPT_ERR_NO_DEVICE, "cpt_create: no HIP device visible");
+    if (device < 0 || device >= n) return fail(nullptr, CPT_ERR_INVALID_ARG, "cpt_create: device %d of %d", device, n);
+    cpt_ctx* c = new (std::nothrow) cpt_ctx;
+    if (!c) return fail(nullptr, CPT_ERR_OUT_OF_MEMORY, "cpt_create: host allocation failed");
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev_start);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev_stop);
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) {
+        const std::vector<uint32_t>& J = jump_tables();
+        e = hipMalloc((void**)&c->d_jumps, J.size() * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemcpy(c->d_jumps, J.data(), J.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+        int rc = fail(nullptr, CPT_ERR_HIP, "cpt_create: %s", hipGetErrorString(e));
+        cpt_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return CPT_OK;
+}
+
+int cpt_destroy(cpt_ctx* c) {
+    if (!c) return CPT_OK;
+    (void)hipSetDevice(c->device);
+    if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+    if (c->user_stream) (void)hipStreamSynchronize(c->user_stream);
+    free_frame(c);
+    (void)hipFree(c->d_nodes);
+    (void)hipFree(c->d_prims);
+    (void)hipFree(c->d_mats);
+    (void)hipFree(c->d_env);
+    (void)hipFree(c->d_jumps);
+    (void)hipFree(c->d_stats);
+    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+    if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return CPT_OK;
+}
+
+const char* cpt_last_error(const cpt_ctx* c) { return c ? c->err.c_str() : g_create_error.c_str(); }
+
+int cpt_set_stream(cpt_ctx* c, void* s) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    c->user_stream = (hipStream_t)s;
+    return CPT_OK;
+}
+
+// MotionalCamera::GetCopy (motional_camera.cu:177-200)
+int cpt_camera_get_copy(cpt_camera* cam) {
+    if (!cam || cam->width <= 0 || cam->height <= 0) return CPT_ERR_INVALID_ARG;
+    auto sub = [](cpt_float3 a, cpt_float3 b) { return cpt_float3{a.x - b.x, a.y - b.y, a.z - b.z}; };
+    auto add = [](cpt_float3 a, cpt_float3 b) { return cpt_float3{a.x + b.x, a.y + b.y, a.z + b.z}; };
+    auto scale = [](float s, cpt_float3 a) { return cpt_float3{s * a.x, s * a.y, s * a.z}; };
+    auto dot = [](cpt_float3 a, cpt_float3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; };
+    auto normalize = [&](cpt_float3 v) {
+        float inv = 1.0f / sqrtf(dot(v, v));
+        return cpt_float3{v.x * inv, v.y * inv, v.z * inv};
+    };
+    auto cross = [](cpt_float3 a, cpt_float3 b) {
+        return cpt_float3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+    };
+    float theta = (float)((double)cam->view_fov * 3.14159265358979323846 / 180);
+    float aspect = float(cam->width) / float(cam->height);
+    float half_height = tanf(theta / 2);
+    float half_width = aspect * half_height;
+    cam->w = normalize(sub(cam->origin, cam->look_at));
+    cam->u = normalize(cross(cam->vup, cam->w));
+    cam->v = cross(cam->w, cam->u);
+    cpt_float3 ol = sub(cam->origin, cam->look_at);
+    cam->dist_to_focus = sqrtf(dot(ol, ol));
+    float d = cam->dist_to_focus;
+    cam->top_left_corner = sub(add(sub(cam->origin, scale(half_width * d, cam->u)), scale(half_height * d, cam->v)),
+                               scale(d, cam->w));
+    cam->horizontal = scale(2 * half_width * d, cam->u);
+    cam->vertical = scale(-2 * half_height * d, cam->v);
+    cam->cur_sample_idx++;
+    return CPT_OK;
+}
+
+int cpt_set_scene(cpt_ctx* c, const cpt_object* objs, int n) {
+    if (!c || n < 0 || (n > 0 && !objs)) return c ? fail(c, CPT_ERR_INVALID_ARG, "cpt_set_scene: bad arguments") : CPT_ERR_INVALID_ARG;
+    try {
+        for (int i = 0; i < n; ++i) {
+            if (objs[i].material.have_tex)
+                return fail(c, CPT_ERR_UNSUPPORTED, "cpt_set_scene: object %d has a textured material (not supported yet)", i);
+        }
+        c->objs.assign(objs, objs + n);
+        build_host_bvh(c->bvh, c->objs);
+        linearise(c->bvh, c->lin, c->pos_of_node);
+        c->prims_h.resize(n);
+        c->mats_h.resize(n);
+        for (int i = 0; i < n; ++i) {
+            c->prims_h[i] = to_prim(c->objs[i], i);   // one material per object (copied by value, bvh.cu:43)
+            c->mats_h[i] = to_mat(c->objs[i].material);
+        }
+    } catch (const std::bad_alloc&) {
+        return fail(c, CPT_ERR_OUT_OF_MEMORY, "cpt_set_scene: host allocation failed");
+    }
+    return upload_scene(c);
+}
+
+// SceneBVH::UpdateObject (bvh.cu:122-157): replace the leaf's object, refit the ancestors
+// (MIN/MAX of the two children per axis), re-upload.
+int cpt_update_object(cpt_ctx* c, int index, const cpt_object* obj) {
+    if (!c || !obj) return CPT_ERR_INVALID_ARG;
+    if (!c->scene_set || index < 0 || index >= (int)c->objs.size())
+        return fail(c, CPT_ERR_INVALID_ARG, "cpt_update_object: index %d out of range", index);
+    if (obj->material.have_tex) return fail(c, CPT_ERR_UNSUPPORTED, "cpt_update_object: textured material");
+    c->objs[index] = *obj;
+    int ni = c->bvh.leaf_of_object[index];
+    while (ni != -1) {
+        BNode& n = c->bvh.nodes[ni];
+        if (n.is_object) {
+            n.bmax = aabb_max(c->objs[n.obj]);
+            n.bmin = aabb_min(c->objs[n.obj]);
+        } else {
+            const BNode& L = c->bvh.nodes[n.left];
+            const BNode& R = c->bvh.nodes[n.right];
+            n.bmax = F3{MAX_(L.bmax.x, R.bmax.x), MAX_(L.bmax.y, R.bmax.y), MAX_(L.bmax.z, R.bmax.z)};
+            n.bmin = F3{MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z)};
+        }
+        Node& g = c->lin[c->pos_of_node[ni]];
+        g.bmin_x = n.bmin.x; g.bmin_y = n.bmin.y; g.bmin_z = n.bmin.z;
+        g.bmax_x = n.bmax.x; g.bmax_y = n.bmax.y; g.bmax_z = n.bmax.z;
+        ni = n.parent;
+    }
+    c->prims_h[index] = to_prim(c->objs[index], index);
+    c->mats_h[index] = to_mat(c->objs[index].material);
+    return upload_scene(c);
+}
+
+int cpt_scene_bvh_export(cpt_ctx* c, float* boxes, int32_t* links, int capacity, int* n_nodes) {
+    if (!c || !n_nodes) return CPT_ERR_INVALID_ARG;
+    int m = (int)c->bvh.nodes.size();
+    *n_nodes = m;
+    for (int i = 0; i < m && i < capacity; ++i) {
+        const BNode& n = c->bvh.nodes[i];
+        if (boxes) {
+            float* b = boxes + 6 * i;
+            b[0] = n.bmin.x; b[1] = n.bmin.y; b[2] = n.bmin.z; b[3] = n.bmax.x; b[4] = n.bmax.y; b[5] = n.bmax.z;
+        }
+        if (links) {
+            int32_t* l = links + 4 * i;
+            l[0] = n.is_object; l[1] = n.left; l[2] = n.right; l[3] = n.obj;
+        }
+    }
+    return CPT_OK;
+}
+
+int cpt_bvh_build_host(const cpt_object* objs, int n, float* boxes, int32_t* links, int capacity, int* n_nodes) {
+    if (n < 0 || (n > 0 && !objs) || !n_nodes) return CPT_ERR_INVALID_ARG;
+    try {
+        std::vector<cpt_object> v(objs, objs + n);
+        HostBvh b;
+        build_host_bvh(b, v);
+        int m = (int)b.nodes.size();
+        *n_nodes = m;
+        for (int i = 0; i < m && i < capacity; ++i) {
+            const BNode& nd = b.nodes[i];
+            if (boxes) {
+                float* x = boxes + 6 * i;
+                x[0] = nd.bmin.x; x[1] = nd.bmin.y; x[2] = nd.bmin.z; x[3] = nd.bmax.x; x[4] = nd.bmax.y; x[5] = nd.bmax.z;
+            }
+            if (links) {
+                int32_t* l = links + 4 * i;
+                l[0] = nd.is_object; l[1] = nd.left; l[2] = nd.right; l[3] = nd.obj;
+            }
+        }
+    } catch (const std::bad_alloc&) {
+        return CPT_ERR_OUT_OF_MEMORY;
+    }
+    return CPT_OK;
+}
+
+int cpt_set_env_texture(cpt_ctx* c, const uint8_t* rgba, int logical_width, int height, int valid_cols) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    if (logical_width <= 0 || height <= 0 || valid_cols < 0 || valid_cols > logical_width || (valid_cols > 0 && !rgba))
+        return fail(c, CPT_ERR_INVALID_ARG, "cpt_set_env_texture: bad geometry %dx%d cols %d", logical_width, height, valid_cols);
+    HIP_TRY(c, hipSetDevice(c->device));
+    size_t n = (size_t)valid_cols * height;
+    int rc = ensure(c, &c->d_env, &c->cap_env, std::max<size_t>(1, n));
+    if (rc != CPT_OK) return rc;
+    if (n) HIP_TRY(c, hipMemcpy(c->d_env, rgba, n * 4, hipMemcpyHostToDevice));
+    c->env_w = logical_width;
+    c->env_h = height;
+    c->env_cols = valid_cols;
+    return CPT_OK;
+}
+
+int cpt_set_frame(cpt_ctx* c, int width, int height, const int32_t* rows, int n_rows) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    if (width <= 0 || height <= 0) return fail(c, CPT_ERR_INVALID_ARG, "cpt_set_frame: %dx%d", width, height);
+    std::vector<int32_t> r;
+    if (rows) {
+        if (n_rows < 0) return fail(c, CPT_ERR_INVALID_ARG, "cpt_set_frame: n_rows %d", n_rows);
+        r.assign(rows, rows + n_rows);
+        for (int32_t y : r)
+            if (y < 0 || y >= height) return fail(c, CPT_ERR_INVALID_ARG, "cpt_set_frame: row %d outside [0,%d)", y, height);
+    } else {
+        r.resize(height);
+        for (int y = 0; y < height; ++y) r[y] = y;
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    free_frame(c);
+    c->width = width;
+    c->height = height;
+    c->n_rows = (int)r.size();
+    c->rows_h = r;
+    size_t npix = (size_t)c->n_rows * width;
+    if (c->n_rows > 0) {
+        HIP_TRY(c, hipMalloc((void**)&c->d_rows, r.size() * sizeof(int32_t)));
+        HIP_TRY(c, hipMemcpy(c->d_rows, r.data(), r.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        HIP_TRY(c, hipMalloc((void**)&c->d_rng, 6 * npix * sizeof(uint32_t)));
+        HIP_TRY(c, hipMalloc((void**)&c->d_accum, npix * sizeof(float4)));
+        HIP_TRY(c, hipMemset(c->d_accum, 0, npix * sizeof(float4)));
+        HIP_TRY(c, hipMemset(c->d_rng, 0, 6 * npix * sizeof(uint32_t)));
+    }
+    c->frame_set = true;
+    c->rng_set = false;
+    return CPT_OK;
+}
+
+int cpt_init_rng(cpt_ctx* c, uint64_t seed) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    if (!c->frame_set) return fail(c, CPT_ERR_STATE, "cpt_init_rng: cpt_set_frame first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (c->n_rows == 0) { c->rng_set = true; return CPT_OK; }
+    if (!c->d_scratch_w) HIP_TRY(c, hipMalloc((void**)&c->d_scratch_w, 5 * (size_t)c->width * sizeof(uint32_t)));
+    if (!c->d_scratch_m) HIP_TRY(c, hipMalloc((void**)&c->d_scratch_m, (size_t)c->n_rows * 800 * sizeof(uint32_t)));
+    uint32_t st[6];
+    curand_seed_state(seed, st);
+    HIP_TRY(c, cpt::launch_init_rng(c->d_jumps, st, c->width, c->d_rows, c->n_rows, c->d_scratch_w, c->d_scratch_m,
+                                   c->d_rng, c->stream()));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    // the scratch matrices are n_rows * 3.2 KB; release them (one-time init)
+    (void)hipFree(c->d_scratch_m); c->d_scratch_m = nullptr;
+    (void)hipFree(c->d_scratch_w); c->d_scratch_w = nullptr;
+    c->rng_set = true;
+    return CPT_OK;
+}
+
+int cpt_read_rng(cpt_ctx* c, uint32_t* planar6) {
+    if (!c || !planar6) return CPT_ERR_INVALID_ARG;
+    if (!c->frame_set) return fail(c, CPT_ERR_STATE, "cpt_read_rng: no frame");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    size_t n = 6 * (size_t)c->n_rows * c->width;
+    if (n) HIP_TRY(c, hipMemcpy(planar6, c->d_rng, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return CPT_OK;
+}
+
+int cpt_write_rng(cpt_ctx* c, const uint32_t* planar6) {
+    if (!c || !planar6) return CPT_ERR_INVALID_ARG;
+    if (!c->frame_set) return fail(c, CPT_ERR_STATE, "cpt_write_rng: no frame");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    size_t n = 6 * (size_t)c->n_rows * c->width;
+    if (n) HIP_TRY(c, hipMemcpy(c->d_rng, planar6, n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->rng_set = true;
+    return CPT_OK;
+}
+
+int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32_t flags) {
+    if (!c || !cam) return CPT_ERR_INVALID_ARG;
+    if (spp < 0 || max_depth < 0 || max_depth > (int)cpt::MAX_RECURSION_DEPTH_SET)
+        return fail(c, CPT_ERR_INVALID_ARG, "cpt_render: spp %d, max_depth %d (must be 0..32)", spp, max_depth);
+    if (!c->scene_set) return fail(c, CPT_ERR_STATE, "cpt_render: cpt_set_scene first");
+    if (!c->frame_set || !c->rng_set) return fail(c, CPT_ERR_STATE, "cpt_render: cpt_set_frame + cpt_init_rng first");
+    if (cam->width != c->width || cam->height != c->height)
+        return fail(c, CPT_ERR_INVALID_ARG, "cpt_render: camera %dx%d vs frame %dx%d", cam->width, cam->height, c->width, c->height);
+    if (flags & CPT_PATH_WAVEFRONT) return fail(c, CPT_ERR_UNSUPPORTED, "cpt_render: wavefront path not built yet");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream();
+    const bool aux = (flags & CPT_RENDER_AUX) != 0;
+    if (aux) {
+        size_t npix = (size_t)c->n_rows * c->width;
+        if (!c->d_normal && npix) HIP_TRY(c, hipMalloc((void**)&c->d_normal, npix * 3 * sizeof(float)));
+        if (!c->d_depth && npix) HIP_TRY(c, hipMalloc((void**)&c->d_depth, npix * sizeof(float)));
+    }
+    cpt::KParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.nodes = c->d_nodes;
+    p.prims = c->d_prims;
+    p.mats = c->d_mats;
+    p.n_nodes = (int)c->lin.size();
+    p.env = c->d_env;
+    p.env_w = c->env_w;
+    p.env_h = c->env_h;
+    p.env_cols = c->d_env ? c->env_cols : 0;
+    for (int k = 0; k < 3; ++k) {
+        p.cam.origin[k] = (&cam->origin.x)[k];
+        p.cam.u[k] = (&cam->u.x)[k];
+        p.cam.v[k] = (&cam->v.x)[k];
+        p.cam.top_left[k] = (&cam->top_left_corner.x)[k];
+        p.cam.horizontal[k] = (&cam->horizontal.x)[k];
+        p.cam.vertical[k] = (&cam->vertical.x)[k];
+    }
+    p.cam.lens_radius = cam->lens_radius;
+    p.cam.width = cam->width;
+    p.cam.height = cam->height;
+    p.rows = c->d_rows;
+    p.n_rows = c->n_rows;
+    p.width = c->width;
+    p.rng = c->d_rng;
+    p.accum = c->d_accum;
+    p.normal = c->d_normal;
+    p.depth = c->d_depth;
+    p.stats = c->d_stats;
+    p.spp = spp;
+    p.max_depth = max_depth;
+    p.accumulate = (flags & CPT_RENDER_ACCUMULATE) ? 1 : 0;
+    HIP_TRY(c, hipEventRecord(c->ev_start, s));
+    HIP_TRY(c, cpt::launch_megakernel(p, (flags & CPT_RENDER_STATS) != 0, aux, s));
+    HIP_TRY(c, hipEventRecord(c->ev_stop, s));
+    c->have_timing = true;
+    c->last_launches = 1;
+    if (flags & CPT_RENDER_SYNC) HIP_TRY(c, hipStreamSynchronize(s));
+    return CPT_OK;
+}
+
+int cpt_synchronize(cpt_ctx* c) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    return CPT_OK;
+}
+
+int cpt_read_accum(cpt_ctx* c, float* rgba) {
+    if (!c || !rgba) return CPT_ERR_INVALID_ARG;
+    if (!c->frame_set) return fail(c, CPT_ERR_STATE, "cpt_read_accum: no frame");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    size_t n = (size_t)c->n_rows * c->width;
+    if (n) HIP_TRY(c, hipMemcpy(rgba, c->d_accum, n * sizeof(float4), hipMemcpyDeviceToHost));
+    return CPT_OK;
+}
+
+int cpt_clear_accum(cpt_ctx* c) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    if (!c->frame_set) return fail(c, CPT_ERR_STATE, "cpt_clear_accum: no frame");
+    HIP_TRY(c, hipSetDevice(c->device));
+    size_t n = (size_t)c->n_rows * c->width;
+    if (n) HIP_TRY(c, hipMemsetAsync(c->d_accum, 0, n * sizeof(float4), c->stream()));
+    return CPT_OK;
+}
+
+int cpt_read_aux(cpt_ctx* c, float* normal3, float* depth) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    if (!c->d_normal || !c->d_depth) return fail(c, CPT_ERR_STATE, "cpt_read_aux: render with CPT_RENDER_AUX first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    size_t n = (size_t)c->n_rows * c->width;
+    if (normal3 && n) HIP_TRY(c, hipMemcpy(normal3, c->d_normal, n * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    if (depth && n) HIP_TRY(c, hipMemcpy(depth, c->d_depth, n * sizeof(float), hipMemcpyDeviceToHost));
+    return CPT_OK;
+}
+
+int cpt_copy_accum_device(cpt_ctx* c, void* dst, size_t bytes) {
+    if (!c || (!dst && bytes)) return CPT_ERR_INVALID_ARG;
+    size_t have = (size_t)c->n_rows * c->width * sizeof(float4);
+    if (bytes > have) return fail(c, CPT_ERR_INVALID_ARG, "cpt_copy_accum_device: %zu > %zu bytes", bytes, have);
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (bytes) HIP_TRY(c, hipMemcpyAsync(dst, c->d_accum, bytes, hipMemcpyDeviceToDevice, c->stream()));
+    return CPT_OK;
+}
+
+int cpt_get_stats(cpt_ctx* c, cpt_stats* out) {
+    if (!c || !out) return CPT_ERR_INVALID_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    unsigned long long h[8];
+    HIP_TRY(c, hipMemcpy(h, c->d_stats, sizeof(h), hipMemcpyDeviceToHost));
+    out->segments = h[0];
+    out->node_visits = h[1];
+    out->prim_tests = h[2];
+    out->hits = h[3];
+    out->misses = h[4];
+    return CPT_OK;
+}
+
+int cpt_reset_stats(cpt_ctx* c) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, 8 * sizeof(unsigned long long), c->stream()));
+    return CPT_OK;
+}
+
+int cpt_last_render_ms(cpt_ctx* c, float* ms) {
+    if (!c || !ms) return CPT_ERR_INVALID_ARG;
+    if (!c->have_timing) return fail(c, CPT_ERR_STATE, "cpt_last_render_ms: nothing rendered");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipEventSynchronize(c->ev_stop));
+    HIP_TRY(c, hipEventElapsedTime(ms, c->ev_start, c->ev_stop));
+    c->last_kernel_ms = *ms;
+    return CPT_OK;
+}
+
+int cpt_last_kernel_stats(cpt_ctx* c, float* avg_ms, int* launches) {
+    if (!c || !avg_ms || !launches) return CPT_ERR_INVALID_ARG;
+    float ms = 0.f;
+    int rc = cpt_last_render_ms(c, &ms);
+    if (rc != CPT_OK) return rc;
+    *launches = c->last_launches;
+    *avg_ms = c->last_launches > 0 ? ms / (float)c->last_launches : 0.f;
+    return CPT_OK;
+}
+
+int cpt_denoise_mix(cpt_ctx* c, uint32_t cur_sample_idx, uint8_t* bgra_host) {
+    (void)cur_sample_idx;
+    (void)bgra_host;
+    return c ? fail(c, CPT_ERR_UNSUPPORTED, "cpt_denoise_mix: display path not built yet") : CPT_ERR_INVALID_ARG;
+}
+
+int cpt_math_batch(cpt_ctx* c, int op, const float* a, const float* b, float* out, size_t n) {
+    if (!c || !a || !b || !out) return CPT_ERR_INVALID_ARG;
+    if (n == 0) return CPT_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    float *da = nullptr, *db = nullptr, *dout = nullptr;
+    hipError_t e = hipMalloc((void**)&da, n * 4);
+    if (e == hipSuccess) e = hipMalloc((void**)&db, n * 4);
+    if (e == hipSuccess) e = hipMalloc((void**)&dout, n * 4);
+    if (e == hipSuccess) e = hipMemcpy(da, a, n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(db, b, n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = cpt::launch_math_batch(op, da, db, dout, n, c->stream());
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream());
+    if (e == hipSuccess) e = hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(da);
+    (void)hipFree(db);
+    (void)hipFree(dout);
+    if (e != hipSuccess) return fail(c, CPT_ERR_HIP, "cpt_math_batch: %s", hipGetErrorString(e));
+    return CPT_OK;
+}
+
+}  // extern "C"

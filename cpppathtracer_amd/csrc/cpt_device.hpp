@@ -1,0 +1,306 @@
+// cpt_device.hpp — device-side building blocks of the integrator (gfx950).
+//
+// Every function here restates a piece of the reference hot path with the reference's
+// floating-point semantics (file:line cited per function).  Compiled with
+// -ffp-contract=off and IEEE f32/f64 division and sqrt, so each expression rounds exactly as
+// written; transcendentals use the deterministic double-precision sequences defined in
+// DESIGN.md §Numerics (same sequences as the CPU oracle), so GPU and oracle agree bit for bit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cpt {
+
+// ------------------------------------------------------------------------------------
+// float3 with the vendored helper_math.h semantics (Common/helper_math.h).
+// ------------------------------------------------------------------------------------
+struct v3 { float x, y, z; };
+
+__device__ __forceinline__ v3 mk(float x, float y, float z) { return v3{x, y, z}; }
+__device__ __forceinline__ v3 mk1(float s) { return v3{s, s, s}; }
+__device__ __forceinline__ v3 operator+(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ v3 operator-(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ v3 operator*(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ v3 operator*(float s, v3 a) { return mk(s * a.x, s * a.y, s * a.z); }   // :834-837
+__device__ __forceinline__ v3 operator*(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ v3 operator/(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }   // :1013-1016
+__device__ __forceinline__ v3 operator-(v3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }  // :1264-1267
+__device__ __forceinline__ v3 normalize(v3 v) {                                                  // :1325-1329
+    float inv = 1.0f / __builtin_sqrtf(dot(v, v));   // host-path rsqrtf = 1/sqrtf (:78-81)
+    return v * inv;
+}
+__device__ __forceinline__ v3 cross(v3 a, v3 b) {                                               // :1436-1439
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ v3 reflect(v3 i, v3 n) { return i - (2.0f * n) * dot(n, i); }        // :1427-1430
+
+// MIN / MAX / ABS ternary macros (ray_tracing_math.hpp:15-26)
+__device__ __forceinline__ float tmin_(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float tmax_(float a, float b) { return a > b ? a : b; }
+
+constexpr float DEFAULT_RAY_TMAX = 1e30f;   // ray_tracing_common.h:11
+constexpr float BOUNCE_RAY_TMIN = 2e-5f;    // ray_tracing_common.h:12
+constexpr uint32_t MAX_RECURSION_DEPTH_SET = 32;  // path_tracer.h:13
+constexpr double REF_PI = 3.14159265358979323846;
+
+// ------------------------------------------------------------------------------------
+// Deterministic transcendentals.  Double-precision sequences with
+// explicit constants; no FMA contraction.  Identical sequences live in the CPU oracle.
+// ------------------------------------------------------------------------------------
+namespace dm {
+
+constexpr double LN2_HI = 6.93147180369123816490e-01;
+constexpr double LN2_LO = 1.90821492927058770002e-10;
+constexpr double INV_LN2 = 1.44269504088896338700e+00;
+constexpr double SQRT2 = 1.41421356237309514547e+00;
+constexpr double PIO2_1 = 1.57079632673412561417e+00;
+constexpr double PIO2_2 = 6.07710050650619224932e-11;
+constexpr double PIO2_3 = 2.02226624879595063154e-21;
+constexpr double TWO_OVER_PI = 6.36619772367581382433e-01;
+constexpr double PI_2_D = 1.57079632679489655800e+00;
+
+__device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
+__device__ __forceinline__ double bitsd(uint64_t u) { return __longlong_as_double((long long)u); }
+
+__device__ inline double log_pos(double x) {
+    // x > 0, finite (callers handle the special cases)
+    uint64_t u = dbits(x);
+    int e = (int)((u >> 52) & 0x7ff);
+    if (e == 0) {
+        x = x * 18014398509481984.0;
+        u = dbits(x);
+        e = (int)((u >> 52) & 0x7ff) - 54;
+    }
+    e -= 1023;
+    double m = bitsd((u & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL);
+    if (m > SQRT2) { m = m * 0.5; e += 1; }
+    double f = m - 1.0;
+    double s = f / (2.0 + f);
+    double s2 = s * s;
+    double p = 1.0 / 25.0;
+    p = 1.0 / 23.0 + s2 * p;
+    p = 1.0 / 21.0 + s2 * p;
+    p = 1.0 / 19.0 + s2 * p;
+    p = 1.0 / 17.0 + s2 * p;
+    p = 1.0 / 15.0 + s2 * p;
+    p = 1.0 / 13.0 + s2 * p;
+    p = 1.0 / 11.0 + s2 * p;
+    p = 1.0 / 9.0 + s2 * p;
+    p = 1.0 / 7.0 + s2 * p;
+    p = 1.0 / 5.0 + s2 * p;
+    p = 1.0 / 3.0 + s2 * p;
+    double r = 2.0 * s + 2.0 * s * (s2 * p);
+    double de = (double)e;
+    return de * LN2_HI + (r + de * LN2_LO);
+}
+
+__device__ inline double log(double x) {
+    if (!(x > 0.0)) return x == 0.0 ? -__builtin_inf() : __builtin_nan("");
+    if (x == __builtin_inf()) return x;
+    return log_pos(x);
+}
+
+__device__ __forceinline__ double ldexp_(double x, int k) {
+    if (k > 1023) { x = x * bitsd(0x7fe0000000000000ULL); k -= 1023; if (k > 1023) k = 1023; }
+    if (k < -1022) { x = x * bitsd(0x0010000000000000ULL); k += 1022; if (k < -1022) k = -1022; }
+    return x * bitsd((uint64_t)(k + 1023) << 52);
+}
+
+__device__ inline double exp(double x) {
+    if (x != x) return x;
+    if (x > 709.782712893384) return __builtin_inf();
+    if (x < -745.1332191019412) return 0.0;
+    double k = __builtin_floor(x * INV_LN2 + 0.5);
+    double r = (x - k * LN2_HI) - k * LN2_LO;
+    double p = 1.0 / 6227020800.0;
+    p = 1.0 / 479001600.0 + r * p;
+    p = 1.0 / 39916800.0 + r * p;
+    p = 1.0 / 3628800.0 + r * p;
+    p = 1.0 / 362880.0 + r * p;
+    p = 1.0 / 40320.0 + r * p;
+    p = 1.0 / 5040.0 + r * p;
+    p = 1.0 / 720.0 + r * p;
+    p = 1.0 / 120.0 + r * p;
+    p = 1.0 / 24.0 + r * p;
+    p = 1.0 / 6.0 + r * p;
+    p = 0.5 + r * p;
+    p = 1.0 + r * p;
+    p = 1.0 + r * p;
+    return ldexp_(p, (int)k);
+}
+
+__device__ inline double pow(double x, double y) {
+    if (y == 0.0) return 1.0;
+    if (x == 1.0) return 1.0;
+    if (x != x || y != y) return __builtin_nan("");
+    if (x == 0.0) return y > 0.0 ? 0.0 : __builtin_inf();
+    if (x < 0.0) {
+        double yi = __builtin_floor(y);
+        if (yi != y) return __builtin_nan("");
+        double m = exp(y * log(-x));
+        double half = y * 0.5;
+        return (__builtin_floor(half) != half) ? -m : m;
+    }
+    if (x == __builtin_inf()) return y > 0.0 ? __builtin_inf() : 0.0;
+    return exp(y * log_pos(x));
+}
+
+__device__ __forceinline__ float powf_(float x, float y) { return (float)pow((double)x, (double)y); }
+
+__device__ inline double sin_poly(double r) {
+    double r2 = r * r;
+    double p = -1.0 / 121645100408832000.0;
+    p = 1.0 / 355687428096000.0 + r2 * p;
+    p = -1.0 / 1307674368000.0 + r2 * p;
+    p = 1.0 / 6227020800.0 + r2 * p;
+    p = -1.0 / 39916800.0 + r2 * p;
+    p = 1.0 / 362880.0 + r2 * p;
+    p = -1.0 / 5040.0 + r2 * p;
+    p = 1.0 / 120.0 + r2 * p;
+    p = -1.0 / 6.0 + r2 * p;
+    return r + r * (r2 * p);
+}
+
+__device__ inline double cos_poly(double r) {
+    double r2 = r * r;
+    double p = 1.0 / 2432902008176640000.0;
+    p = -1.0 / 6402373705728000.0 + r2 * p;
+    p = 1.0 / 20922789888000.0 + r2 * p;
+    p = -1.0 / 87178291200.0 + r2 * p;
+    p = 1.0 / 479001600.0 + r2 * p;
+    p = -1.0 / 3628800.0 + r2 * p;
+    p = 1.0 / 40320.0 + r2 * p;
+    p = -1.0 / 720.0 + r2 * p;
+    p = 1.0 / 24.0 + r2 * p;
+    p = -0.5 + r2 * p;
+    return 1.0 + r2 * p;
+}
+
+__device__ __forceinline__ double reduce(double x, int* q) {
+    double k = __builtin_floor(x * TWO_OVER_PI + 0.5);
+    double r = ((x - k * PIO2_1) - k * PIO2_2) - k * PIO2_3;
+    double km = k - 4.0 * __builtin_floor(k * 0.25);
+    *q = (int)km;
+    return r;
+}
+
+// sinf and cosf of the same argument (the BSDF lobes always need both).
+__device__ inline void sincosf_(float xf, float* s_out, float* c_out) {
+    double x = (double)xf;
+    if (x != x || x == __builtin_inf() || x == -__builtin_inf()) {
+        *s_out = __builtin_nanf("");
+        *c_out = __builtin_nanf("");
+        return;
+    }
+    int q;
+    double r = reduce(x, &q);
+    double sp = sin_poly(r), cp = cos_poly(r);
+    double s, c;
+    switch (q) {
+        case 0: s = sp; c = cp; break;
+        case 1: s = cp; c = -sp; break;
+        case 2: s = -sp; c = -cp; break;
+        default: s = -cp; c = sp; break;
+    }
+    *s_out = (float)s;
+    *c_out = (float)c;
+}
+
+__device__ inline double atan(double t) {
+    if (t != t) return t;
+    double sgn = 1.0;
+    double a = t;
+    if (a < 0.0) { a = -a; sgn = -1.0; }
+    if (a == __builtin_inf()) return sgn * PI_2_D;
+    bool inv = false;
+    if (a > 1.0) { a = 1.0 / a; inv = true; }
+    a = a / (1.0 + __builtin_sqrt(1.0 + a * a));
+    a = a / (1.0 + __builtin_sqrt(1.0 + a * a));
+    double a2 = a * a;
+    double p = -1.0 / 27.0;
+    p = 1.0 / 25.0 + a2 * p;
+    p = -1.0 / 23.0 + a2 * p;
+    p = 1.0 / 21.0 + a2 * p;
+    p = -1.0 / 19.0 + a2 * p;
+    p = 1.0 / 17.0 + a2 * p;
+    p = -1.0 / 15.0 + a2 * p;
+    p = 1.0 / 13.0 + a2 * p;
+    p = -1.0 / 11.0 + a2 * p;
+    p = 1.0 / 9.0 + a2 * p;
+    p = -1.0 / 7.0 + a2 * p;
+    p = 1.0 / 5.0 + a2 * p;
+    p = -1.0 / 3.0 + a2 * p;
+    double r = 4.0 * (a + a * (a2 * p));
+    if (inv) r = PI_2_D - r;
+    return sgn * r;
+}
+
+__device__ __forceinline__ float atanf_(float x) { return (float)atan((double)x); }
+
+__device__ inline float asinf_(float xf) {
+    double x = (double)xf;
+    if (x != x) return __builtin_nanf("");
+    if (x > 1.0 || x < -1.0) return __builtin_nanf("");
+    if (x == 1.0) return (float)PI_2_D;
+    if (x == -1.0) return (float)(-PI_2_D);
+    return (float)atan(x / __builtin_sqrt((1.0 - x) * (1.0 + x)));
+}
+
+}  // namespace dm
+
+// ------------------------------------------------------------------------------------
+// cuRAND XORWOW (curand_kernel.h restated).  State lives in registers
+// for a whole render; HBM holds it planar [6][npix] between renders.
+// ------------------------------------------------------------------------------------
+struct Xorwow { uint32_t v0, v1, v2, v3, v4, d; };
+
+__device__ __forceinline__ uint32_t xorwow_next(Xorwow& s) {
+    uint32_t t = s.v0 ^ (s.v0 >> 2);
+    s.v0 = s.v1; s.v1 = s.v2; s.v2 = s.v3; s.v3 = s.v4;
+    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+    s.d += 362437u;
+    return s.v4 + s.d;
+}
+
+// curand_uniform: x * 2^-32 + 2^-33 (the product is exact; result in (0, 1]).
+__device__ __forceinline__ float uniform(Xorwow& s) {
+    uint32_t x = xorwow_next(s);
+    return (float)x * 2.3283064e-10f + (2.3283064e-10f / 2.0f);
+}
+
+// ------------------------------------------------------------------------------------
+// Scene data in HBM (DESIGN.md §Data layout)
+// ------------------------------------------------------------------------------------
+// BVH node, 32 B, right-first preorder ("skip-link" order): the node after n in memory is
+// its right child (the child the reference's DFS pops first, bvh.cu:201-202); `miss` is the
+// next node in that order once n's subtree is skipped or finished.
+struct __attribute__((aligned(16))) Node {
+    float bmin_x, bmin_y, bmin_z;
+    int32_t miss;
+    float bmax_x, bmax_y, bmax_z;
+    int32_t prim;         // >= 0: leaf holding primitive `prim`; -1: internal node
+};
+
+// Primitive, 32 B: the geometric part of Object (object.h:17-32).
+struct __attribute__((aligned(16))) Prim {
+    float cx, cy, cz, radius;
+    float y_pos, height;
+    int32_t type;
+    int32_t material;
+};
+
+// Material, 48 B: Material (material.h:17-35) + per-material constants prepared once on the
+// device (alpha = powf(1000, smoothness) and 1.0/(double)alpha, material.cu:43,69,103).
+struct __attribute__((aligned(16))) Mat {
+    float kd_x, kd_y, kd_z, emit;
+    float ior, smoothness, reflectivity;
+    int32_t type;
+    double inv_alpha;
+    double pad_;
+};
+
+struct Ray { v3 o, d; float tmin, tmax; };
+
+}  // namespace cpt

@@ -1,0 +1,47 @@
+// cpt_internal.hpp — shared between the HIP kernels and the C-ABI implementation.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cpt_device.hpp"
+
+namespace cpt {
+
+// Camera snapshot as the kernel needs it (the reference passes the whole MotionalCamera by
+// value in PathTracerParams, path_tracer.cu:14-27; only these fields are read by RayGen).
+struct CamK {
+    float origin[3];
+    float u[3], v[3];
+    float top_left[3], horizontal[3], vertical[3];
+    float lens_radius;
+    int width, height;
+};
+
+// Kernel arguments (passed by value: they land in the kernarg segment and are read with
+// scalar loads).
+struct KParams {
+    const Node* nodes;
+    const Prim* prims;
+    const Mat* mats;
+    int n_nodes;
+    const uint32_t* env;    // packed RGBA8, env_cols x env_h
+    int env_w, env_h, env_cols;
+    CamK cam;
+    const int32_t* rows;    // global row index per context row
+    int n_rows, width;
+    uint32_t* rng;          // planar [6][n_rows*width]
+    float4* accum;          // [n_rows*width] rgb sums + pass count
+    float* normal;          // [n_rows*width][3] (AUX)
+    float* depth;           // [n_rows*width]    (AUX)
+    unsigned long long* stats;  // [5]           (STATS)
+    int spp, max_depth, accumulate;
+};
+
+hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t stream);
+hipError_t launch_prepare_materials(Mat* mats, int n, hipStream_t stream);
+hipError_t launch_init_rng(const uint32_t* jumps, const uint32_t seed_state[6], int width, const int32_t* rows,
+                           int n_rows, uint32_t* scratch_w, uint32_t* scratch_mats, uint32_t* rng, hipStream_t stream);
+hipError_t launch_math_batch(int op, const float* a, const float* b, float* out, size_t n, hipStream_t stream);
+
+}  // namespace cpt

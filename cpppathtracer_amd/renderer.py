@@ -1,0 +1,173 @@
+"""Host-side driver over the C-ABI: one ``Renderer`` = one ``cpt_ctx`` on one GPU.
+
+This is the Python view of the reference's PathTracer pipeline (path_tracer.cu:44-115,
+256-319) for tests, the benchmark and multi-GPU tiling; C++ users get the same through
+include/cpppathtracer/path_tracer.h.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import (CPT_RENDER_ACCUMULATE, CPT_RENDER_AUX, CPT_RENDER_STATS, CPT_RENDER_SYNC, CptError, check)
+from .types import CAMERA_DTYPE, OBJECT_DTYPE
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def device_count() -> int:
+    L = _lib.load()
+    n = ctypes.c_int(0)
+    check(L.cpt_get_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def camera_get_copy(cam):
+    """MotionalCamera::GetCopy on a CAMERA_DTYPE value (returns the updated copy)."""
+    L = _lib.load()
+    c = np.array(cam, dtype=CAMERA_DTYPE, copy=True)
+    check(L.cpt_camera_get_copy(_p(c)))
+    return c
+
+
+class Renderer:
+    def __init__(self, device: int = 0):
+        self._L = _lib.load()
+        h = ctypes.c_void_p()
+        st = self._L.cpt_create(device, ctypes.byref(h))
+        if st != 0:
+            raise CptError(st, (self._L.cpt_last_error(None) or b"").decode())
+        self._ctx = h
+        self.device = device
+        self.width = self.height = self.n_rows = 0
+        self.rows = None
+
+    # -- lifecycle -------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._L.cpt_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, st):
+        return check(st, self._ctx)
+
+    # -- setup -----------------------------------------------------------------------
+    def set_stream(self, hip_stream_handle):
+        self._check(self._L.cpt_set_stream(self._ctx, ctypes.c_void_p(hip_stream_handle or 0)))
+
+    def set_scene(self, objs):
+        objs = np.ascontiguousarray(objs, dtype=OBJECT_DTYPE)
+        self._check(self._L.cpt_set_scene(self._ctx, _p(objs) if len(objs) else None, len(objs)))
+
+    def update_object(self, index, obj):
+        o = np.array(obj, dtype=OBJECT_DTYPE, copy=True)
+        self._check(self._L.cpt_update_object(self._ctx, index, _p(o)))
+
+    def bvh_export(self):
+        n = ctypes.c_int(0)
+        self._check(self._L.cpt_scene_bvh_export(self._ctx, None, None, 0, ctypes.byref(n)))
+        m = n.value
+        boxes = np.zeros((max(m, 1), 6), dtype=np.float32)
+        links = np.zeros((max(m, 1), 4), dtype=np.int32)
+        self._check(self._L.cpt_scene_bvh_export(self._ctx, _p(boxes), _p(links), m, ctypes.byref(n)))
+        return boxes[:m], links[:m]
+
+    def set_env(self, env):
+        """env: texture_io.EnvTexture (or None for a black environment)."""
+        if env is None:
+            self._check(self._L.cpt_set_env_texture(self._ctx, None, 1, 1, 0))
+            return
+        rgba = np.ascontiguousarray(env.rgba, dtype=np.uint8)
+        self._check(self._L.cpt_set_env_texture(self._ctx, _p(rgba), env.width, env.height, env.valid_cols))
+
+    def set_frame(self, width, height, rows=None):
+        if rows is None:
+            self._check(self._L.cpt_set_frame(self._ctx, width, height, None, 0))
+            self.rows = np.arange(height, dtype=np.int32)
+        else:
+            r = np.ascontiguousarray(rows, dtype=np.int32)
+            self._check(self._L.cpt_set_frame(self._ctx, width, height, _p(r), r.size))
+            self.rows = r
+        self.width, self.height, self.n_rows = width, height, int(self.rows.size)
+
+    def init_rng(self, seed):
+        self._check(self._L.cpt_init_rng(self._ctx, ctypes.c_uint64(seed)))
+
+    # -- render ----------------------------------------------------------------------
+    def render(self, cam, spp, max_depth, accumulate=False, aux=False, stats=False, sync=False, flags=0):
+        c = np.ascontiguousarray(np.array(cam, dtype=CAMERA_DTYPE))
+        f = flags
+        f |= CPT_RENDER_ACCUMULATE if accumulate else 0
+        f |= CPT_RENDER_AUX if aux else 0
+        f |= CPT_RENDER_STATS if stats else 0
+        f |= CPT_RENDER_SYNC if sync else 0
+        self._check(self._L.cpt_render(self._ctx, _p(c), spp, max_depth, f))
+
+    def synchronize(self):
+        self._check(self._L.cpt_synchronize(self._ctx))
+
+    def last_render_ms(self) -> float:
+        ms = ctypes.c_float(0)
+        self._check(self._L.cpt_last_render_ms(self._ctx, ctypes.byref(ms)))
+        return float(ms.value)
+
+    # -- readback --------------------------------------------------------------------
+    @property
+    def npix(self):
+        return self.n_rows * self.width
+
+    def read_accum(self):
+        out = np.zeros((self.npix, 4), dtype=np.float32)
+        self._check(self._L.cpt_read_accum(self._ctx, _p(out)))
+        return out
+
+    def clear_accum(self):
+        self._check(self._L.cpt_clear_accum(self._ctx))
+
+    def read_rng(self):
+        out = np.zeros((6, self.npix), dtype=np.uint32)
+        self._check(self._L.cpt_read_rng(self._ctx, _p(out)))
+        return out
+
+    def write_rng(self, planar6):
+        a = np.ascontiguousarray(planar6, dtype=np.uint32)
+        assert a.shape == (6, self.npix)
+        self._check(self._L.cpt_write_rng(self._ctx, _p(a)))
+
+    def read_aux(self):
+        n = np.zeros((self.npix, 3), dtype=np.float32)
+        d = np.zeros(self.npix, dtype=np.float32)
+        self._check(self._L.cpt_read_aux(self._ctx, _p(n), _p(d)))
+        return n, d
+
+    def copy_accum_device(self, device_ptr, nbytes):
+        self._check(self._L.cpt_copy_accum_device(self._ctx, ctypes.c_void_p(device_ptr), nbytes))
+
+    def stats(self):
+        s = (ctypes.c_uint64 * 5)()
+        self._check(self._L.cpt_get_stats(self._ctx, s))
+        return dict(zip(("segments", "nodes", "prims", "hits", "misses"), (int(x) for x in s)))
+
+    def reset_stats(self):
+        self._check(self._L.cpt_reset_stats(self._ctx))
+
+    def math_batch(self, op, a, b=None):
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        b = np.ascontiguousarray(b if b is not None else np.zeros_like(a), dtype=np.float32)
+        out = np.empty_like(a)
+        self._check(self._L.cpt_math_batch(self._ctx, op, _p(a), _p(b), _p(out), a.size))
+        return out

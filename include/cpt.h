@@ -1,0 +1,203 @@
+/*
+ * cpt.h — C-ABI of the MI355X path-tracing integrator (libcpt.so).
+ *
+ * This is the drop-in boundary for the reference's hot path (DearPoca/CppPathTracer,
+ * cuSrc/path_tracer.cu:124-175 `SamplePixel` and everything it reaches).  Plain C types
+ * only: no HIP, CUDA or torch types cross it.  Every function returns an int status
+ * (0 = CPT_OK); no exception crosses the ABI.  The reference logs CUDA errors and
+ * continues (path_tracer.cu:54-57, 279-283); here the status is returned and the message
+ * is kept in cpt_last_error().
+ *
+ * Which reference interface each entry point replaces (file:line under the reference):
+ *
+ *   cpt_create / cpt_destroy        PathTracer construction + InitBuffers' cudaMallocs
+ *                                   (path_tracer.cu:44-115); the reference never frees.
+ *   cpt_set_scene                   SceneBVH::AddObject + BuildBVH + BuildBVHInGpu
+ *                                   (bvh.cu:22-29, 116-120, 97-114), reached from
+ *                                   PathTracer::AddObject / InitPipeline (path_tracer.cu:29-34, 308-314).
+ *   cpt_update_object               SceneBVH::UpdateObject (bvh.cu:144-157).
+ *   cpt_set_env_texture             PocaTextureUtils::AddTexByFile (textures.cu:14-62) +
+ *                                   the sky load in InitBuffers (path_tracer.cu:47).
+ *   cpt_set_frame                   InitBuffers' per-pixel buffers (path_tracer.cu:44-115),
+ *                                   plus a row window/list for multi-GPU row tiling.
+ *   cpt_init_rng                    InitCuRand kernel (path_tracer.cu:36-42, 99-107).
+ *   cpt_camera_get_copy             MotionalCamera::GetCopy (motional_camera.cu:177-200).
+ *   cpt_render                      The SamplePixel launch in PipelineLoop
+ *                                   (path_tracer.cu:264-283), `spp` passes at once.
+ *   cpt_read_accum / cpt_read_aux   The per-pixel render_target / normal / depth buffers
+ *                                   written by SamplePixel (path_tracer.cu:172-174).
+ *   cpt_denoise_mix                 Denoising + Mix + BGRA8 readback (path_tracer.cu:177-254,
+ *                                   285-303).
+ */
+#ifndef CPT_H_
+#define CPT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CPT_ABI_VERSION 1
+
+enum cpt_status {
+    CPT_OK = 0,
+    CPT_ERR_INVALID_ARG = 1,
+    CPT_ERR_NO_DEVICE = 2,
+    CPT_ERR_HIP = 3,
+    CPT_ERR_OUT_OF_MEMORY = 4,
+    CPT_ERR_STATE = 5,       /* e.g. render before scene/frame/rng were set */
+    CPT_ERR_UNSUPPORTED = 6
+};
+
+/* PrimitiveType::Enum (object.h:7-15) and MaterialType::Enum (material.h:5-15). */
+enum cpt_primitive_type { CPT_PRIM_SPHERE = 0, CPT_PRIM_PLATFORM = 1, CPT_PRIM_CYLINDER = 2 };
+enum cpt_material_type {
+    CPT_MAT_DIFFUSE = 0,
+    CPT_MAT_METAL = 1,   /* shaded by MirrorHitShader (material.cu:151-153 swap, kept) */
+    CPT_MAT_MIRROR = 2,  /* shaded by MetalHitShader  (material.cu:154-156 swap, kept) */
+    CPT_MAT_GLASS = 3,
+    CPT_MAT_TEST = 4     /* falls through to Diffuse (material.cu:160-161) */
+};
+
+/* Layout-identical to CUDA float3 (12 bytes, 4-byte aligned). */
+typedef struct cpt_float3 { float x, y, z; } cpt_float3;
+
+/* Material (material.h:17-35), 40 bytes. */
+typedef struct cpt_material {
+    int32_t type;              /* @0  cpt_material_type */
+    uint8_t have_tex;          /* @4  textured materials: not supported yet (CPT_ERR_UNSUPPORTED) */
+    uint8_t pad_[3];
+    union {                    /* @8  union { float3 kd_; cudaTextureObject_t tex_; } */
+        cpt_float3 kd;
+        uint64_t tex;
+    } u;
+    float refractive_index;    /* @24 */
+    float emit_intensity;      /* @28 */
+    float smoothness;          /* @32 */
+    float reflectivity;        /* @36 */
+} cpt_material;
+
+/* Object (object.h:17-32), 72 bytes. */
+typedef struct cpt_object {
+    int32_t type;              /* @0  cpt_primitive_type */
+    int32_t pad_;
+    cpt_material material;     /* @8  */
+    cpt_float3 center;         /* @48 */
+    float radius;              /* @60 sphere, cylinder */
+    float y_pos;               /* @64 platform */
+    float height;              /* @68 cylinder */
+} cpt_object;
+
+/* MotionalCamera (motional_camera.h:8-24), 136 bytes.  u/v/w/top_left/horizontal/vertical
+ * are the GetCopy() outputs; cpt_camera_get_copy() fills them. */
+typedef struct cpt_camera {
+    cpt_float3 vup;            /* @0   */
+    int32_t width, height;     /* @12, @16 */
+    uint32_t cur_sample_idx;   /* @20  */
+    cpt_float3 origin;         /* @24  */
+    cpt_float3 look_at;        /* @36  */
+    float view_fov;            /* @48  degrees */
+    float dist_to_focus;       /* @52  */
+    float lens_radius;         /* @56  */
+    float move_speed;          /* @60  */
+    cpt_float3 u, v, w;        /* @64, @76, @88 */
+    cpt_float3 top_left_corner;/* @100 */
+    cpt_float3 horizontal;     /* @112 */
+    cpt_float3 vertical;       /* @124 */
+} cpt_camera;
+
+/* Per-render counters for the algorithmic byte model. */
+typedef struct cpt_stats {
+    uint64_t segments;     /* TraceRay calls                          */
+    uint64_t node_visits;  /* non-sentinel nodes popped (bvh.cu:173)  */
+    uint64_t prim_tests;   /* IntersectionTest calls (bvh.cu:176)     */
+    uint64_t hits;
+    uint64_t misses;
+} cpt_stats;
+
+typedef struct cpt_ctx cpt_ctx;
+
+/* cpt_render flags */
+#define CPT_RENDER_ACCUMULATE 0x1u   /* add into the accumulator instead of overwriting it   */
+#define CPT_RENDER_AUX        0x2u   /* write first-hit normal + depth of the last pass       */
+#define CPT_RENDER_STATS      0x4u   /* count segments/nodes/prims/hits/misses (slower)       */
+#define CPT_RENDER_SYNC       0x8u   /* block until the render finished                        */
+#define CPT_PATH_MEGAKERNEL   0x000u /* per-lane path regeneration megakernel (default)        */
+#define CPT_PATH_WAVEFRONT    0x100u /* SoA wavefront: extend / shade / compact per bounce      */
+
+int cpt_abi_version(void);
+const char* cpt_status_string(int status);
+int cpt_get_device_count(int* count);
+
+int cpt_create(int device, cpt_ctx** out);
+int cpt_destroy(cpt_ctx* ctx);
+/* Last error message of ctx (or of the last failed cpt_create when ctx is NULL). */
+const char* cpt_last_error(const cpt_ctx* ctx);
+/* Launch on `hip_stream` (a hipStream_t) instead of the context's own stream; NULL restores it. */
+int cpt_set_stream(cpt_ctx* ctx, void* hip_stream);
+
+/* Host-side MotionalCamera::GetCopy: computes the basis and corner vectors, increments
+ * cur_sample_idx (motional_camera.cu:177-200). */
+int cpt_camera_get_copy(cpt_camera* cam);
+
+/* Builds the reference's median-split BVH over `objs` (objects copied by value, like
+ * bvh.cu:43) and uploads it.  n_objs may be 0 (every ray misses). */
+int cpt_set_scene(cpt_ctx* ctx, const cpt_object* objs, int n_objs);
+/* Replace object `index` (AddObject order) and refit the ancestors' boxes. */
+int cpt_update_object(cpt_ctx* ctx, int index, const cpt_object* obj);
+/* Exports the BVH in the reference's node order (Divide creation order): per node
+ * boxes[6] = {min xyz, max xyz}, links[4] = {is_object, left, right, object index}. */
+int cpt_scene_bvh_export(cpt_ctx* ctx, float* boxes, int32_t* links, int capacity, int* n_nodes);
+/* Same BVH build without a context or a GPU (host only), same export format. */
+int cpt_bvh_build_host(const cpt_object* objs, int n_objs, float* boxes, int32_t* links, int capacity, int* n_nodes);
+
+/* Environment map, RGBA8 rows of `valid_cols` texels (the reference uploads only
+ * logical_width/4 texels per row, textures.cu:32-33; texels at x >= valid_cols read 0).
+ * Sampler: normalized coords, mirror addressing, bilinear, c/255 (textures.cu:36-44). */
+int cpt_set_env_texture(cpt_ctx* ctx, const uint8_t* rgba, int logical_width, int height, int valid_cols);
+
+/* Per-pixel buffers for a width x height frame; the context renders the global image rows
+ * listed in `rows` (n_rows of them; rows == NULL means 0..height-1).  Pixel i of the
+ * context's buffers is (x = i % width, y = rows[i / width]). */
+int cpt_set_frame(cpt_ctx* ctx, int width, int height, const int32_t* rows, int n_rows);
+/* curand_init(seed, (x << 32) | y, 0) for every pixel of the context (InitCuRand). */
+int cpt_init_rng(cpt_ctx* ctx, uint64_t seed);
+int cpt_read_rng(cpt_ctx* ctx, uint32_t* planar6);          /* [6][n_rows*width]: v0..v4, d */
+int cpt_write_rng(cpt_ctx* ctx, const uint32_t* planar6);
+
+/* `spp` SamplePixel passes for every pixel of the context, each pass continuing the
+ * pixel's XORWOW stream; the accumulator holds rgb sums + pass count per pixel.
+ * max_depth in [0, 32] (MAX_RECURSION_DEPTH_SET, path_tracer.h:13).  Asynchronous unless
+ * CPT_RENDER_SYNC. */
+int cpt_render(cpt_ctx* ctx, const cpt_camera* cam, int spp, int max_depth, uint32_t flags);
+int cpt_synchronize(cpt_ctx* ctx);
+int cpt_read_accum(cpt_ctx* ctx, float* rgba);               /* [n_rows*width][4] */
+int cpt_clear_accum(cpt_ctx* ctx);
+int cpt_read_aux(cpt_ctx* ctx, float* normal3, float* depth); /* either may be NULL */
+/* Device-to-device copy of the accumulator (e.g. into an RCCL send buffer). */
+int cpt_copy_accum_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
+int cpt_get_stats(cpt_ctx* ctx, cpt_stats* out);
+int cpt_reset_stats(cpt_ctx* ctx);
+/* Device time of the last cpt_render (HIP events on the launch stream); waits for it. */
+int cpt_last_render_ms(cpt_ctx* ctx, float* ms);
+/* Average device time of one kernel launch of the last cpt_render's dominant kernel. */
+int cpt_last_kernel_stats(cpt_ctx* ctx, float* avg_ms, int* launches);
+
+/* Display path (path_tracer.cu:177-254): 5x5 edge-aware denoise of the current 1-spp
+ * radiance (accumulator / pass count), running-mean Mix with weight 1/cur_sample_idx,
+ * BGRA8 out (alpha byte untouched).  Needs a full frame (rows == NULL). */
+int cpt_denoise_mix(cpt_ctx* ctx, uint32_t cur_sample_idx, uint8_t* bgra_host);
+
+/* Device-math known-answer surface used by the parity tests: op 0 powf(a,b), 1 sinf(a),
+ * 2 cosf(a), 3 asinf(a), 4 atanf(a), 5 (float)pow((double)a, 1.0/(double)b),
+ * 6 (float)((double)a / (double)b) [IEEE f64 division], 7 a / b [f32 division],
+ * 8 sqrtf(a). */
+int cpt_math_batch(cpt_ctx* ctx, int op, const float* a, const float* b, float* out, size_t n);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif  /* CPT_H_ */

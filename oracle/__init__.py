@@ -55,6 +55,8 @@ def lib():
         L.or_uniform.restype = f32
         L.or_seq_jump_matrix_pow4.argtypes = [i32, P]
         L.or_seq_jump_matrix_pow4.restype = None
+        L.or_jump_matrix_pow4.argtypes = [i32, P]
+        L.or_jump_matrix_pow4.restype = None
         L.or_init_rng.argtypes = [u64, i32, P, i32, P, i32]
         L.or_init_rng.restype = None
         L.or_camera_get_copy.argtypes = [P]
@@ -88,6 +90,12 @@ def curand_init(seed: int, subsequence: int) -> np.ndarray:
 def seq_jump_matrix_pow4(t: int) -> np.ndarray:
     out = np.zeros(800, dtype=np.uint32)
     lib().or_seq_jump_matrix_pow4(t, _ptr(out))
+    return out
+
+
+def jump_matrix_pow4(t: int) -> np.ndarray:
+    out = np.zeros(800, dtype=np.uint32)
+    lib().or_jump_matrix_pow4(t, _ptr(out))
     return out
 
 

@@ -1024,6 +1024,19 @@ void or_seq_jump_matrix_pow4(int t, uint32_t out[800]) {
     std::memcpy(out, J.seq[2 * t].m, sizeof(uint32_t) * 800);
 }
 
+// A^(4^t) in rocRAND layout (compare: h_xorwow_jump_matrices[t]) — pins the transition.
+void or_jump_matrix_pow4(int t, uint32_t out[800]) {
+    BitMat A;
+    for (int c = 0; c < 160; ++c) {
+        Xorwow s{};
+        s.v[c / 32] = 1u << (c % 32);
+        xorwow_next(s);
+        std::memcpy(&A.m[c * 5], s.v, 20);
+    }
+    for (int i = 0; i < 2 * t; ++i) A = matmul(A, A);
+    std::memcpy(out, A.m, sizeof(uint32_t) * 800);
+}
+
 // InitCuRand (path_tracer.cu:36-42): per pixel curand_init(seed, (x<<32)|y, 0).
 void or_init_rng(uint64_t seed, int width, const int32_t* rows, int n_rows, uint32_t* rng_planar, int nthreads) {
     jump_tables();

@@ -1,0 +1,189 @@
+"""GPU parity: the HIP kernels in libcpt.so vs the CPU oracle, bit for bit.
+
+The integrator is integer RNG + IEEE float arithmetic with FMA contraction off on both
+sides and deterministic transcendentals, so the bar here is exact equality of the
+per-pixel radiance sums, the XORWOW end states and the traversal counters — stronger than
+the north star's RMSE < 1e-4 (which test_gpu_full_size checks at full size).
+"""
+import numpy as np
+import pytest
+
+from cpppathtracer_amd import camera_get_copy, scenes, types
+
+pytestmark = pytest.mark.gpu
+RNG = np.random.default_rng(11)
+
+
+# ------------------------------------------------------------------------------ math
+@pytest.mark.parametrize("op", [1, 2, 3, 4])
+def test_unary_math_bitexact(gpu, oracle_mod, op):
+    x = np.concatenate([
+        (RNG.random(300000) * 2 * np.pi).astype(np.float32),
+        ((RNG.random(100000) - 0.5) * 2e4).astype(np.float32),
+        (RNG.random(100000) * 2 - 1).astype(np.float32),
+        np.tan((RNG.random(100000) - 0.5) * np.pi).astype(np.float32),
+        np.array([0, -0.0, 1, -1, 1e-30, -1e-38, 1e-45, np.inf, -np.inf, np.nan, 3.4e38], np.float32),
+    ])
+    g = gpu.math_batch(op, x)
+    o = oracle_mod.math_batch(op, x)
+    np.testing.assert_array_equal(g.view(np.uint32), o.view(np.uint32))
+
+
+@pytest.mark.parametrize("op", [0, 5])
+def test_binary_pow_bitexact(gpu, oracle_mod, op):
+    a = np.concatenate([RNG.random(200000).astype(np.float32) + np.float32(2 ** -33),
+                        (RNG.random(50000) * 2 - 0.5).astype(np.float32),
+                        np.array([0, 1, -2, np.nan, np.inf, 1e-40], np.float32)])
+    b = np.concatenate([(RNG.random(200000) * 6).astype(np.float32),
+                        np.full(50000, 5.0, np.float32),
+                        np.array([5, 3, 5, 2, 2, 0.5], np.float32)])
+    if op == 0:
+        a[:200000] = 1000.0
+    else:
+        b = np.abs(b) + np.float32(1.0)
+    g = gpu.math_batch(op, a, b)
+    o = oracle_mod.math_batch(op, a, b)
+    np.testing.assert_array_equal(g.view(np.uint32), o.view(np.uint32))
+
+
+def test_ieee_div_sqrt(gpu):
+    a = (RNG.standard_normal(500000) * 10.0 ** RNG.integers(-30, 30, 500000)).astype(np.float32)
+    b = (RNG.standard_normal(500000) * 10.0 ** RNG.integers(-30, 30, 500000)).astype(np.float32)
+    np.testing.assert_array_equal(gpu.math_batch(7, a, b).view(np.uint32), (a / b).view(np.uint32))
+    np.testing.assert_array_equal(gpu.math_batch(6, a, b).view(np.uint32),
+                                  (a.astype(np.float64) / b.astype(np.float64)).astype(np.float32).view(np.uint32))
+    s = np.abs(a)
+    np.testing.assert_array_equal(gpu.math_batch(8, s).view(np.uint32), np.sqrt(s).view(np.uint32))
+
+
+# ------------------------------------------------------------------------------- rng
+@pytest.mark.parametrize("w,rows", [(64, list(range(64))), (3840, [0, 1, 7, 1079, 2159]),
+                                    (333, [5, 3, 200, 3])])
+def test_rng_init_bitexact(gpu, oracle_mod, w, rows):
+    gpu.set_frame(w, max(rows) + 1, rows)
+    gpu.init_rng(1234)
+    g = gpu.read_rng()
+    o = oracle_mod.init_rng(1234, w, np.array(rows, np.int32), threads=8)
+    np.testing.assert_array_equal(g, o)
+
+
+# ------------------------------------------------------------------------- integrator
+def _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, rows=None, seed=1234, aux=False, env=True):
+    rows = np.arange(H, dtype=np.int32) if rows is None else np.asarray(rows, np.int32)
+    cam = camera_get_copy(scenes.camera_for(W, H))
+    gpu.set_scene(objs)
+    gpu.set_env(sky if env else None)
+    gpu.set_frame(W, H, rows)
+    gpu.init_rng(seed)
+    gpu.reset_stats()
+    gpu.render(cam, spp, depth, aux=aux, stats=True, sync=True)
+    g_acc, g_rng, g_st = gpu.read_accum(), gpu.read_rng(), gpu.stats()
+    g_aux = gpu.read_aux() if aux else None
+    rng = oracle_mod.init_rng(seed, W, rows, threads=8)
+    o_acc, o_st, o_n, o_d = oracle_mod.render(objs, cam, sky if env else None, rows, spp, depth, rng,
+                                             want_aux=aux, threads=8)
+    return (g_acc, g_rng, g_st, g_aux), (o_acc, rng, o_st, (o_n, o_d))
+
+
+CASES = [
+    ("s3", 64, 64, 4, 4),
+    ("s3", 67, 33, 3, 8),
+    ("s4", 64, 48, 4, 16),
+    ("s4", 40, 40, 2, 32),
+    ("s1000", 64, 36, 2, 16),
+    ("s1000", 96, 54, 1, 8),
+]
+
+
+@pytest.mark.parametrize("name,W,H,spp,depth", CASES)
+def test_render_bitexact(gpu, oracle_mod, sky, name, W, H, spp, depth):
+    objs = scenes.SCENES[name]()
+    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth)
+    np.testing.assert_array_equal(gr, orng)
+    assert gs == os_
+    np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
+    assert np.isfinite(ga).all() and (ga[:, 3] == spp).all()
+
+
+def test_render_aux_bitexact(gpu, oracle_mod, sky):
+    objs = scenes.scene_s4()
+    (ga, gr, gs, (gn, gd)), (oa, orng, os_, (on, od)) = _run_both(gpu, oracle_mod, sky, objs, 48, 32, 2, 8, aux=True)
+    np.testing.assert_array_equal(gn.view(np.uint32), on.view(np.uint32))
+    np.testing.assert_array_equal(gd, od)
+    assert (gd == np.float32(1e30)).all()   # depth quirk (a18): TraceRay gets the ray by value
+
+
+def test_row_subset_and_order(gpu, oracle_mod, sky):
+    """Any row list (tiles, interleaved blocks, unsorted, repeated) gives per-row results
+    identical to the monolithic render: a pixel's stream depends only on (seed, x, y)."""
+    objs = scenes.scene_s1000()
+    W, H = 48, 40
+    (ga, gr, _, _), _ = _run_both(gpu, oracle_mod, sky, objs, W, H, 2, 8)
+    rows = [39, 0, 17, 17, 5]
+    (sa, sr, _, _), (oa, orng, _, _) = _run_both(gpu, oracle_mod, sky, objs, W, H, 2, 8, rows=rows)
+    np.testing.assert_array_equal(sa, oa)
+    full = ga.reshape(H, W, 4)
+    np.testing.assert_array_equal(sa.reshape(len(rows), W, 4), full[rows])
+
+
+@pytest.mark.parametrize("depth", [0, 1])
+def test_tiny_depths(gpu, oracle_mod, sky, depth):
+    objs = scenes.scene_s4()
+    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, objs, 32, 16, 3, depth)
+    np.testing.assert_array_equal(gr, orng)
+    np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
+    assert gs == os_
+
+
+def test_empty_scene_and_no_env(gpu, oracle_mod, sky):
+    empty = np.zeros(0, dtype=types.OBJECT_DTYPE)
+    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, empty, 32, 16, 2, 8)
+    np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
+    np.testing.assert_array_equal(gr, orng)
+    assert gs["hits"] == 0 and gs == os_
+    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, scenes.scene_s3(), 32, 16, 2, 8, env=False)
+    np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
+
+
+def test_single_object_and_cylinders(gpu, oracle_mod, sky):
+    objs = scenes.scene_s1000(n=3)
+    for sl in (slice(0, 1), slice(1, 2), slice(0, 4)):
+        o = np.ascontiguousarray(objs[sl])
+        (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, o, 40, 24, 2, 8)
+        np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
+        assert gs == os_
+
+
+def test_accumulate_and_spp0(gpu, oracle_mod, sky):
+    objs = scenes.scene_s3()
+    W, H = 32, 32
+    cam = camera_get_copy(scenes.camera_for(W, H))
+    gpu.set_scene(objs)
+    gpu.set_env(sky)
+    gpu.set_frame(W, H)
+    gpu.init_rng(99)
+    gpu.render(cam, 0, 4, sync=True)
+    assert (gpu.read_accum() == 0).all()
+    gpu.render(cam, 2, 4, sync=True)
+    gpu.render(cam, 3, 4, accumulate=True, sync=True)
+    a = gpu.read_accum()
+    rng = oracle_mod.init_rng(99, W, np.arange(H, dtype=np.int32))
+    acc, _, _, _ = oracle_mod.render(objs, cam, sky, np.arange(H, dtype=np.int32), 2, 4, rng)
+    acc, _, _, _ = oracle_mod.render(objs, cam, sky, np.arange(H, dtype=np.int32), 3, 4, rng, accum=acc,
+                                     accumulate=True)
+    np.testing.assert_array_equal(a.view(np.uint32), acc.view(np.uint32))
+    assert (a[:, 3] == 5).all()
+
+
+def test_invalid_arguments(gpu):
+    from cpppathtracer_amd import CptError
+    cam = camera_get_copy(scenes.camera_for(16, 16))
+    gpu.set_scene(scenes.scene_s3())
+    gpu.set_frame(16, 16)
+    gpu.init_rng(1)
+    with pytest.raises(CptError):
+        gpu.render(cam, 1, 33)
+    with pytest.raises(CptError):
+        gpu.render(camera_get_copy(scenes.camera_for(8, 16)), 1, 4)
+    with pytest.raises(CptError):
+        gpu.set_frame(16, 16, [16])
