@@ -46,6 +46,7 @@ PROTOTYPES = {
     "cpt_last_kernel_stats": (_I, [_P, _P, _P]),
     "cpt_denoise_mix": (_I, [_P, _U32, _P]),
     "cpt_math_batch": (_I, [_P, _I, _P, _P, _P, _SZ]),
+    "cpt_selftest_qdiv": (_I, [_P, _I, _U64, _U64, _P, _I]),
 }
 
 CPT_RENDER_ACCUMULATE = 0x1
@@ -71,7 +72,7 @@ def load(build_if_missing: bool = True):
     global _lib
     if _lib is not None:
         return _lib
-    path = _build.LIB_PATH
+    path = os.environ.get("CPT_LIB_PATH") or _build.LIB_PATH   # CPT_LIB_PATH: A/B builds only
     if not os.path.exists(path):
         if not build_if_missing:
             raise CptError(-1, f"{path} missing: run __graft_entry__.build() (hipcc) first")

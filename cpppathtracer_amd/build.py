@@ -62,16 +62,19 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: str = None, defines=()) -> str:
+    """Build libcpt.so; `out`/`defines` produce A/B variants (e.g. defines=["CPT_LDS=0"])."""
+    target = out or LIB_PATH
+    if not force and out is None and not defines and not needs_build():
         return LIB_PATH
-    tmp = LIB_PATH + ".tmp"
-    cmd = [_hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO_DIR, "include"), "-o", tmp, *_extra_sources()]
+    tmp = target + ".tmp"
+    cmd = [_hipcc(), *HIPCC_FLAGS, *[f"-D{d}" for d in defines], "-I", os.path.join(REPO_DIR, "include"), "-o", tmp,
+           *_extra_sources()]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":

@@ -28,7 +28,6 @@ namespace {
 
 using cpt::Mat;
 using cpt::Node;
-using cpt::Prim;
 
 std::string g_create_error;
 
@@ -141,9 +140,28 @@ void build_host_bvh(HostBvh& b, const std::vector<cpt_object>& objs) {
     b.nodes[0].parent = -1;
 }
 
+// Node contents: internal -> its box; leaf -> the primitive inline (cpt_device.hpp Node).
+Node make_node(const BNode& n, const std::vector<cpt_object>& objs, const std::vector<int>& mat_of_obj) {
+    Node g;
+    if (n.is_object) {
+        const cpt_object& o = objs[n.obj];
+        g.a0 = o.center.x; g.a1 = o.center.y; g.a2 = o.center.z;
+        g.b0 = o.radius; g.b1 = o.y_pos; g.b2 = o.height;
+        int type = (o.type >= 0 && o.type <= 2) ? o.type : 3;
+        g.code = (mat_of_obj[n.obj] << 2) | type;
+    } else {
+        g.a0 = n.bmin.x; g.a1 = n.bmin.y; g.a2 = n.bmin.z;
+        g.b0 = n.bmax.x; g.b1 = n.bmax.y; g.b2 = n.bmax.z;
+        g.code = -1;
+    }
+    g.miss = -1;
+    return g;
+}
+
 // Right-first preorder = the order the reference's stack DFS pops nodes (left pushed first,
-// bvh.cu:201-202).  skip[i] = position after node i's subtree.
-void linearise(const HostBvh& b, std::vector<Node>& out, std::vector<int>& pos_of_node) {
+// bvh.cu:201-202).  miss[i] = position after node i's subtree.
+void linearise(const HostBvh& b, const std::vector<cpt_object>& objs, const std::vector<int>& mat_of_obj,
+               std::vector<Node>& out, std::vector<int>& pos_of_node) {
     out.clear();
     pos_of_node.assign(b.nodes.size(), -1);
     if (b.nodes.empty()) return;
@@ -156,12 +174,7 @@ void linearise(const HostBvh& b, std::vector<Node>& out, std::vector<int>& pos_o
         const BNode& n = b.nodes[f.node];
         if (f.stage == 0) {
             pos_of_node[f.node] = (int)out.size();
-            Node g;
-            g.bmin_x = n.bmin.x; g.bmin_y = n.bmin.y; g.bmin_z = n.bmin.z;
-            g.bmax_x = n.bmax.x; g.bmax_y = n.bmax.y; g.bmax_z = n.bmax.z;
-            g.prim = n.is_object ? n.obj : -1;
-            g.miss = -1;
-            out.push_back(g);
+            out.push_back(make_node(n, objs, mat_of_obj));
             if (n.is_object) {
                 out[pos_of_node[f.node]].miss = (int)out.size();
                 st.pop_back();
@@ -258,12 +271,11 @@ struct cpt_ctx {
     HostBvh bvh;
     std::vector<Node> lin;
     std::vector<int> pos_of_node;
-    std::vector<Prim> prims_h;
-    std::vector<Mat> mats_h;
+    std::vector<Mat> mats_h;           // deduplicated materials
+    std::vector<int> mat_of_obj;       // object index -> material index
     Node* d_nodes = nullptr;
-    Prim* d_prims = nullptr;
     Mat* d_mats = nullptr;
-    size_t cap_nodes = 0, cap_prims = 0, cap_mats = 0;
+    size_t cap_nodes = 0, cap_mats = 0;
     bool scene_set = false;
 
     // environment
@@ -287,6 +299,7 @@ struct cpt_ctx {
     uint32_t* d_scratch_m = nullptr;
 
     unsigned long long* d_stats = nullptr;
+    uint32_t* d_work = nullptr;
     float last_kernel_ms = 0.f;
     int last_launches = 0;
 
@@ -335,17 +348,6 @@ void free_frame(cpt_ctx* c) {
     c->frame_set = c->rng_set = false;
 }
 
-Prim to_prim(const cpt_object& o, int mat_index) {
-    Prim p;
-    p.cx = o.center.x; p.cy = o.center.y; p.cz = o.center.z;
-    p.radius = o.radius;
-    p.y_pos = o.y_pos;
-    p.height = o.height;
-    p.type = o.type;
-    p.material = mat_index;
-    return p;
-}
-
 Mat to_mat(const cpt_material& m) {
     Mat g;
     g.kd_x = m.u.kd.x; g.kd_y = m.u.kd.y; g.kd_z = m.u.kd.z;
@@ -359,17 +361,22 @@ Mat to_mat(const cpt_material& m) {
     return g;
 }
 
+int material_slot(cpt_ctx* c, const cpt_material& m) {
+    Mat g = to_mat(m);
+    for (size_t i = 0; i < c->mats_h.size(); ++i)
+        if (std::memcmp(&c->mats_h[i], &g, sizeof(Mat)) == 0) return (int)i;
+    c->mats_h.push_back(g);
+    return (int)c->mats_h.size() - 1;
+}
+
 int upload_scene(cpt_ctx* c) {
     HIP_TRY(c, hipSetDevice(c->device));
     int rc;
     if ((rc = ensure(c, &c->d_nodes, &c->cap_nodes, std::max<size_t>(1, c->lin.size()))) != CPT_OK) return rc;
-    if ((rc = ensure(c, &c->d_prims, &c->cap_prims, std::max<size_t>(1, c->prims_h.size()))) != CPT_OK) return rc;
     if ((rc = ensure(c, &c->d_mats, &c->cap_mats, std::max<size_t>(1, c->mats_h.size()))) != CPT_OK) return rc;
     hipStream_t s = c->stream();
     if (!c->lin.empty())
         HIP_TRY(c, hipMemcpyAsync(c->d_nodes, c->lin.data(), c->lin.size() * sizeof(Node), hipMemcpyHostToDevice, s));
-    if (!c->prims_h.empty())
-        HIP_TRY(c, hipMemcpyAsync(c->d_prims, c->prims_h.data(), c->prims_h.size() * sizeof(Prim), hipMemcpyHostToDevice, s));
     if (!c->mats_h.empty()) {
         HIP_TRY(c, hipMemcpyAsync(c->d_mats, c->mats_h.data(), c->mats_h.size() * sizeof(Mat), hipMemcpyHostToDevice, s));
         HIP_TRY(c, cpt::launch_prepare_materials(c->d_mats, (int)c->mats_h.size(), s));
@@ -421,6 +428,7 @@ int cpt_create(int device, cpt_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&c->ev_start);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_stop);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_work, 64);
     if (e == hipSuccess) e = hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long));
     if (e == hipSuccess) {
         const std::vector<uint32_t>& J = jump_tables();
@@ -443,11 +451,11 @@ int cpt_destroy(cpt_ctx* c) {
     if (c->user_stream) (void)hipStreamSynchronize(c->user_stream);
     free_frame(c);
     (void)hipFree(c->d_nodes);
-    (void)hipFree(c->d_prims);
     (void)hipFree(c->d_mats);
     (void)hipFree(c->d_env);
     (void)hipFree(c->d_jumps);
     (void)hipFree(c->d_stats);
+    (void)hipFree(c->d_work);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -504,13 +512,11 @@ int cpt_set_scene(cpt_ctx* c, const cpt_object* objs, int n) {
         }
         c->objs.assign(objs, objs + n);
         build_host_bvh(c->bvh, c->objs);
-        linearise(c->bvh, c->lin, c->pos_of_node);
-        c->prims_h.resize(n);
-        c->mats_h.resize(n);
-        for (int i = 0; i < n; ++i) {
-            c->prims_h[i] = to_prim(c->objs[i], i);   // one material per object (copied by value, bvh.cu:43)
-            c->mats_h[i] = to_mat(c->objs[i].material);
-        }
+        // Objects carry their Material by value (bvh.cu:43); identical materials share one slot.
+        c->mats_h.clear();
+        c->mat_of_obj.assign(n, 0);
+        for (int i = 0; i < n; ++i) c->mat_of_obj[i] = material_slot(c, c->objs[i].material);
+        linearise(c->bvh, c->objs, c->mat_of_obj, c->lin, c->pos_of_node);
     } catch (const std::bad_alloc&) {
         return fail(c, CPT_ERR_OUT_OF_MEMORY, "cpt_set_scene: host allocation failed");
     }
@@ -525,6 +531,7 @@ int cpt_update_object(cpt_ctx* c, int index, const cpt_object* obj) {
         return fail(c, CPT_ERR_INVALID_ARG, "cpt_update_object: index %d out of range", index);
     if (obj->material.have_tex) return fail(c, CPT_ERR_UNSUPPORTED, "cpt_update_object: textured material");
     c->objs[index] = *obj;
+    c->mat_of_obj[index] = material_slot(c, obj->material);
     int ni = c->bvh.leaf_of_object[index];
     while (ni != -1) {
         BNode& n = c->bvh.nodes[ni];
@@ -538,12 +545,11 @@ int cpt_update_object(cpt_ctx* c, int index, const cpt_object* obj) {
             n.bmin = F3{MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z)};
         }
         Node& g = c->lin[c->pos_of_node[ni]];
-        g.bmin_x = n.bmin.x; g.bmin_y = n.bmin.y; g.bmin_z = n.bmin.z;
-        g.bmax_x = n.bmax.x; g.bmax_y = n.bmax.y; g.bmax_z = n.bmax.z;
+        int miss = g.miss;
+        g = make_node(n, c->objs, c->mat_of_obj);
+        g.miss = miss;
         ni = n.parent;
     }
-    c->prims_h[index] = to_prim(c->objs[index], index);
-    c->mats_h[index] = to_mat(c->objs[index].material);
     return upload_scene(c);
 }
 
@@ -699,7 +705,6 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     cpt::KParams p;
     std::memset(&p, 0, sizeof(p));
     p.nodes = c->d_nodes;
-    p.prims = c->d_prims;
     p.mats = c->d_mats;
     p.n_nodes = (int)c->lin.size();
     p.env = c->d_env;
@@ -725,6 +730,7 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     p.normal = c->d_normal;
     p.depth = c->d_depth;
     p.stats = c->d_stats;
+    p.work = c->d_work;
     p.spp = spp;
     p.max_depth = max_depth;
     p.accumulate = (flags & CPT_RENDER_ACCUMULATE) ? 1 : 0;
@@ -847,6 +853,20 @@ int cpt_math_batch(cpt_ctx* c, int op, const float* a, const float* b, float* ou
     (void)hipFree(db);
     (void)hipFree(dout);
     if (e != hipSuccess) return fail(c, CPT_ERR_HIP, "cpt_math_batch: %s", hipGetErrorString(e));
+    return CPT_OK;
+}
+
+int cpt_selftest_qdiv(cpt_ctx* c, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len) {
+    if (!c || !out || out_len < 1 || which < 0 || which > 2) return CPT_ERR_INVALID_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    unsigned long long* d = nullptr;
+    HIP_TRY(c, hipMalloc((void**)&d, out_len * sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(d, 0, out_len * sizeof(unsigned long long), c->stream());
+    if (e == hipSuccess) e = cpt::launch_selftest_qdiv(which, n, seed, d, out_len, c->stream());
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream());
+    if (e == hipSuccess) e = hipMemcpy(out, d, out_len * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(c, CPT_ERR_HIP, "cpt_selftest_qdiv: %s", hipGetErrorString(e));
     return CPT_OK;
 }
 

@@ -276,20 +276,18 @@ __device__ __forceinline__ float uniform(Xorwow& s) {
 // BVH node, 32 B, right-first preorder ("skip-link" order): the node after n in memory is
 // its right child (the child the reference's DFS pops first, bvh.cu:201-202); `miss` is the
 // next node in that order once n's subtree is skipped or finished.
+//   internal (code < 0): a = AABB min, b = AABB max
+//   leaf     (code >= 0): the primitive inline (a leaf's own box is never tested: in the
+//            reference its slab test only decides whether to push two -1 sentinels):
+//            a = center, b = {radius, y_pos, height}, code = material << 2 | type
+//            (type 3 = unknown PrimitiveType: IntersectionTest returns false, object.cu:126)
 struct __attribute__((aligned(16))) Node {
-    float bmin_x, bmin_y, bmin_z;
+    float a0, a1, a2;
     int32_t miss;
-    float bmax_x, bmax_y, bmax_z;
-    int32_t prim;         // >= 0: leaf holding primitive `prim`; -1: internal node
+    float b0, b1, b2;
+    int32_t code;
 };
-
-// Primitive, 32 B: the geometric part of Object (object.h:17-32).
-struct __attribute__((aligned(16))) Prim {
-    float cx, cy, cz, radius;
-    float y_pos, height;
-    int32_t type;
-    int32_t material;
-};
+static_assert(sizeof(Node) == 32, "Node is 32 B");
 
 // Material, 48 B: Material (material.h:17-35) + per-material constants prepared once on the
 // device (alpha = powf(1000, smoothness) and 1.0/(double)alpha, material.cu:43,69,103).
@@ -302,5 +300,43 @@ struct __attribute__((aligned(16))) Mat {
 };
 
 struct Ray { v3 o, d; float tmin, tmax; };
+
+// ------------------------------------------------------------------------------------
+// Exact f32 quotients through a per-ray double reciprocal.
+//
+// qdiv_raw(a, y) with y = RN_f64(1 / (double)d) equals RN_f32(a / d), the IEEE f32 quotient,
+// whenever that quotient is a normal number, infinite, NaN, or a is +-0:
+//   * (double)a and y are exact / correctly rounded, so the product has relative error
+//     < 2^-52 before the final rounding to f32;
+//   * a quotient of two 24-bit significands in the normal range is never a f32 rounding
+//     midpoint (the product of an odd 25-bit and a 24-bit integer has >= 25 significant
+//     bits) and is >= 2^-50 (relative) away from every midpoint, so the double result rounds
+//     to the same f32 (the innocuous double-rounding bound p' >= 2p + 2 for division);
+//   * d = +-0 gives y = +-inf and a*y = +-inf / NaN exactly as a/d.
+// Subnormal (and underflowed-to-zero) quotients CAN sit exactly on a midpoint (d with few
+// significant bits), where the rounded reciprocal breaks the tie the wrong way; qdiv() and
+// the slab test fall back to the IEEE divide whenever |q| < 2^-126.  k_selftest_qdiv checks
+// qdiv against v_div_* on 4.3e9 hashed pairs per operand family.
+// One reciprocal per ray and axis replaces the 11-instruction IEEE divide sequence per slab
+// plane and per intersector root.
+// ------------------------------------------------------------------------------------
+#ifndef CPT_QDIV
+#define CPT_QDIV 1     // CPT_QDIV=0 builds plain IEEE divides everywhere (A/B builds only)
+#endif
+constexpr float FLT_MIN_NORMAL = 1.17549435e-38f;   // 2^-126
+
+__device__ __forceinline__ double rcp_d(float d) { return 1.0 / (double)d; }
+__device__ __forceinline__ float qdiv_raw(float a, double y) { return (float)((double)a * y); }
+
+__device__ __forceinline__ float qdiv(float a, float d, double y) {
+#if CPT_QDIV
+    float q = qdiv_raw(a, y);
+    if (__builtin_expect(__builtin_fabsf(q) < FLT_MIN_NORMAL, 0)) q = a / d;
+    return q;
+#else
+    (void)y;
+    return a / d;
+#endif
+}
 
 }  // namespace cpt

@@ -21,9 +21,8 @@ struct CamK {
 // Kernel arguments (passed by value: they land in the kernarg segment and are read with
 // scalar loads).
 struct KParams {
-    const Node* nodes;
-    const Prim* prims;
-    const Mat* mats;
+    const Node* nodes;      // skip-link order, leaves inline (cpt_device.hpp)
+    const Mat* mats;        // deduplicated materials, indexed by Node::code >> 2
     int n_nodes;
     const uint32_t* env;    // packed RGBA8, env_cols x env_h
     int env_w, env_h, env_cols;
@@ -35,6 +34,7 @@ struct KParams {
     float* normal;          // [n_rows*width][3] (AUX)
     float* depth;           // [n_rows*width]    (AUX)
     unsigned long long* stats;  // [5]           (STATS)
+    uint32_t* work;         // pixel dequeue counter (zeroed before each launch)
     int spp, max_depth, accumulate;
 };
 
@@ -43,5 +43,8 @@ hipError_t launch_prepare_materials(Mat* mats, int n, hipStream_t stream);
 hipError_t launch_init_rng(const uint32_t* jumps, const uint32_t seed_state[6], int width, const int32_t* rows,
                            int n_rows, uint32_t* scratch_w, uint32_t* scratch_mats, uint32_t* rng, hipStream_t stream);
 hipError_t launch_math_batch(int op, const float* a, const float* b, float* out, size_t n, hipStream_t stream);
+hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len,
+                                hipStream_t stream);
+int lds_node_capacity();
 
 }  // namespace cpt

@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "cpt_device.hpp"
 #include "cpt_internal.hpp"
 
@@ -62,28 +64,53 @@ __device__ inline v3 tex2d(const KParams& p, float u, float v) {
 }
 
 // ======================================================================================
-// Intersectors (object.cu:10-128).  `tmax` is the traversal's shrinking closest distance.
+// Per-segment ray with its exact reciprocals (see qdiv in cpt_device.hpp).
+// ======================================================================================
+struct RayK {
+    v3 o, d;
+    float tmin;
+    double yx, yy, yz;   // 1/d.x, 1/d.y, 1/d.z   (slab planes; d.y also for caps / platform)
+    double ya;           // 1/dot(d,d)            (sphere roots, object.cu:15-20)
+    double yc;           // 1/(dx*dx + dz*dz)     (cylinder side roots, object.cu:69-79)
+};
+
+__device__ __forceinline__ RayK make_rayk(const Ray& r) {
+    RayK k;
+    k.o = r.o;
+    k.d = r.d;
+    k.tmin = r.tmin;
+    k.yx = rcp_d(r.d.x);
+    k.yy = rcp_d(r.d.y);
+    k.yz = rcp_d(r.d.z);
+    k.ya = rcp_d(dot(r.d, r.d));
+    k.yc = rcp_d(r.d.x * r.d.x + r.d.z * r.d.z);
+    return k;
+}
+
+// ======================================================================================
+// Intersectors (object.cu:10-128) on an inline leaf.  `tmax` is the traversal's shrinking
+// closest distance (TraceRay's by-value ray, bvh.cu:167).
 // ======================================================================================
 struct Hit { v3 normal, pos; };
 
-__device__ __forceinline__ bool sphere_test(const Prim& s, const Ray& ray, float& tmax, Hit& h) {
-    v3 c = mk(s.cx, s.cy, s.cz);
+__device__ __forceinline__ bool sphere_test(const Node& s, const RayK& ray, float& tmax, Hit& h) {
+    const v3 c = mk(s.a0, s.a1, s.a2);
+    const float radius = s.b0;
     v3 A_C = ray.o - c;
-    v3 B = ray.d;
-    float a = dot(B, B);
-    float b = dot(A_C, B);
-    float cc = dot(A_C, A_C) - s.radius * s.radius;
+    float b = dot(A_C, ray.d);
+    float cc = dot(A_C, A_C) - radius * radius;
+    float a = dot(ray.d, ray.d);
     float disc = b * b - a * cc;
     if (disc > 0) {
         float sq = __builtin_sqrtf(disc);
-        float temp = (-b - sq) / a;
+        float temp = qdiv(-b - sq, a, ray.ya);
         if (temp < tmax && temp > ray.tmin) {
             tmax = temp;
             h.pos = ray.o + temp * ray.d;
-            h.normal = (h.pos - c) / s.radius;       // first root: divided by the signed radius
+            h.normal = (h.pos - c) / radius;        // first root: divided by the signed radius
             return true;
         }
-        temp = (-b + sq) / a;
+        temp = qdiv(-b + sq, a, ray.ya);
         if (temp < tmax && temp > ray.tmin) {
             tmax = temp;
             h.pos = ray.o + temp * ray.d;
@@ -94,9 +121,10 @@ __device__ __forceinline__ bool sphere_test(const Prim& s, const Ray& ray, float
     return false;
 }
 
-__device__ __forceinline__ bool platform_test(const Prim& pl, const Ray& ray, float& tmax, Hit& h) {
-    if ((ray.o.y < pl.y_pos && ray.d.y > 0.f) || (ray.o.y > pl.y_pos && ray.d.y < 0.f)) {
-        float temp = (pl.y_pos - ray.o.y) / ray.d.y;
+__device__ __forceinline__ bool platform_test(const Node& pl, const RayK& ray, float& tmax, Hit& h) {
+    const float y_pos = pl.b1;
+    if ((ray.o.y < y_pos && ray.d.y > 0.f) || (ray.o.y > y_pos && ray.d.y < 0.f)) {
+        float temp = qdiv(y_pos - ray.o.y, ray.d.y, ray.yy);
         if (temp < tmax && temp > ray.tmin) {
             tmax = temp;
             h.pos = ray.o + temp * ray.d;
@@ -107,12 +135,13 @@ __device__ __forceinline__ bool platform_test(const Prim& pl, const Ray& ray, fl
     return false;
 }
 
-__device__ __forceinline__ bool cap_test(const Prim& cy, const Ray& ray, float& tmax, Hit& h, float ypos) {
+__device__ __forceinline__ bool cap_test(float cx, float cz, float radius, const RayK& ray, float& tmax, Hit& h,
+                                         float ypos) {
     if ((ray.o.y < ypos && ray.d.y > 0.f) || (ray.o.y > ypos && ray.d.y < 0.f)) {
-        float temp = (ypos - ray.o.y) / ray.d.y;
+        float temp = qdiv(ypos - ray.o.y, ray.d.y, ray.yy);
         v3 hp = ray.o + temp * ray.d;
         if (temp < tmax && temp > ray.tmin &&
-            __builtin_sqrtf((hp.x - cy.cx) * (hp.x - cy.cx) + (hp.z - cy.cz) * (hp.z - cy.cz)) < cy.radius) {
+            __builtin_sqrtf((hp.x - cx) * (hp.x - cx) + (hp.z - cz) * (hp.z - cz)) < radius) {
             tmax = temp;
             h.pos = hp;
             h.normal = normalize(mk(0, -ray.d.y, 0));
@@ -122,35 +151,36 @@ __device__ __forceinline__ bool cap_test(const Prim& cy, const Ray& ray, float& 
     return false;
 }
 
-__device__ inline bool cylinder_test(const Prim& cy, const Ray& ray, float& tmax, Hit& h) {
+__device__ inline bool cylinder_test(const Node& cy, const RayK& ray, float& tmax, Hit& h) {
+    const float ccx = cy.a0, ccy = cy.a1, ccz = cy.a2, r = cy.b0, height = cy.b2;
     bool ret = false;
-    float upper = cy.cy + cy.height / 2;
-    if (cap_test(cy, ray, tmax, h, upper)) ret = true;
-    float lower = cy.cy - cy.height / 2;
-    if (cap_test(cy, ray, tmax, h, lower)) ret = true;
-    float dx = ray.d.x, dz = ray.d.z, r = cy.radius;
-    float cx = ray.o.x - cy.cx;
-    float cz = ray.o.z - cy.cz;
+    float upper = ccy + height / 2;
+    if (cap_test(ccx, ccz, r, ray, tmax, h, upper)) ret = true;
+    float lower = ccy - height / 2;
+    if (cap_test(ccx, ccz, r, ray, tmax, h, lower)) ret = true;
+    float dx = ray.d.x, dz = ray.d.z;
+    float cx = ray.o.x - ccx;
+    float cz = ray.o.z - ccz;
     float a = dx * dx + dz * dz;
     float b = cx * dx + cz * dz;
     float c = cx * cx + cz * cz - r * r;
     float disc = b * b - a * c;
     if (disc > 0.f) {
         float sq = __builtin_sqrtf(disc);
-        float temp = (-b - sq) / a;
+        float temp = qdiv(-b - sq, a, ray.yc);
         v3 hp = ray.o + temp * ray.d;
         if (temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper) {
             tmax = temp;
             h.pos = hp;
-            h.normal = normalize(mk(hp.x - cy.cx, 0.f, hp.z - cy.cz));
+            h.normal = normalize(mk(hp.x - ccx, 0.f, hp.z - ccz));
             ret = true;
         }
-        temp = (-b + sq) / a;
+        temp = qdiv(-b + sq, a, ray.yc);
         hp = ray.o + temp * ray.d;
         if (temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper) {
             tmax = temp;
             h.pos = hp;
-            h.normal = normalize(mk(hp.x - cy.cx, 0.f, hp.z - cy.cz));
+            h.normal = normalize(mk(hp.x - ccx, 0.f, hp.z - ccz));
             ret = true;
         }
     }
@@ -163,52 +193,86 @@ __device__ inline bool cylinder_test(const Prim& cy, const Ray& ray, float& tmax
 // n, then n+1 on a box hit or node.miss on a box miss / after a leaf, reproduces the
 // reference's visit sequence, leaf-before-box order and pruning against the shrinking tmax
 // one for one — no stack, no scratch memory.
+//
+// CPT_WHILEWHILE=1 selects a while-while loop (internal nodes until every lane of the wave
+// sits on a leaf, then the leaf tests together); per-lane visit order is the same either way.
 // ======================================================================================
+#ifndef CPT_WHILEWHILE
+#define CPT_WHILEWHILE 0
+#endif
+#ifndef CPT_WAVES_PER_SIMD
+#define CPT_WAVES_PER_SIMD 3   // occupancy target of k_megakernel (VGPR budget 168)
+#endif
+
 struct Counters { uint32_t segments, nodes, prims, hits, misses; };
 
+// Slab test of one internal node (bvh.cu:181-200).  The six plane distances use the exact
+// quotient; if any of them is zero/subnormal the node is redone with the IEEE divide.
+__device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, float tmax) {
+    float t0x = qdiv_raw(nd.a0 - ray.o.x, ray.yx), t1x = qdiv_raw(nd.b0 - ray.o.x, ray.yx);
+    float t0y = qdiv_raw(nd.a1 - ray.o.y, ray.yy), t1y = qdiv_raw(nd.b1 - ray.o.y, ray.yy);
+    float t0z = qdiv_raw(nd.a2 - ray.o.z, ray.yz), t1z = qdiv_raw(nd.b2 - ray.o.z, ray.yz);
+#if CPT_QDIV
+    float mn = __builtin_fminf(__builtin_fminf(__builtin_fminf(__builtin_fabsf(t0x), __builtin_fabsf(t1x)),
+                                               __builtin_fminf(__builtin_fabsf(t0y), __builtin_fabsf(t1y))),
+                               __builtin_fminf(__builtin_fabsf(t0z), __builtin_fabsf(t1z)));
+    if (__builtin_expect(mn < FLT_MIN_NORMAL, 0)) {
+#else
+    {
+#endif
+        t0x = (nd.a0 - ray.o.x) / ray.d.x; t1x = (nd.b0 - ray.o.x) / ray.d.x;
+        t0y = (nd.a1 - ray.o.y) / ray.d.y; t1y = (nd.b1 - ray.o.y) / ray.d.y;
+        t0z = (nd.a2 - ray.o.z) / ray.d.z; t1z = (nd.b2 - ray.o.z) / ray.d.z;
+    }
+    float lo = -DEFAULT_RAY_TMAX * 2, hi = DEFAULT_RAY_TMAX * 2;
+    if (ray.d.x != 0.f) { lo = tmax_(lo, tmin_(t0x, t1x)); hi = tmin_(hi, tmax_(t0x, t1x)); }
+    if (ray.d.y != 0.f) { lo = tmax_(lo, tmin_(t0y, t1y)); hi = tmin_(hi, tmax_(t0y, t1y)); }
+    if (ray.d.z != 0.f) { lo = tmax_(lo, tmin_(t0z, t1z)); hi = tmin_(hi, tmax_(t0z, t1z)); }
+    return lo > hi || lo > tmax || hi < ray.tmin;
+}
+
+__device__ __forceinline__ bool leaf_test(const Node& nd, const RayK& ray, float& tmax, Hit& h) {
+    const int type = nd.code & 3;
+    if (type == 0) return sphere_test(nd, ray, tmax, h);
+    if (type == 2) return cylinder_test(nd, ray, tmax, h);
+    if (type == 1) return platform_test(nd, ray, tmax, h);
+    return false;
+}
+
 template <bool STATS>
-__device__ inline bool trace(const KParams& p, const Ray& ray, Hit& h, int& prim_out, Counters& cnt) {
-    float tmax = ray.tmax;
+__device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_nodes, const RayK& ray, Hit& h,
+                                      int& code_out, Counters& cnt) {
+    float tmax = DEFAULT_RAY_TMAX;
     bool hit = false;
     int ni = 0;
-    const int n_nodes = p.n_nodes;
+#if CPT_WHILEWHILE
     while (ni < n_nodes) {
-        const Node nd = p.nodes[ni];
+        Node nd = nodes[ni];
+        while (nd.code < 0) {
+            if (STATS) cnt.nodes++;
+            ni = slab_reject(nd, ray, tmax) ? nd.miss : ni + 1;
+            if (ni >= n_nodes) break;
+            nd = nodes[ni];
+        }
+        if (ni >= n_nodes) break;
+        if (STATS) { cnt.nodes++; cnt.prims++; }
+        if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
+        ni = nd.miss;
+    }
+#else
+    while (ni < n_nodes) {
+        const Node nd = nodes[ni];
         if (STATS) cnt.nodes++;
-        if (nd.prim >= 0) {
+        if (nd.code >= 0) {
+            // leaf: IntersectionTest first (bvh.cu:175-180); its own box test is moot
             if (STATS) cnt.prims++;
-            const Prim pr = p.prims[nd.prim];
-            bool r;
-            if (pr.type == 0) r = sphere_test(pr, ray, tmax, h);
-            else if (pr.type == 1) r = platform_test(pr, ray, tmax, h);
-            else if (pr.type == 2) r = cylinder_test(pr, ray, tmax, h);
-            else r = false;
-            if (r) { hit = true; prim_out = nd.prim; }
-            ni = nd.miss;   // the leaf's own slab test only decides whether to push (-1,-1)
+            if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
+            ni = nd.miss;
         } else {
-            float lo = -DEFAULT_RAY_TMAX * 2, hi = DEFAULT_RAY_TMAX * 2;
-            if (ray.d.x != 0.f) {
-                float t0 = (nd.bmin_x - ray.o.x) / ray.d.x;
-                float t1 = (nd.bmax_x - ray.o.x) / ray.d.x;
-                lo = tmax_(lo, tmin_(t0, t1));
-                hi = tmin_(hi, tmax_(t0, t1));
-            }
-            if (ray.d.y != 0.f) {
-                float t0 = (nd.bmin_y - ray.o.y) / ray.d.y;
-                float t1 = (nd.bmax_y - ray.o.y) / ray.d.y;
-                lo = tmax_(lo, tmin_(t0, t1));
-                hi = tmin_(hi, tmax_(t0, t1));
-            }
-            if (ray.d.z != 0.f) {
-                float t0 = (nd.bmin_z - ray.o.z) / ray.d.z;
-                float t1 = (nd.bmax_z - ray.o.z) / ray.d.z;
-                lo = tmax_(lo, tmin_(t0, t1));
-                hi = tmin_(hi, tmax_(t0, t1));
-            }
-            bool reject = lo > hi || lo > tmax || hi < ray.tmin;
-            ni = reject ? nd.miss : ni + 1;
+            ni = slab_reject(nd, ray, tmax) ? nd.miss : ni + 1;
         }
     }
+#endif
     return hit;
 }
 
@@ -351,98 +415,156 @@ __device__ __forceinline__ uint64_t wave_sum(uint32_t v) {
 }
 
 // ======================================================================================
-// k_megakernel — SamplePixel (path_tracer.cu:124-175) for `spp` consecutive passes.
+// k_megakernel — SamplePixel (path_tracer.cu:124-175) for `spp` consecutive passes, as a
+// persistent kernel.
 //
-// One lane owns one pixel for the whole launch: the XORWOW state, the path state and the
-// pass accumulator stay in VGPRs; HBM is touched once per pixel on entry (24 B rng + 16 B
-// accumulator) and once on exit.  When a lane's path ends it immediately starts the
-// pixel's next pass (per-lane path regeneration), so a wave stays full until its lanes run
-// out of passes — the pixel's passes are sequential anyway (the RNG stream persists across
-// passes, a16).  Waves cover 8x8 pixel tiles so first-bounce rays of a wave are coherent.
+// A lane owns one pixel at a time: the pixel's XORWOW state, path state and pass
+// accumulator stay in VGPRs; HBM is touched once when the lane takes the pixel (24 B rng +
+// 16 B accumulator) and once when it has run all `spp` passes.  A lane whose path ends
+// starts the pixel's next pass at once; a lane whose pixel is finished takes the next pixel
+// from a device-wide counter (one aggregated atomic per wave and refill), so every lane of
+// every wave does useful work until the image runs out — no per-pass kernel boundaries and
+// no idle lanes behind a wave's slowest path.  Pixels are handed out in 8x8 tiles so a fresh
+// wave starts coherent.  LDS variant: the BVH (32 B nodes, leaves inline) is staged in LDS
+// once per resident block.
 // ======================================================================================
-template <bool STATS, bool AUX>
-__global__ void __launch_bounds__(256) k_megakernel(const KParams p) {
-    const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+struct Lane {
+    int x, y;
+    size_t pix;
+    Xorwow s;
+    v3 sum;
+    float passes;
+    int left;
+};
+
+__device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int& x, int& ri) {
     const int tiles_x = (p.width + 7) >> 3;
-    const int tx = wave % tiles_x, ty = wave / tiles_x;
-    const int x = tx * 8 + (lane & 7);
-    const int ri = ty * 8 + (lane >> 3);
+    const uint32_t tile = id >> 6, k = id & 63;
+    x = (int)(tile % tiles_x) * 8 + (int)(k & 7);
+    ri = (int)(tile / tiles_x) * 8 + (int)(k >> 3);
+    return x < p.width && ri < p.n_rows;
+}
+
+template <bool STATS, bool AUX, bool LDS>
+__global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVES_PER_SIMD) k_megakernel(const KParams p) {
+    extern __shared__ Node lds_nodes[];
+    if (LDS) {
+        const float4* src = reinterpret_cast<const float4*>(p.nodes);
+        float4* dst = reinterpret_cast<float4*>(lds_nodes);
+        for (int i = threadIdx.x; i < 2 * p.n_nodes; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
+    const Node* __restrict__ nodes = LDS ? lds_nodes : p.nodes;
+    const int lane = threadIdx.x & 63;
+    const size_t npix = (size_t)p.n_rows * p.width;
+    const uint32_t n_work = (uint32_t)(((p.width + 7) >> 3) * ((p.n_rows + 7) >> 3)) * 64u;
+    const uint32_t max_depth = (uint32_t)p.max_depth;
     Counters cnt{0, 0, 0, 0, 0};
-    const bool active = x < p.width && ri < p.n_rows;
-    if (active) {
-        const int y = p.rows[ri];
-        const size_t npix = (size_t)p.n_rows * p.width;
-        const size_t pix = (size_t)ri * p.width + x;
-        Xorwow s;
-        s.v0 = p.rng[pix];
-        s.v1 = p.rng[npix + pix];
-        s.v2 = p.rng[2 * npix + pix];
-        s.v3 = p.rng[3 * npix + pix];
-        s.v4 = p.rng[4 * npix + pix];
-        s.d = p.rng[5 * npix + pix];
-        float4 acc = p.accumulate ? p.accum[pix] : make_float4(0.f, 0.f, 0.f, 0.f);
-        v3 sum = mk(acc.x, acc.y, acc.z);
-        float passes = acc.w;
-        v3 first_normal = mk1(0.f);
-        float first_depth = 0.f;
-        const uint32_t max_depth = (uint32_t)p.max_depth;
-        int left = p.spp;
-        if (left > 0 && max_depth == 0) {
-            // while (0 < 0) never runs: each pass is RayGen's three draws and zero radiance.
-            for (; left > 0; --left) {
-                (void)ray_gen(p, x, y, s);
-                sum = sum + mk1(0.f);
-                passes += 1.0f;
+
+    Lane L;
+    bool busy = false;
+    bool exhausted = false;      // wave-uniform: the counter ran past n_work
+    Ray ray;
+    v3 att = mk1(1.f), rad = mk1(0.f);
+    uint32_t depth = 0;
+    bool first = true;
+    v3 nrm_acc = mk1(0.f), first_normal = mk1(0.f);
+    float dep_acc = 0.f, first_depth = 0.f;
+
+    for (;;) {
+        // ---- refill idle lanes with new pixels (wave-aggregated dequeue) ----------------
+        if (!exhausted) {
+            const uint64_t need = __ballot(!busy);
+            if (need) {
+                const int leader = __ffsll((unsigned long long)need) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(p.work, (uint32_t)__popcll(need));
+                base = __shfl(base, leader);
+                if (base + (uint32_t)__popcll(need) >= n_work) exhausted = true;
+                if (!busy) {
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                    const uint32_t id = base + rank;
+                    int x, ri;
+                    if (id < n_work && decode_pixel(p, id, x, ri)) {
+                        L.x = x;
+                        L.y = p.rows[ri];
+                        L.pix = (size_t)ri * p.width + x;
+                        L.s.v0 = p.rng[L.pix];
+                        L.s.v1 = p.rng[npix + L.pix];
+                        L.s.v2 = p.rng[2 * npix + L.pix];
+                        L.s.v3 = p.rng[3 * npix + L.pix];
+                        L.s.v4 = p.rng[4 * npix + L.pix];
+                        L.s.d = p.rng[5 * npix + L.pix];
+                        float4 acc = p.accumulate ? p.accum[L.pix] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        L.sum = mk(acc.x, acc.y, acc.z);
+                        L.passes = acc.w;
+                        L.left = p.spp;
+                        first_normal = mk1(0.f);
+                        first_depth = 0.f;
+                        if (max_depth == 0) {
+                            // while (0 < 0) never runs: each pass is RayGen's draws and zero radiance
+                            for (; L.left > 0; --L.left) {
+                                (void)ray_gen(p, L.x, L.y, L.s);
+                                L.sum = L.sum + mk1(0.f);
+                                L.passes += 1.0f;
+                            }
+                        }
+                        busy = true;
+                        if (L.left > 0) {
+                            ray = ray_gen(p, L.x, L.y, L.s);
+                            att = mk1(1.f);
+                            rad = mk1(0.f);
+                            depth = 0;
+                            first = true;
+                            nrm_acc = mk1(0.f);
+                            dep_acc = 0.f;
+                        }
+                    }
+                }
             }
-            first_normal = mk1(0.f);
-            first_depth = 0.f;
         }
-        if (left > 0) {
-            Ray ray = ray_gen(p, x, y, s);
-            v3 att = mk1(1.f), rad = mk1(0.f);
-            uint32_t depth = 0;
-            bool first = true;
-            v3 nrm_acc = mk1(0.f);
-            float dep_acc = 0.f;
-            for (;;) {
-                Hit h;
-                int prim = -1;
-                if (STATS) cnt.segments++;
-                bool hit = trace<STATS>(p, ray, h, prim, cnt);
-                Shade sh;
-                v3 attr_normal;
-                if (hit) {
-                    if (STATS) cnt.hits++;
-                    const Mat m = p.mats[p.prims[prim].material];
-                    eval_material(m, h.normal, ray.d, s, sh);
-                    attr_normal = h.normal;
-                    ray.o = h.pos;                         // payload.hit_pos = position
-                } else {
-                    if (STATS) cnt.misses++;
-                    sh.radiance = miss_radiance(p, ray.d);
-                    sh.attenuation = mk1(0.f);             // never read: the path ends here
-                    sh.bounce = ray.d;
-                    attr_normal = -ray.d;
-                    depth = MAX_RECURSION_DEPTH_SET;       // termination sentinel (path_tracer.cu:121)
-                }
-                rad = rad + att * sh.radiance;
-                att = att * sh.attenuation;
-                if (AUX && first) {
-                    nrm_acc = nrm_acc + attr_normal;
-                    dep_acc += DEFAULT_RAY_TMAX;           // TraceRay took the ray by value (a18)
-                }
-                first = false;
-                ray.d = normalize(sh.bounce);
-                ray.tmin = BOUNCE_RAY_TMIN;
-                ray.tmax = DEFAULT_RAY_TMAX;
-                depth++;
-                if (!(depth < max_depth)) {
-                    sum = sum + rad;
-                    passes += 1.0f;
-                    if (AUX) { first_normal = nrm_acc; first_depth = dep_acc; }
-                    if (--left == 0) break;
-                    ray = ray_gen(p, x, y, s);
+        if (!__any(busy)) break;
+        if (busy && L.left > 0) {
+            // ---- one path segment: TraceRay + ClosetHit/Miss (path_tracer.cu:141-169) ----
+            Hit h;
+            int code = -1;
+            if (STATS) cnt.segments++;
+            const RayK rk = make_rayk(ray);
+            const bool hit = trace<STATS>(nodes, p.n_nodes, rk, h, code, cnt);
+            Shade sh;
+            v3 attr_normal;
+            if (hit) {
+                if (STATS) cnt.hits++;
+                const Mat m = p.mats[code >> 2];
+                eval_material(m, h.normal, ray.d, L.s, sh);
+                attr_normal = h.normal;
+                ray.o = h.pos;                         // payload.hit_pos = position
+            } else {
+                if (STATS) cnt.misses++;
+                sh.radiance = miss_radiance(p, ray.d);
+                sh.attenuation = mk1(0.f);             // never read: the path ends here
+                sh.bounce = ray.d;
+                attr_normal = -ray.d;
+                depth = MAX_RECURSION_DEPTH_SET;       // termination sentinel (path_tracer.cu:121)
+            }
+            rad = rad + att * sh.radiance;
+            att = att * sh.attenuation;
+            if (AUX && first) {
+                nrm_acc = nrm_acc + attr_normal;
+                dep_acc += DEFAULT_RAY_TMAX;           // TraceRay took the ray by value (a18)
+            }
+            first = false;
+            ray.d = normalize(sh.bounce);
+            ray.tmin = BOUNCE_RAY_TMIN;
+            ray.tmax = DEFAULT_RAY_TMAX;
+            depth++;
+            if (!(depth < max_depth)) {
+                L.sum = L.sum + rad;
+                L.passes += 1.0f;
+                if (AUX) { first_normal = nrm_acc; first_depth = dep_acc; }
+                if (--L.left > 0) {
+                    ray = ray_gen(p, L.x, L.y, L.s);
                     att = mk1(1.f);
                     rad = mk1(0.f);
                     depth = 0;
@@ -452,19 +574,23 @@ __global__ void __launch_bounds__(256) k_megakernel(const KParams p) {
                 }
             }
         }
-        p.accum[pix] = make_float4(sum.x, sum.y, sum.z, passes);
-        if (AUX && p.spp > 0) {
-            p.normal[3 * pix + 0] = first_normal.x;
-            p.normal[3 * pix + 1] = first_normal.y;
-            p.normal[3 * pix + 2] = first_normal.z;
-            p.depth[pix] = first_depth;
+        if (busy && L.left == 0) {
+            // ---- pixel finished: write back (path_tracer.cu:172-174) ---------------------
+            p.accum[L.pix] = make_float4(L.sum.x, L.sum.y, L.sum.z, L.passes);
+            if (AUX && p.spp > 0) {
+                p.normal[3 * L.pix + 0] = first_normal.x;
+                p.normal[3 * L.pix + 1] = first_normal.y;
+                p.normal[3 * L.pix + 2] = first_normal.z;
+                p.depth[L.pix] = first_depth;
+            }
+            p.rng[L.pix] = L.s.v0;
+            p.rng[npix + L.pix] = L.s.v1;
+            p.rng[2 * npix + L.pix] = L.s.v2;
+            p.rng[3 * npix + L.pix] = L.s.v3;
+            p.rng[4 * npix + L.pix] = L.s.v4;
+            p.rng[5 * npix + L.pix] = L.s.d;
+            busy = false;
         }
-        p.rng[pix] = s.v0;
-        p.rng[npix + pix] = s.v1;
-        p.rng[2 * npix + pix] = s.v2;
-        p.rng[3 * npix + pix] = s.v3;
-        p.rng[4 * npix + pix] = s.v4;
-        p.rng[5 * npix + pix] = s.d;
     }
     if (STATS) {
         uint64_t a = wave_sum(cnt.segments), b = wave_sum(cnt.nodes), c = wave_sum(cnt.prims);
@@ -475,6 +601,42 @@ __global__ void __launch_bounds__(256) k_megakernel(const KParams p) {
             atomicAdd((unsigned long long*)&p.stats[2], (unsigned long long)c);
             atomicAdd((unsigned long long*)&p.stats[3], (unsigned long long)d);
             atomicAdd((unsigned long long*)&p.stats[4], (unsigned long long)e);
+        }
+    }
+}
+
+// ======================================================================================
+// Self-test of qdiv against the hardware IEEE divide on hashed bit patterns.
+// which = 0: all 2^32 x 2^32 patterns (NaN/inf/subnormal included); 1: a = box-plane
+// differences (|a| < 2^20), d = unit-vector components; 2: a, d in [2^-30, 2^30].
+// ======================================================================================
+__device__ __forceinline__ uint32_t hash32(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+    return (uint32_t)x;
+}
+
+// out[0] = mismatch count; out[1..out_len) = (a bits << 32 | d bits) of some mismatches.
+__global__ void k_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint32_t ua = hash32(seed * 0x9e3779b97f4a7c15ULL + 2 * i), ud = hash32(seed * 0x9e3779b97f4a7c15ULL + 2 * i + 1);
+        float a, d;
+        if (which == 0) {
+            a = __uint_as_float(ua);
+            d = __uint_as_float(ud);
+        } else if (which == 1) {
+            a = __uint_as_float((ua & 0x807fffffu) | ((100u + (ua >> 23) % 47u) << 23));   // 2^-27 .. 2^20
+            d = __uint_as_float((ud & 0x807fffffu) | ((97u + (ud >> 23) % 30u) << 23));    // 2^-30 .. 2^-1
+        } else {
+            a = __uint_as_float((ua & 0x807fffffu) | ((97u + (ua >> 23) % 60u) << 23));
+            d = __uint_as_float((ud & 0x807fffffu) | ((97u + (ud >> 23) % 60u) << 23));
+        }
+        float q_ref = a / d;
+        float q = qdiv(a, d, rcp_d(d));
+        bool same = (__float_as_uint(q_ref) == __float_as_uint(q)) || (q_ref != q_ref && q != q);
+        if (!same) {
+            unsigned long long k = atomicAdd(&out[0], 1ull);
+            if ((long long)k + 1 < out_len) out[k + 1] = ((unsigned long long)__float_as_uint(a) << 32) | __float_as_uint(d);
         }
     }
 }
@@ -589,15 +751,50 @@ __global__ void k_math_batch(int op, const float* a, const float* b, float* out,
 // ======================================================================================
 // Host-side launchers (called from cpt_capi.cpp).
 // ======================================================================================
-hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t stream) {
-    const int tiles = ((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
-    const int blocks = (tiles + 3) / 4;
-    if (blocks == 0) return hipSuccess;
-    if (stats && aux) hipLaunchKernelGGL((k_megakernel<true, true>), dim3(blocks), dim3(256), 0, stream, p);
-    else if (stats) hipLaunchKernelGGL((k_megakernel<true, false>), dim3(blocks), dim3(256), 0, stream, p);
-    else if (aux) hipLaunchKernelGGL((k_megakernel<false, true>), dim3(blocks), dim3(256), 0, stream, p);
-    else hipLaunchKernelGGL((k_megakernel<false, false>), dim3(blocks), dim3(256), 0, stream, p);
+#ifndef CPT_LDS
+#define CPT_LDS 0   // A/B: LDS-staged BVH measured 9% slower than L1/L2 (bank conflicts), see DESIGN.md
+#endif
+// LDS variant: one block per CU holding all of the CU's waves, BVH up to 96 KB in LDS.
+int lds_node_capacity() { return CPT_LDS ? (96 * 1024) / (int)sizeof(Node) : 0; }
+
+template <bool S, bool A, bool L>
+static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
+    static int blocks_per_cu = -1, cus = 0;
+    const int block = L ? 256 * CPT_WAVES_PER_SIMD : 256;
+    const size_t shmem = L ? (size_t)lds_node_capacity() * sizeof(Node) : 0;
+    if (blocks_per_cu < 0) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_megakernel<S, A, L>, block, shmem);
+        if (e != hipSuccess) return e;
+        if (blocks_per_cu < 1) blocks_per_cu = 1;
+    }
+    // persistent grid: every resident slot once; lanes pull pixels from p.work
+    const long long tiles = (long long)((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
+    long long want = (tiles * 64 + block - 1) / block;
+    long long grid = std::min<long long>(want, (long long)blocks_per_cu * cus);
+    if (grid < 1) return hipSuccess;
+    hipLaunchKernelGGL((k_megakernel<S, A, L>), dim3((unsigned)grid), dim3(block), shmem, stream, p);
     return hipGetLastError();
+}
+
+hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t stream) {
+    if (p.width <= 0 || p.n_rows <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(p.work, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const bool lds = p.n_nodes > 0 && p.n_nodes <= lds_node_capacity();
+    if (lds) {
+        if (stats && aux) return launch_mk<true, true, true>(p, stream);
+        if (stats) return launch_mk<true, false, true>(p, stream);
+        if (aux) return launch_mk<false, true, true>(p, stream);
+        return launch_mk<false, false, true>(p, stream);
+    }
+    if (stats && aux) return launch_mk<true, true, false>(p, stream);
+    if (stats) return launch_mk<true, false, false>(p, stream);
+    if (aux) return launch_mk<false, true, false>(p, stream);
+    return launch_mk<false, false, false>(p, stream);
 }
 
 hipError_t launch_prepare_materials(Mat* mats, int n, hipStream_t stream) {
@@ -620,6 +817,12 @@ hipError_t launch_init_rng(const uint32_t* jumps, const uint32_t seed_state[6], 
 hipError_t launch_math_batch(int op, const float* a, const float* b, float* out, size_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_math_batch, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, op, a, b, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len,
+                                hipStream_t stream) {
+    hipLaunchKernelGGL(k_selftest_qdiv, dim3(4096), dim3(256), 0, stream, which, n, seed, out, out_len);
     return hipGetLastError();
 }
 

@@ -165,6 +165,15 @@ class Renderer:
     def reset_stats(self):
         self._check(self._L.cpt_reset_stats(self._ctx))
 
+    def selftest_qdiv(self, which, n, seed=1, examples=16):
+        """Returns (mismatch count, [(a, d) float32 pairs of some mismatches])."""
+        out = np.zeros(examples + 1, dtype=np.uint64)
+        self._check(self._L.cpt_selftest_qdiv(self._ctx, which, n, seed, _p(out), out.size))
+        cnt = int(out[0])
+        pairs = [(np.uint32(int(v) >> 32).view(np.float32), np.uint32(int(v) & 0xFFFFFFFF).view(np.float32))
+                 for v in out[1:1 + min(cnt, examples)]]
+        return cnt, pairs
+
     def math_batch(self, op, a, b=None):
         a = np.ascontiguousarray(a, dtype=np.float32)
         b = np.ascontiguousarray(b if b is not None else np.zeros_like(a), dtype=np.float32)

@@ -195,6 +195,11 @@ int cpt_denoise_mix(cpt_ctx* ctx, uint32_t cur_sample_idx, uint8_t* bgra_host);
  * 6 (float)((double)a / (double)b) [IEEE f64 division], 7 a / b [f32 division],
  * 8 sqrtf(a). */
 int cpt_math_batch(cpt_ctx* ctx, int op, const float* a, const float* b, float* out, size_t n);
+/* Device self-test of the exact-quotient kernel helper against the hardware IEEE f32 divide
+ * over n hashed operand pairs (which: 0 all bit patterns, 1 slab-like ranges, 2 mid ranges).
+ * out[0] receives the mismatch count (0 expected), out[1..out_len) up to out_len-1 failing
+ * pairs as (a bits << 32 | d bits). */
+int cpt_selftest_qdiv(cpt_ctx* ctx, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len);
 
 #ifdef __cplusplus
 }  /* extern "C" */

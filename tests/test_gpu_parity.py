@@ -56,6 +56,14 @@ def test_ieee_div_sqrt(gpu):
     np.testing.assert_array_equal(gpu.math_batch(8, s).view(np.uint32), np.sqrt(s).view(np.uint32))
 
 
+@pytest.mark.parametrize("which,n", [(0, 1 << 32), (1, 1 << 32), (2, 1 << 32)])
+def test_exact_quotient_selftest(gpu, which, n):
+    """qdiv(a, RN64(1/d)) == IEEE f32 a/d (cpt_device.hpp): 4.3e9 hashed pairs per family,
+    compared on the device against the hardware v_div_* sequence."""
+    cnt, pairs = gpu.selftest_qdiv(which, n, seed=which + 1)
+    assert cnt == 0, [(float(a), float(d), float(a) / float(d)) for a, d in pairs]
+
+
 # ------------------------------------------------------------------------------- rng
 @pytest.mark.parametrize("w,rows", [(64, list(range(64))), (3840, [0, 1, 7, 1079, 2159]),
                                     (333, [5, 3, 200, 3])])
