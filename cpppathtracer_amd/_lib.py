@@ -42,6 +42,7 @@ PROTOTYPES = {
     "cpt_copy_accum_device": (_I, [_P, _P, _SZ]),
     "cpt_get_stats": (_I, [_P, _P]),
     "cpt_reset_stats": (_I, [_P]),
+    "cpt_get_raw_counters": (_I, [_P, _P]),
     "cpt_last_render_ms": (_I, [_P, _P]),
     "cpt_last_kernel_stats": (_I, [_P, _P, _P]),
     "cpt_denoise_mix": (_I, [_P, _U32, _P]),

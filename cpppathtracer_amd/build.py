@@ -67,6 +67,7 @@ def build(force: bool = False, verbose: bool = False, out: str = None, defines=(
     target = out or LIB_PATH
     if not force and out is None and not defines and not needs_build():
         return LIB_PATH
+    os.makedirs(os.path.dirname(os.path.abspath(target)), exist_ok=True)
     tmp = target + ".tmp"
     cmd = [_hipcc(), *HIPCC_FLAGS, *[f"-D{d}" for d in defines], "-I", os.path.join(REPO_DIR, "include"), "-o", tmp,
            *_extra_sources()]

@@ -803,6 +803,14 @@ int cpt_get_stats(cpt_ctx* c, cpt_stats* out) {
     return CPT_OK;
 }
 
+int cpt_get_raw_counters(cpt_ctx* c, uint64_t* out8) {
+    if (!c || !out8) return CPT_ERR_INVALID_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    HIP_TRY(c, hipMemcpy(out8, c->d_stats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return CPT_OK;
+}
+
 int cpt_reset_stats(cpt_ctx* c) {
     if (!c) return CPT_ERR_INVALID_ARG;
     HIP_TRY(c, hipSetDevice(c->device));

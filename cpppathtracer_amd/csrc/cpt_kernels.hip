@@ -187,6 +187,43 @@ __device__ inline bool cylinder_test(const Node& cy, const RayK& ray, float& tma
     return ret;
 }
 
+// Sphere (object.cu:10-35) and cylinder side (object.cu:81-111) share one quadratic: the
+// cylinder's 2-D terms are the sphere's 3-D ones with the y terms replaced by +0, which
+// leaves every rounding unchanged ((u + 0) + w == u + w for the squares and products here,
+// up to the sign of a zero b that cannot change the roots).  The cylinder's second root can
+// never replace an accepted first root (temp2 >= temp1 under monotone rounding), so both
+// shapes return after the first accepted root as the sphere does.
+__device__ __forceinline__ bool quad_test(const Node& nd, const RayK& ray, float& tmax, Hit& h, bool cyl,
+                                          float lower, float upper) {
+    const float cx = nd.a0, cy = nd.a1, cz = nd.a2, r = nd.b0;
+    const float ax = ray.o.x - cx, ay = ray.o.y - cy, az = ray.o.z - cz;
+    const float ay_dy = cyl ? 0.f : ay * ray.d.y;
+    const float ay_ay = cyl ? 0.f : ay * ay;
+    const float dy_dy = cyl ? 0.f : ray.d.y * ray.d.y;
+    const float a = (ray.d.x * ray.d.x + dy_dy) + ray.d.z * ray.d.z;
+    const float b = (ax * ray.d.x + ay_dy) + az * ray.d.z;
+    const float c = ((ax * ax + ay_ay) + az * az) - r * r;
+    const float disc = b * b - a * c;
+    if (!(disc > 0.f)) return false;
+    const double y = cyl ? ray.yc : ray.ya;
+    const float sq = __builtin_sqrtf(disc);
+    float temp = qdiv(-b - sq, a, y);
+    v3 hp = ray.o + temp * ray.d;
+    bool first = true;
+    if (!(temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper)) {
+        temp = qdiv(-b + sq, a, y);
+        hp = ray.o + temp * ray.d;
+        if (!(temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper)) return false;
+        first = false;
+    }
+    tmax = temp;
+    h.pos = hp;
+    const v3 v = mk(hp.x - cx, cyl ? 0.f : hp.y - cy, hp.z - cz);
+    // sphere first root: (p - c) / r with the signed radius; every other case normalizes
+    h.normal = (first && !cyl) ? v / r : normalize(v);
+    return true;
+}
+
 // ======================================================================================
 // SceneBVH::TraceRay (bvh.cu:167-205) as a stackless skip-link walk.  The nodes are stored
 // in the exact order the reference's stack DFS pops them (right child first), so visiting
@@ -208,6 +245,11 @@ struct Counters { uint32_t segments, nodes, prims, hits, misses; };
 
 // Slab test of one internal node (bvh.cu:181-200).  The six plane distances use the exact
 // quotient; if any of them is zero/subnormal the node is redone with the IEEE divide.
+// FAST (rays without NaN): the plane distances of the axes that are used are never NaN
+// (finite box coordinate minus finite origin, times a finite reciprocal), so the ternary
+// MIN/MAX of the reference equal v_min/v_max_f32 up to the sign of a zero, which none of
+// the three comparisons can see.  Rays carrying a NaN take the exact ternary form.
+template <bool FAST>
 __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, float tmax) {
     float t0x = qdiv_raw(nd.a0 - ray.o.x, ray.yx), t1x = qdiv_raw(nd.b0 - ray.o.x, ray.yx);
     float t0y = qdiv_raw(nd.a1 - ray.o.y, ray.yy), t1y = qdiv_raw(nd.b1 - ray.o.y, ray.yy);
@@ -224,22 +266,76 @@ __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, flo
         t0y = (nd.a1 - ray.o.y) / ray.d.y; t1y = (nd.b1 - ray.o.y) / ray.d.y;
         t0z = (nd.a2 - ray.o.z) / ray.d.z; t1z = (nd.b2 - ray.o.z) / ray.d.z;
     }
+    // axes with d == 0 are skipped (bvh.cu:182,188,194): selects, not branches
     float lo = -DEFAULT_RAY_TMAX * 2, hi = DEFAULT_RAY_TMAX * 2;
-    if (ray.d.x != 0.f) { lo = tmax_(lo, tmin_(t0x, t1x)); hi = tmin_(hi, tmax_(t0x, t1x)); }
-    if (ray.d.y != 0.f) { lo = tmax_(lo, tmin_(t0y, t1y)); hi = tmin_(hi, tmax_(t0y, t1y)); }
-    if (ray.d.z != 0.f) { lo = tmax_(lo, tmin_(t0z, t1z)); hi = tmin_(hi, tmax_(t0z, t1z)); }
+    float lx, hx, ly, hy, lz, hz;
+    if (FAST) {
+        lx = __builtin_fmaxf(lo, __builtin_fminf(t0x, t1x));
+        hx = __builtin_fminf(hi, __builtin_fmaxf(t0x, t1x));
+    } else {
+        lx = tmax_(lo, tmin_(t0x, t1x));
+        hx = tmin_(hi, tmax_(t0x, t1x));
+    }
+    lo = ray.d.x != 0.f ? lx : lo;
+    hi = ray.d.x != 0.f ? hx : hi;
+    if (FAST) {
+        ly = __builtin_fmaxf(lo, __builtin_fminf(t0y, t1y));
+        hy = __builtin_fminf(hi, __builtin_fmaxf(t0y, t1y));
+    } else {
+        ly = tmax_(lo, tmin_(t0y, t1y));
+        hy = tmin_(hi, tmax_(t0y, t1y));
+    }
+    lo = ray.d.y != 0.f ? ly : lo;
+    hi = ray.d.y != 0.f ? hy : hi;
+    if (FAST) {
+        lz = __builtin_fmaxf(lo, __builtin_fminf(t0z, t1z));
+        hz = __builtin_fminf(hi, __builtin_fmaxf(t0z, t1z));
+    } else {
+        lz = tmax_(lo, tmin_(t0z, t1z));
+        hz = tmin_(hi, tmax_(t0z, t1z));
+    }
+    lo = ray.d.z != 0.f ? lz : lo;
+    hi = ray.d.z != 0.f ? hz : hi;
     return lo > hi || lo > tmax || hi < ray.tmin;
 }
 
+#ifndef CPT_UNIFIED_QUAD
+#define CPT_UNIFIED_QUAD 1
+#endif
 __device__ __forceinline__ bool leaf_test(const Node& nd, const RayK& ray, float& tmax, Hit& h) {
     const int type = nd.code & 3;
+#if CPT_UNIFIED_QUAD
+    bool r = false;
+    float lower = -__builtin_inff(), upper = __builtin_inff();
+    if (type == 2) {
+        // Cylinder caps first (object.cu:52-77), then the side.
+        upper = nd.a1 + nd.b2 / 2;
+        if (cap_test(nd.a0, nd.a2, nd.b0, ray, tmax, h, upper)) r = true;
+        lower = nd.a1 - nd.b2 / 2;
+        if (cap_test(nd.a0, nd.a2, nd.b0, ray, tmax, h, lower)) r = true;
+    }
+    if (type == 0 || type == 2) {
+        if (quad_test(nd, ray, tmax, h, type == 2, lower, upper)) r = true;
+    } else if (type == 1) {
+        r = platform_test(nd, ray, tmax, h);
+    }
+    return r;
+#else
     if (type == 0) return sphere_test(nd, ray, tmax, h);
     if (type == 2) return cylinder_test(nd, ray, tmax, h);
     if (type == 1) return platform_test(nd, ray, tmax, h);
     return false;
+#endif
 }
 
-template <bool STATS>
+#ifndef CPT_LEAF_BATCH
+#define CPT_LEAF_BATCH 0   // K > 0: run the leaf phase when >= 1/K of the walking lanes wait on a leaf
+#endif
+#ifndef CPT_PREFETCH
+#define CPT_PREFETCH 1     // load both possible successors of a node while it is being tested
+#endif
+
+template <bool STATS, bool FAST>
 __device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_nodes, const RayK& ray, Hit& h,
                                       int& code_out, Counters& cnt) {
     float tmax = DEFAULT_RAY_TMAX;
@@ -250,7 +346,7 @@ __device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_node
         Node nd = nodes[ni];
         while (nd.code < 0) {
             if (STATS) cnt.nodes++;
-            ni = slab_reject(nd, ray, tmax) ? nd.miss : ni + 1;
+            ni = slab_reject<FAST>(nd, ray, tmax) ? nd.miss : ni + 1;
             if (ni >= n_nodes) break;
             nd = nodes[ni];
         }
@@ -258,6 +354,53 @@ __device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_node
         if (STATS) { cnt.nodes++; cnt.prims++; }
         if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
         ni = nd.miss;
+    }
+#elif CPT_LEAF_BATCH > 0
+    // Lanes that reach a leaf park there until a leaf phase; a lane's own visit sequence (and
+    // so its tmax history, pruning and first-found tie rule) is unchanged — only the
+    // interleaving of lanes changes.
+    Node nd;
+    if (ni < n_nodes) nd = nodes[ni];
+    for (;;) {
+        const bool walking = ni < n_nodes;
+        const bool at_leaf = walking && nd.code >= 0;
+        const uint64_t lm = __ballot(at_leaf), wm = __ballot(walking);
+        if (wm == 0) break;
+        const bool leaf_phase = (lm == wm) || (__popcll(lm) * CPT_LEAF_BATCH >= __popcll(wm));
+        if (leaf_phase ? at_leaf : (walking && !at_leaf)) {
+            if (STATS) cnt.nodes++;
+            if (leaf_phase) {
+                if (STATS) cnt.prims++;
+                if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
+                ni = nd.miss;
+            } else {
+                ni = slab_reject<FAST>(nd, ray, tmax) ? nd.miss : ni + 1;
+            }
+            if (ni < n_nodes) nd = nodes[ni];
+        }
+    }
+#elif CPT_PREFETCH
+    // The successor of node ni is ni + 1 (box hit: its right child) or nd.miss; both loads are
+    // issued before the node's test so their latency hides under it (leaves: miss == ni + 1).
+    Node nd;
+    if (ni < n_nodes) nd = nodes[0];
+    const int last = n_nodes - 1;
+    while (ni < n_nodes) {
+        const int na = ni + 1, nb = nd.miss;
+        const Node pa = nodes[na < last ? na : last];
+        const Node pb = nodes[nb < last ? nb : last];
+        if (STATS) cnt.nodes++;
+        bool take_a;
+        if (nd.code >= 0) {
+            // leaf: IntersectionTest first (bvh.cu:175-180); its own box test is moot
+            if (STATS) cnt.prims++;
+            if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
+            take_a = false;
+        } else {
+            take_a = !slab_reject<FAST>(nd, ray, tmax);
+        }
+        ni = take_a ? na : nb;
+        nd = take_a ? pa : pb;
     }
 #else
     while (ni < n_nodes) {
@@ -269,7 +412,7 @@ __device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_node
             if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
             ni = nd.miss;
         } else {
-            ni = slab_reject(nd, ray, tmax) ? nd.miss : ni + 1;
+            ni = slab_reject<FAST>(nd, ray, tmax) ? nd.miss : ni + 1;
         }
     }
 #endif
@@ -428,6 +571,21 @@ __device__ __forceinline__ uint64_t wave_sum(uint32_t v) {
 // wave starts coherent.  LDS variant: the BVH (32 B nodes, leaves inline) is staged in LDS
 // once per resident block.
 // ======================================================================================
+#ifndef CPT_STAMPS
+#define CPT_STAMPS 0   // diagnostic build: per-phase s_memtime sums into stats[5..7] (never timed)
+#endif
+__device__ __forceinline__ unsigned long long stamp() {
+#if CPT_STAMPS
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+#else
+    return 0;
+#endif
+}
+
 struct Lane {
     int x, y;
     size_t pix;
@@ -471,7 +629,9 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
     v3 nrm_acc = mk1(0.f), first_normal = mk1(0.f);
     float dep_acc = 0.f, first_depth = 0.f;
 
+    unsigned long long st_refill = 0, st_trace = 0, st_shade = 0;
     for (;;) {
+        const unsigned long long t0 = stamp();
         // ---- refill idle lanes with new pixels (wave-aggregated dequeue) ----------------
         if (!exhausted) {
             const uint64_t need = __ballot(!busy);
@@ -525,13 +685,20 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             }
         }
         if (!__any(busy)) break;
+        const unsigned long long t1 = stamp();
+        unsigned long long t2 = t1;
         if (busy && L.left > 0) {
             // ---- one path segment: TraceRay + ClosetHit/Miss (path_tracer.cu:141-169) ----
             Hit h;
             int code = -1;
             if (STATS) cnt.segments++;
             const RayK rk = make_rayk(ray);
-            const bool hit = trace<STATS>(nodes, p.n_nodes, rk, h, code, cnt);
+            const bool finite_ray = !(ray.o.x != ray.o.x || ray.o.y != ray.o.y || ray.o.z != ray.o.z ||
+                                      ray.d.x != ray.d.x || ray.d.y != ray.d.y || ray.d.z != ray.d.z);
+            bool hit;
+            if (__builtin_expect(finite_ray, 1)) hit = trace<STATS, true>(nodes, p.n_nodes, rk, h, code, cnt);
+            else hit = trace<STATS, false>(nodes, p.n_nodes, rk, h, code, cnt);
+            t2 = stamp();
             Shade sh;
             v3 attr_normal;
             if (hit) {
@@ -574,6 +741,12 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
                 }
             }
         }
+        if (CPT_STAMPS) {
+            const unsigned long long t3 = stamp();
+            st_refill += t1 - t0;
+            st_trace += t2 - t1;
+            st_shade += t3 - t2;
+        }
         if (busy && L.left == 0) {
             // ---- pixel finished: write back (path_tracer.cu:172-174) ---------------------
             p.accum[L.pix] = make_float4(L.sum.x, L.sum.y, L.sum.z, L.passes);
@@ -591,6 +764,11 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             p.rng[5 * npix + L.pix] = L.s.d;
             busy = false;
         }
+    }
+    if (CPT_STAMPS && lane == 0) {
+        atomicAdd(&p.stats[5], st_refill);
+        atomicAdd(&p.stats[6], st_trace);
+        atomicAdd(&p.stats[7], st_shade);
     }
     if (STATS) {
         uint64_t a = wave_sum(cnt.segments), b = wave_sum(cnt.nodes), c = wave_sum(cnt.prims);

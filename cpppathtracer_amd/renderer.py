@@ -162,6 +162,11 @@ class Renderer:
         self._check(self._L.cpt_get_stats(self._ctx, s))
         return dict(zip(("segments", "nodes", "prims", "hits", "misses"), (int(x) for x in s)))
 
+    def raw_counters(self):
+        out = np.zeros(8, dtype=np.uint64)
+        self._check(self._L.cpt_get_raw_counters(self._ctx, _p(out)))
+        return [int(x) for x in out]
+
     def reset_stats(self):
         self._check(self._L.cpt_reset_stats(self._ctx))
 
