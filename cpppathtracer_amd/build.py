@@ -78,5 +78,25 @@ def build(force: bool = False, verbose: bool = False, out: str = None, defines=(
     return target
 
 
+EXAMPLE_SRC = os.path.join(REPO_DIR, "examples", "headless_render.cpp")
+EXAMPLE_BIN = os.path.join(REPO_DIR, "build", "bin", "cpt_headless")
+
+
+def build_examples(force: bool = False, verbose: bool = False) -> str:
+    """The reference-app-shaped headless driver, host C++ only (g++), linked to libcpt.so."""
+    lib = build()
+    if (not force and os.path.exists(EXAMPLE_BIN)
+            and os.path.getmtime(EXAMPLE_BIN) > max(os.path.getmtime(EXAMPLE_SRC), os.path.getmtime(lib))):
+        return EXAMPLE_BIN
+    os.makedirs(os.path.dirname(EXAMPLE_BIN), exist_ok=True)
+    cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-pthread", "-I", os.path.join(REPO_DIR, "include"),
+           "-o", EXAMPLE_BIN, EXAMPLE_SRC, lib, "-Wl,-rpath,$ORIGIN/../../cpppathtracer_amd"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return EXAMPLE_BIN
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_examples(force="--force" in sys.argv, verbose=True))

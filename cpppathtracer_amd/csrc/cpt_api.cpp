@@ -1,0 +1,518 @@
+// cpt_api.cpp — the reference-shaped C++ construction API (include/cpppathtracer/*.h) on top
+// of the C-ABI (include/cpt.h).  Host code only; every GPU operation goes through cpt_*.
+#include <dlfcn.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <set>
+#include <sstream>
+
+#include "../../include/cpppathtracer/path_tracer.h"
+
+// ======================================================================================
+// Object (object.cu:134-170)
+// ======================================================================================
+float3 Object::GetAABBMax() {
+    float3 m = make_float3(0.f);
+    const float tol = BOUNCE_RAY_TMIN * 5.f;
+    switch (type_) {
+        case PrimitiveType::Sphere: m = center_ + make_float3(ABS(radius_)); break;
+        case PrimitiveType::Platform: m = make_float3(DEFAULT_RAY_TMAX * 5, y_pos_ + tol, DEFAULT_RAY_TMAX * 5); break;
+        case PrimitiveType::Cylinder:
+            m = make_float3(center_.x + ABS(radius_), center_.y + height_ / 2 + tol, center_.z + ABS(radius_));
+            break;
+        default: break;
+    }
+    return m;
+}
+
+float3 Object::GetAABBMin() {
+    float3 m = make_float3(0.f);
+    const float tol = BOUNCE_RAY_TMIN * 5.f;
+    switch (type_) {
+        case PrimitiveType::Sphere: m = center_ - make_float3(ABS(radius_)); break;
+        case PrimitiveType::Platform: m = make_float3(-DEFAULT_RAY_TMAX * 5, y_pos_ - tol, -DEFAULT_RAY_TMAX * 5); break;
+        case PrimitiveType::Cylinder:
+            m = make_float3(center_.x - ABS(radius_), center_.y - height_ / 2 - tol, center_.z - ABS(radius_));
+            break;
+        default: break;
+    }
+    return m;
+}
+
+// ======================================================================================
+// MotionalCamera (motional_camera.cu)
+// ======================================================================================
+static std::mutex camera_mutex;   // motional_camera.cu:12
+
+MotionalCamera::MotionalCamera()
+    : width_(1920), height_(1080), cur_sample_idx_(0), origin_(make_float3(0.f)), look_at_(make_float3(0.f, 0.f, 1.f)) {}
+MotionalCamera::MotionalCamera(int width, int height)
+    : width_(width), height_(height), cur_sample_idx_(0), origin_(make_float3(0.f)), look_at_(make_float3(0.f, 0.f, 1.f)) {}
+MotionalCamera::MotionalCamera(int width, int height, float3 ori, float3 at)
+    : width_(width), height_(height), cur_sample_idx_(0), origin_(ori), look_at_(at) {}
+MotionalCamera::~MotionalCamera() {}
+
+void MotionalCamera::Refresh() { cur_sample_idx_ = 0; }
+void MotionalCamera::SetViewFov(float fov) { view_fov_ = fov; }
+void MotionalCamera::Resize(int width, int height) { width_ = width; height_ = height; }
+void MotionalCamera::SetOrigin(float3 ori) { origin_ = ori; }
+void MotionalCamera::SetOrigin(float x, float y, float z) { origin_ = make_float3(x, y, z); }
+void MotionalCamera::SetLookAt(float3 look_at) { look_at_ = look_at; }
+void MotionalCamera::SetLookAt(float x, float y, float z) { look_at_ = make_float3(x, y, z); }
+
+// motional_camera.cu:76-168
+void MotionalCamera::MoveEyeLeft(float k) {
+    float3 w = normalize(origin_ - look_at_);
+    float3 left = -normalize(cross(vup, w));
+    origin_ += k * move_speed_ * left;
+    look_at_ += k * move_speed_ * left;
+}
+void MotionalCamera::MoveEyeRight(float k) {
+    float3 w = normalize(origin_ - look_at_);
+    float3 left = -normalize(cross(vup, w));
+    origin_ -= k * move_speed_ * left;
+    look_at_ -= k * move_speed_ * left;
+}
+void MotionalCamera::MoveEyeForward(float k) {
+    float3 w = normalize(origin_ - look_at_);
+    float3 left = -normalize(cross(vup, w));
+    float3 back = -normalize(cross(left, vup));
+    origin_ -= k * move_speed_ * back;
+    look_at_ -= k * move_speed_ * back;
+}
+void MotionalCamera::MoveEyeBackward(float k) {
+    float3 w = normalize(origin_ - look_at_);
+    float3 left = -normalize(cross(vup, w));
+    float3 back = -normalize(cross(left, vup));
+    origin_ += k * move_speed_ * back;
+    look_at_ += k * move_speed_ * back;
+}
+void MotionalCamera::MoveEyeUp(float k) {
+    origin_ += k * move_speed_ * vup;
+    look_at_ += k * move_speed_ * vup;
+}
+void MotionalCamera::MoveEyeDown(float k) {
+    origin_ -= k * move_speed_ * vup;
+    look_at_ -= k * move_speed_ * vup;
+}
+void MotionalCamera::RotateAroundUp(float dy) {
+    look_at_ = origin_ + normalize(look_at_ - origin_);
+    float3 w = normalize(look_at_ - origin_);
+    float3 left = normalize(cross(vup, w));
+    float3 up = normalize(cross(w, left));
+    look_at_ += dy * up;
+    look_at_ = origin_ + normalize(look_at_ - origin_);
+}
+void MotionalCamera::RotateAroundDown(float dy) {
+    look_at_ = origin_ + normalize(look_at_ - origin_);
+    float3 w = normalize(look_at_ - origin_);
+    float3 left = normalize(cross(vup, w));
+    float3 up = normalize(cross(w, left));
+    look_at_ -= dy * up;
+    look_at_ = origin_ + normalize(look_at_ - origin_);
+}
+void MotionalCamera::RotateAroundLeft(float dx) {
+    look_at_ = origin_ + normalize(look_at_ - origin_);
+    float3 w = normalize(look_at_ - origin_);
+    float3 left = normalize(cross(vup, w));
+    look_at_ += dx * left;
+    look_at_ = origin_ + normalize(look_at_ - origin_);
+}
+void MotionalCamera::RotateAroundRight(float dx) {
+    look_at_ = origin_ + normalize(look_at_ - origin_);
+    float3 w = normalize(look_at_ - origin_);
+    float3 left = normalize(cross(vup, w));
+    look_at_ -= dx * left;
+    look_at_ = origin_ + normalize(look_at_ - origin_);
+}
+void MotionalCamera::ScaleFov(float d) { view_fov_ = (float)(view_fov_ + d * M_PI / 180.0f); }
+void MotionalCamera::Lock() { camera_mutex.lock(); }
+void MotionalCamera::Unlock() { camera_mutex.unlock(); }
+
+MotionalCamera MotionalCamera::GetCopy() {
+    std::lock_guard<std::mutex> lock(camera_mutex);
+    cpt_camera_get_copy(reinterpret_cast<cpt_camera*>(this));   // basis + cur_sample_idx_++
+    return *this;
+}
+
+// ======================================================================================
+// SceneBVH statics (bvh.cu:16-29, 116-165)
+// ======================================================================================
+namespace {
+std::mutex bvh_mutex;
+std::vector<Object*> bvh_objs;
+std::set<Object*> bvh_seen;
+std::vector<cpt_object> bvh_snapshot;
+uint64_t bvh_build_id = 0;
+std::vector<int> bvh_update_log;
+SceneBVH* const bvh_handle = reinterpret_cast<SceneBVH*>(&bvh_snapshot);   // opaque, non-null
+
+// texture registry
+std::mutex tex_mutex;
+std::map<PocaTexture, PocaTextureData> tex_registry;
+PocaTexture tex_next = 1;
+}  // namespace
+
+void SceneBVH::AddObject(Object* obj) {
+    std::lock_guard<std::mutex> lk(bvh_mutex);
+    if (obj == nullptr || bvh_seen.count(obj)) return;
+    bvh_objs.push_back(obj);
+    bvh_seen.insert(obj);
+}
+
+SceneBVHGPUHandle SceneBVH::BuildBVH() {
+    std::lock_guard<std::mutex> lk(bvh_mutex);
+    bvh_snapshot.resize(bvh_objs.size());
+    for (size_t i = 0; i < bvh_objs.size(); ++i) std::memcpy(&bvh_snapshot[i], bvh_objs[i], sizeof(cpt_object));
+    bvh_build_id++;
+    bvh_update_log.clear();
+    return bvh_handle;
+}
+
+void SceneBVH::UpdateObject(Object* obj) {
+    std::lock_guard<std::mutex> lk(bvh_mutex);
+    for (size_t i = 0; i < bvh_objs.size() && i < bvh_snapshot.size(); ++i)
+        if (bvh_objs[i] == obj) {
+            std::memcpy(&bvh_snapshot[i], obj, sizeof(cpt_object));
+            bvh_update_log.push_back((int)i);
+            return;
+        }
+}
+
+void SceneBVH::ReleaseBVH() {
+    std::lock_guard<std::mutex> lk(bvh_mutex);
+    bvh_objs.clear();
+    bvh_seen.clear();
+    bvh_snapshot.clear();
+    bvh_update_log.clear();
+    bvh_build_id++;
+}
+
+const std::vector<cpt_object>& SceneBVH::Snapshot() { return bvh_snapshot; }
+uint64_t SceneBVH::BuildId() {
+    std::lock_guard<std::mutex> lk(bvh_mutex);
+    return bvh_build_id;
+}
+std::vector<int> SceneBVH::UpdateLog() {
+    std::lock_guard<std::mutex> lk(bvh_mutex);
+    return bvh_update_log;
+}
+int SceneBVH::IndexOf(const Object* obj) {
+    for (size_t i = 0; i < bvh_objs.size(); ++i)
+        if (bvh_objs[i] == obj) return (int)i;
+    return -1;
+}
+
+// ======================================================================================
+// PocaTextureUtils (textures.cu:14-66)
+// ======================================================================================
+static bool load_cptex(const std::string& path, PocaTextureData& t) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    char magic[8];
+    uint32_t hdr[4];
+    if (!f.read(magic, 8) || std::memcmp(magic, "CPTTEX01", 8) != 0) return false;
+    if (!f.read(reinterpret_cast<char*>(hdr), sizeof(hdr))) return false;
+    t.width = (int)hdr[0];
+    t.height = (int)hdr[1];
+    t.valid_cols = (int)hdr[2];
+    t.rgba.resize((size_t)t.valid_cols * t.height * 4);
+    return (bool)f.read(reinterpret_cast<char*>(t.rgba.data()), (std::streamsize)t.rgba.size());
+}
+
+static bool load_ppm(const std::string& path, PocaTextureData& t) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    std::string magic;
+    f >> magic;
+    if (magic != "P6") return false;
+    int w = 0, h = 0, maxv = 0;
+    f >> w >> h >> maxv;
+    f.get();
+    if (w <= 0 || h <= 0 || maxv != 255) return false;
+    std::vector<uint8_t> rgb((size_t)w * h * 3);
+    if (!f.read(reinterpret_cast<char*>(rgb.data()), (std::streamsize)rgb.size())) return false;
+    // textures.cu:32-33: cudaMemcpy2DToArray copies `width` BYTES per row = width/4 texels.
+    t.width = w;
+    t.height = h;
+    t.valid_cols = w / 4;
+    t.rgba.resize((size_t)t.valid_cols * h * 4);
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < t.valid_cols; ++x) {
+            const uint8_t* s = &rgb[((size_t)y * w + x) * 3];
+            uint8_t* d = &t.rgba[((size_t)y * t.valid_cols + x) * 4];
+            d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; d[3] = 255;
+        }
+    return true;
+}
+
+PocaTexture PocaTextureUtils::AddTexByFile(std::string file_path, PocaAddressMode addr_mode, PocaFilterMode filter_mode) {
+    PocaTextureData t;
+    t.addr = addr_mode;
+    t.filter = filter_mode;
+    if (!load_cptex(file_path, t) && !load_ppm(file_path, t)) {
+        fprintf(stderr, "[cpt] AddTexByFile: cannot load %s (.cptex or binary PPM)\n", file_path.c_str());
+        return 0;
+    }
+    std::lock_guard<std::mutex> lk(tex_mutex);
+    PocaTexture h = tex_next++;
+    tex_registry[h] = std::move(t);
+    return h;
+}
+
+void PocaTextureUtils::DestroyTexture(PocaTexture tex) {
+    std::lock_guard<std::mutex> lk(tex_mutex);
+    tex_registry.erase(tex);
+}
+
+const PocaTextureData* PocaTextureUtils::Get(PocaTexture tex) {
+    std::lock_guard<std::mutex> lk(tex_mutex);
+    auto it = tex_registry.find(tex);
+    return it == tex_registry.end() ? nullptr : &it->second;
+}
+
+// ======================================================================================
+// PathTracer (path_tracer.cu:29-319)
+// ======================================================================================
+static std::string default_sky_path() {
+    if (const char* e = getenv("CPT_SKY_PATH")) return e;
+    {
+        std::ifstream f("assets/sky.cptex");
+        if (f) return "assets/sky.cptex";
+    }
+    Dl_info info;
+    if (dladdr(reinterpret_cast<void*>(&default_sky_path), &info) && info.dli_fname) {
+        std::string so = info.dli_fname;
+        std::string dir = so.substr(0, so.find_last_of('/'));
+        return dir + "/../assets/sky.cptex";
+    }
+    return "assets/sky.cptex";
+}
+
+PathTracer::PathTracer() {}
+
+PathTracer::~PathTracer() {
+    Stop();
+    if (ctx_) cpt_destroy(ctx_);
+}
+
+bool PathTracer::Fail(const char* what) {
+    err_ = std::string(what) + ": " + (ctx_ ? cpt_last_error(ctx_) : cpt_last_error(nullptr));
+    fprintf(stderr, "[cpt] %s\n", err_.c_str());   // the reference logs and continues
+    return false;
+}
+
+void PathTracer::AddObject(Object* obj) { SceneBVH::AddObject(obj); }
+
+void PathTracer::SetCamera(std::shared_ptr<MotionalCamera>& camera) { camera_ = camera; }
+std::shared_ptr<MotionalCamera> PathTracer::GetCamera() { return camera_; }
+
+bool PathTracer::SetMaxRecursionDepth(uint depth) {
+    if (depth > MAX_RECURSION_DEPTH_SET) {
+        err_ = "SetMaxRecursionDepth: depth must be <= 32";
+        return false;
+    }
+    max_recursion_depth_ = depth;
+    return true;
+}
+
+void PathTracer::SetSeed(uint64_t seed) {
+    std::lock_guard<std::mutex> lk(mu_);
+    seed_ = seed;
+    rng_ready_ = false;
+}
+
+bool PathTracer::SetDevice(int device) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (ctx_) {
+        err_ = "SetDevice: the context already exists";
+        return false;
+    }
+    device_ = device;
+    return true;
+}
+
+bool PathTracer::SetEnvTexture(PocaTexture tex) {
+    std::lock_guard<std::mutex> lk(mu_);
+    env_ = tex;
+    env_uploaded_ = false;
+    return true;
+}
+
+bool PathTracer::EnsureContext() {
+    if (ctx_) return true;
+    if (cpt_create(device_, &ctx_) != CPT_OK) {
+        ctx_ = nullptr;
+        return Fail("cpt_create");
+    }
+    return true;
+}
+
+bool PathTracer::SyncScene() {
+    if (!EnsureContext()) return false;
+    const uint64_t build = SceneBVH::BuildId();
+    if (scene_build_ != build) {
+        std::vector<cpt_object> objs;
+        {
+            std::lock_guard<std::mutex> lk(bvh_mutex);
+            objs = bvh_snapshot;
+        }
+        if (cpt_set_scene(ctx_, objs.empty() ? nullptr : objs.data(), (int)objs.size()) != CPT_OK)
+            return Fail("cpt_set_scene");
+        scene_build_ = build;
+        updates_applied_ = 0;
+    }
+    const std::vector<int> log = SceneBVH::UpdateLog();
+    for (; updates_applied_ < log.size(); ++updates_applied_) {
+        const int i = log[updates_applied_];
+        cpt_object o;
+        {
+            std::lock_guard<std::mutex> lk(bvh_mutex);
+            o = bvh_snapshot[i];
+        }
+        if (cpt_update_object(ctx_, i, &o) != CPT_OK) return Fail("cpt_update_object");
+    }
+    if (!env_uploaded_) {
+        if (env_ == 0) env_ = PocaTextureUtils::AddTexByFile(default_sky_path());   // path_tracer.cu:47
+        const PocaTextureData* t = PocaTextureUtils::Get(env_);
+        int rc = t ? cpt_set_env_texture(ctx_, t->rgba.data(), t->width, t->height, t->valid_cols)
+                   : cpt_set_env_texture(ctx_, nullptr, 1, 1, 0);
+        if (rc != CPT_OK) return Fail("cpt_set_env_texture");
+        env_uploaded_ = true;
+    }
+    return true;
+}
+
+// InitBuffers (path_tracer.cu:44-115): per-pixel buffers and RNG when the size changes.
+bool PathTracer::EnsureFrame(const MotionalCamera& cam) {
+    if (cam.width_ != width_ || cam.height_ != height_) {
+        if (cpt_set_frame(ctx_, cam.width_, cam.height_, nullptr, 0) != CPT_OK) return Fail("cpt_set_frame");
+        width_ = cam.width_;
+        height_ = cam.height_;
+        rng_ready_ = false;
+        output_buffer_.assign((size_t)width_ * height_ * 4, 0);
+    }
+    if (!rng_ready_) {
+        if (cpt_init_rng(ctx_, seed_) != CPT_OK) return Fail("cpt_init_rng");
+        rng_ready_ = true;
+    }
+    return true;
+}
+
+bool PathTracer::RenderPass(MotionalCamera& cam, int spp, bool accumulate) {
+    if (!SyncScene() || !EnsureFrame(cam)) return false;
+    uint32_t flags = CPT_RENDER_AUX | (accumulate ? CPT_RENDER_ACCUMULATE : 0u) | CPT_RENDER_SYNC;
+    if (cpt_render(ctx_, reinterpret_cast<const cpt_camera*>(&cam), spp, (int)max_recursion_depth_, flags) != CPT_OK)
+        return Fail("cpt_render");
+    return true;
+}
+
+void PathTracer::InitPipeline() {
+    SceneBVH::BuildBVH();   // bvh.cu:116-120
+    if (running_.exchange(true)) return;
+    worker_ = std::thread(&PathTracer::PipelineLoop, this);
+}
+
+void PathTracer::DispatchRay(DispatchRayArgs args) {
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        tasks_queue_.push_back(args);
+    }
+    cv_.notify_one();
+}
+
+// PipelineLoop (path_tracer.cu:256-306): one sample per pixel per task, then denoise + mix and
+// the callback with the BGRA8 frame, on this thread.
+void PathTracer::PipelineLoop() {
+    if (camera_) {
+        MotionalCamera first = camera_->GetCopy();   // the reference's InitBuffers(GetCopy()) (:258)
+        std::lock_guard<std::mutex> lk(mu_);
+        if (SyncScene()) EnsureFrame(first);
+    }
+    while (running_.load()) {
+        DispatchRayArgs task;
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return !tasks_queue_.empty() || !running_.load(); });
+            if (!running_.load()) break;
+            task = tasks_queue_.front();
+            tasks_queue_.pop_front();
+        }
+        if (!camera_) continue;
+        MotionalCamera cma = camera_->GetCopy();
+        bool ok;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            ok = RenderPass(cma, 1, false);
+            if (ok && cpt_denoise_mix(ctx_, cma.cur_sample_idx_, output_buffer_.data()) != CPT_OK)
+                ok = Fail("cpt_denoise_mix");
+        }
+        if (ok && task.Callback) task.Callback(output_buffer_.data(), width_, height_, task.cbParam);
+    }
+}
+
+void PathTracer::Stop() {
+    if (!running_.exchange(false)) return;
+    cv_.notify_all();
+    if (worker_.joinable()) worker_.join();
+}
+
+bool PathTracer::Render(int spp, bool accumulate) {
+    if (!camera_) {
+        err_ = "Render: SetCamera first";
+        return false;
+    }
+    if (SceneBVH::BuildId() == 0) SceneBVH::BuildBVH();
+    MotionalCamera cma = camera_->GetCopy();
+    std::lock_guard<std::mutex> lk(mu_);
+    return RenderPass(cma, spp, accumulate);
+}
+
+bool PathTracer::ReadRadiance(std::vector<float>& rgb) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!ctx_ || width_ == 0) {
+        err_ = "ReadRadiance: nothing rendered";
+        return false;
+    }
+    std::vector<float> acc((size_t)width_ * height_ * 4);
+    if (cpt_read_accum(ctx_, acc.data()) != CPT_OK) return Fail("cpt_read_accum");
+    rgb.resize((size_t)width_ * height_ * 3);
+    for (size_t i = 0; i < (size_t)width_ * height_; ++i) {
+        float n = acc[4 * i + 3] > 0.f ? acc[4 * i + 3] : 1.f;
+        rgb[3 * i] = acc[4 * i] / n;
+        rgb[3 * i + 1] = acc[4 * i + 1] / n;
+        rgb[3 * i + 2] = acc[4 * i + 2] / n;
+    }
+    return true;
+}
+
+bool PathTracer::ReadFrameBGRA(std::vector<uint8_t>& bgra) {
+    std::lock_guard<std::mutex> lk(mu_);
+    bgra = output_buffer_;
+    return !bgra.empty();
+}
+
+bool PathTracer::SaveRadiancePFM(const std::string& path) {
+    std::vector<float> rgb;
+    if (!ReadRadiance(rgb)) return false;
+    std::ofstream f(path, std::ios::binary);
+    if (!f) {
+        err_ = "SaveRadiancePFM: cannot open " + path;
+        return false;
+    }
+    f << "PF\n" << width_ << " " << height_ << "\n-1.0\n";
+    for (int y = height_ - 1; y >= 0; --y)   // PFM rows are bottom-to-top
+        f.write(reinterpret_cast<const char*>(&rgb[(size_t)y * width_ * 3]), (std::streamsize)width_ * 3 * sizeof(float));
+    return (bool)f;
+}
+
+bool PathTracer::GetStats(cpt_stats* out) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!ctx_) return false;
+    return cpt_get_stats(ctx_, out) == CPT_OK;
+}

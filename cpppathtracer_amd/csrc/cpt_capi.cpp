@@ -300,6 +300,8 @@ struct cpt_ctx {
 
     unsigned long long* d_stats = nullptr;
     uint32_t* d_work = nullptr;
+    float* d_mix = nullptr;      // display running mean (Mix), rgb per pixel
+    uint8_t* d_bgra = nullptr;   // display frame
     float last_kernel_ms = 0.f;
     int last_launches = 0;
 
@@ -343,6 +345,8 @@ void free_frame(cpt_ctx* c) {
     (void)hipFree(c->d_accum); c->d_accum = nullptr;
     (void)hipFree(c->d_normal); c->d_normal = nullptr;
     (void)hipFree(c->d_depth); c->d_depth = nullptr;
+    (void)hipFree(c->d_mix); c->d_mix = nullptr;
+    (void)hipFree(c->d_bgra); c->d_bgra = nullptr;
     (void)hipFree(c->d_scratch_w); c->d_scratch_w = nullptr;
     (void)hipFree(c->d_scratch_m); c->d_scratch_m = nullptr;
     c->frame_set = c->rng_set = false;
@@ -839,9 +843,38 @@ int cpt_last_kernel_stats(cpt_ctx* c, float* avg_ms, int* launches) {
 }
 
 int cpt_denoise_mix(cpt_ctx* c, uint32_t cur_sample_idx, uint8_t* bgra_host) {
-    (void)cur_sample_idx;
-    (void)bgra_host;
-    return c ? fail(c, CPT_ERR_UNSUPPORTED, "cpt_denoise_mix: display path not built yet") : CPT_ERR_INVALID_ARG;
+    if (!c) return CPT_ERR_INVALID_ARG;
+    if (!c->frame_set || c->n_rows != c->height) return fail(c, CPT_ERR_STATE, "cpt_denoise_mix: needs a full frame");
+    for (int y = 0; y < c->height; ++y)
+        if (c->rows_h[y] != y) return fail(c, CPT_ERR_STATE, "cpt_denoise_mix: needs rows 0..height-1 in order");
+    if (!c->d_normal || !c->d_depth) return fail(c, CPT_ERR_STATE, "cpt_denoise_mix: render with CPT_RENDER_AUX first");
+    if (cur_sample_idx == 0) return fail(c, CPT_ERR_INVALID_ARG, "cpt_denoise_mix: cur_sample_idx must be >= 1");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t npix = (size_t)c->width * c->height;
+    hipStream_t s = c->stream();
+    if (!c->d_mix) {
+        HIP_TRY(c, hipMalloc((void**)&c->d_mix, npix * 3 * sizeof(float)));
+        HIP_TRY(c, hipMemsetAsync(c->d_mix, 0, npix * 3 * sizeof(float), s));
+    }
+    if (!c->d_bgra) {
+        HIP_TRY(c, hipMalloc((void**)&c->d_bgra, npix * 4));
+        HIP_TRY(c, hipMemsetAsync(c->d_bgra, 0, npix * 4, s));
+    }
+    HIP_TRY(c, cpt::launch_denoise_mix(c->d_accum, c->d_normal, c->d_depth, c->d_mix, c->d_bgra, c->width, c->height,
+                                      cur_sample_idx, s));
+    if (bgra_host) {
+        HIP_TRY(c, hipMemcpyAsync(bgra_host, c->d_bgra, npix * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipStreamSynchronize(s));
+    }
+    return CPT_OK;
+}
+
+int cpt_reset_display(cpt_ctx* c) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t npix = (size_t)c->width * c->height;
+    if (c->d_mix) HIP_TRY(c, hipMemsetAsync(c->d_mix, 0, npix * 3 * sizeof(float), c->stream()));
+    return CPT_OK;
 }
 
 int cpt_math_batch(cpt_ctx* c, int op, const float* a, const float* b, float* out, size_t n) {

@@ -46,5 +46,7 @@ hipError_t launch_math_batch(int op, const float* a, const float* b, float* out,
 hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len,
                                 hipStream_t stream);
 int lds_node_capacity();
+hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
+                              int width, int height, uint32_t cur_sample_idx, hipStream_t stream);
 
 }  // namespace cpt

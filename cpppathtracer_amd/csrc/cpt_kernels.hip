@@ -905,6 +905,95 @@ __global__ void k_rng_pixels(const uint32_t* __restrict__ rowmats, const uint32_
 }
 
 // ======================================================================================
+// Display path: Denoising + Mix (path_tracer.cu:177-254) fused into one stencil kernel.
+//
+// Input: the pass radiance (accumulator rgb / pass count) and first-hit normals of the
+// last render; depth is the constant 1e30 (a18), so its weight is exp(0) = 1.  The
+// reference's launch covers W' x H' = 16*floor(W/16) x 16*floor(H/16) pixels and indexes
+// neighbours by LINEAR offset v*W' + u, so x +- 1, 2 wraps into the adjacent row and only
+// offsets outside [0, W'*H') get zero weight (path_tracer.cu:205-216); reproduced here.
+// Weights min(exp(-d2/M_PI), 1.0) are double (path_tracer.cu:215-222).  Mix:
+// mix = lerp(mix, clamp(denoised, 0, 1), 1/cur_sample_idx); bytes 0..2 = 255.99*(b, g, r)
+// (path_tracer.cu:241-254); the alpha byte is not written.
+// ======================================================================================
+__device__ __forceinline__ float dn_weight(float dist2) {
+    double w = dm::exp(-((double)dist2) / REF_PI);
+    return (float)(w < 1.0 ? w : 1.0);
+}
+
+__global__ void k_denoise_mix(const float4* __restrict__ accum, const float* __restrict__ normal,
+                              const float* __restrict__ depth, float* __restrict__ mix, uint8_t* __restrict__ out,
+                              int width, int height, int w_eff, int h_eff, float inv_idx) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y * blockDim.y + threadIdx.y;
+    if (x >= w_eff || y >= h_eff) return;
+    const float kernel5[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
+                                 {4.f, 16.f, 26.f, 16.f, 4.f},
+                                 {7.f, 26.f, 41.f, 26.f, 7.f},
+                                 {4.f, 16.f, 26.f, 16.f, 4.f},
+                                 {1.f, 4.f, 7.f, 4.f, 1.f}};
+    auto radiance = [&](int px) {
+        const float4 a = accum[px];
+        return a.w != 0.f ? mk(a.x, a.y, a.z) / a.w : mk(a.x, a.y, a.z);
+    };
+    const int self = y * width + x;
+    const v3 cval = radiance(self);
+    const v3 nval = mk(normal[3 * self], normal[3 * self + 1], normal[3 * self + 2]);
+    const float pval = depth[self];
+    v3 sum = mk1(0.f);
+    float cum_w = 0.0f;
+    const int limit = w_eff * h_eff;
+    for (int i = 0; i < 5; ++i) {
+        for (int j = 0; j < 5; ++j) {
+            const int u = x + (i - 2), v = y + (j - 2);
+            const int cur_off = v * w_eff + u;
+            float weight;
+            v3 ctmp;
+            if (cur_off < 0 || cur_off >= limit) {
+                weight = 0.f * 0.f * 0.f;
+                ctmp = mk1(0.f);
+            } else {
+                const int px = (cur_off / w_eff) * width + (cur_off % w_eff);
+                ctmp = radiance(px);
+                v3 t = cval - ctmp;
+                const float c_w = dn_weight(dot(t, t));
+                const v3 ntmp = mk(normal[3 * px], normal[3 * px + 1], normal[3 * px + 2]);
+                t = nval - ntmp;
+                const double dn = (double)dot(t, t);
+                const float n_w = dn_weight((float)(dn > 0.0 ? dn : 0.0));
+                const float ptmp = depth[px];
+                const float p_w = dn_weight((pval - ptmp) * (pval - ptmp));
+                weight = c_w * n_w * p_w;
+            }
+            sum = sum + (weight * kernel5[i][j]) * ctmp;
+            cum_w += weight * kernel5[i][j];
+        }
+    }
+    const v3 dn = sum / cum_w;
+    const v3 cl = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),
+                     __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));
+    v3 m = mk(mix[3 * self], mix[3 * self + 1], mix[3 * self + 2]);
+    m = m + inv_idx * (cl - m);      // lerp(a, b, t) = a + t*(b-a) (helper_math.h:1154-1157)
+    mix[3 * self] = m.x;
+    mix[3 * self + 1] = m.y;
+    mix[3 * self + 2] = m.z;
+    out[4 * (size_t)self + 0] = (uint8_t)(255.99f * m.z);
+    out[4 * (size_t)self + 1] = (uint8_t)(255.99f * m.y);
+    out[4 * (size_t)self + 2] = (uint8_t)(255.99f * m.x);
+}
+
+hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
+                              int width, int height, uint32_t cur_sample_idx, hipStream_t stream) {
+    const int w_eff = 16 * (width / 16), h_eff = 16 * (height / 16);
+    if (w_eff == 0 || h_eff == 0) return hipSuccess;
+    const float inv_idx = 1.f / float(cur_sample_idx);
+    dim3 block(16, 16), grid(w_eff / 16, h_eff / 16);
+    hipLaunchKernelGGL(k_denoise_mix, grid, block, 0, stream, accum, normal, depth, mix, out, width, height, w_eff,
+                       h_eff, inv_idx);
+    return hipGetLastError();
+}
+
+// ======================================================================================
 // Device-math KAT (see cpt.h cpt_math_batch).
 // ======================================================================================
 __global__ void k_math_batch(int op, const float* a, const float* b, float* out, size_t n) {

@@ -179,6 +179,15 @@ class Renderer:
                  for v in out[1:1 + min(cnt, examples)]]
         return cnt, pairs
 
+    def denoise_mix(self, cur_sample_idx):
+        """Denoising + Mix display pass; returns the BGRA8 frame (height, width, 4)."""
+        out = np.zeros((self.height, self.width, 4), dtype=np.uint8)
+        self._check(self._L.cpt_denoise_mix(self._ctx, cur_sample_idx, _p(out)))
+        return out
+
+    def reset_display(self):
+        self._check(self._L.cpt_reset_display(self._ctx))
+
     def math_batch(self, op, a, b=None):
         a = np.ascontiguousarray(a, dtype=np.float32)
         b = np.ascontiguousarray(b if b is not None else np.zeros_like(a), dtype=np.float32)

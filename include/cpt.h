@@ -192,6 +192,9 @@ int cpt_last_kernel_stats(cpt_ctx* ctx, float* avg_ms, int* launches);
  * radiance (accumulator / pass count), running-mean Mix with weight 1/cur_sample_idx,
  * BGRA8 out (alpha byte untouched).  Needs a full frame (rows == NULL). */
 int cpt_denoise_mix(cpt_ctx* ctx, uint32_t cur_sample_idx, uint8_t* bgra_host);
+/* Zero the Mix running mean (the reference's buffer starts uninitialised; here it is zeroed
+ * when the frame is created and by this call). */
+int cpt_reset_display(cpt_ctx* ctx);
 
 /* Device-math known-answer surface used by the parity tests: op 0 powf(a,b), 1 sinf(a),
  * 2 cosf(a), 3 asinf(a), 4 atanf(a), 5 (float)pow((double)a, 1.0/(double)b),

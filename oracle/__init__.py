@@ -63,6 +63,8 @@ def lib():
         L.or_camera_get_copy.restype = None
         L.or_build_bvh.argtypes = [P, i32, P, P, i32]
         L.or_build_bvh.restype = i32
+        L.or_denoise_mix.argtypes = [P, P, P, P, P, i32, i32, ctypes.c_uint32]
+        L.or_denoise_mix.restype = None
         L.or_render.argtypes = [P, i32, P, P, i32, i32, i32, P, i32, i32, i32, P, P, P, P, P, i32, i32]
         L.or_render.restype = i32
         _lib = L
@@ -149,3 +151,10 @@ def render(objs, cam, env, rows, spp, max_depth, rng, accum=None, want_aux=False
         raise ValueError(f"or_render failed: {rc}")
     st = dict(zip(("segments", "nodes", "prims", "hits", "misses"), (int(x) for x in stats)))
     return accum, st, normal, depth
+
+
+def denoise_mix(accum, normal, depth, mix, out, width, height, cur_sample_idx):
+    """Denoising + Mix on host arrays (mix [W*H,3] float32 and out [H,W,4] uint8 in/out)."""
+    for a, dt in ((accum, np.float32), (normal, np.float32), (depth, np.float32), (mix, np.float32), (out, np.uint8)):
+        assert a.dtype == dt and a.flags.c_contiguous
+    lib().or_denoise_mix(_ptr(accum), _ptr(normal), _ptr(depth), _ptr(mix), _ptr(out), width, height, cur_sample_idx)

@@ -1127,4 +1127,69 @@ int or_render(const void* objs, int n_objs, const void* camera, const uint8_t* e
     return 0;
 }
 
+// Denoising + Mix (path_tracer.cu:177-254) for a full W x H frame.  radiance = accum rgb /
+// pass count; neighbours by linear offset over the W' x H' = 16*floor(W/16) x 16*floor(H/16)
+// launch (rows wrap); weights in double; mix = lerp(mix, clamp(dn, 0, 1), 1/idx); bytes
+// 0..2 = 255.99*(b, g, r); alpha untouched.
+void or_denoise_mix(const float* accum, const float* normal, const float* depth, float* mix, uint8_t* out, int W,
+                    int H, uint32_t cur_sample_idx) {
+    const int we = 16 * (W / 16), he = 16 * (H / 16);
+    const float kernel[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
+                                {4.f, 16.f, 26.f, 16.f, 4.f},
+                                {7.f, 26.f, 41.f, 26.f, 7.f},
+                                {4.f, 16.f, 26.f, 16.f, 4.f},
+                                {1.f, 4.f, 7.f, 4.f, 1.f}};
+    auto rad = [&](int px) {
+        const float* a = accum + 4 * (size_t)px;
+        return a[3] != 0.f ? divs(mk(a[0], a[1], a[2]), a[3]) : mk(a[0], a[1], a[2]);
+    };
+    auto nrm = [&](int px) { return mk(normal[3 * px], normal[3 * px + 1], normal[3 * px + 2]); };
+    auto wgt = [](float d2) {
+        double w = dm_exp(-((double)d2) / REF_PI);   // min(exp(-d2/M_PI), 1.0)
+        return (float)(w < 1.0 ? w : 1.0);
+    };
+    const float inv_idx = 1.f / float(cur_sample_idx);
+    for (int y = 0; y < he; ++y)
+        for (int x = 0; x < we; ++x) {
+            const int self = y * W + x;
+            f3 cval = rad(self), nval = nrm(self);
+            float pval = depth[self];
+            f3 sum = mk1(0.f);
+            float cum_w = 0.0f;
+            for (int i = 0; i < 5; ++i)
+                for (int j = 0; j < 5; ++j) {
+                    int u = x + (i - 2), v = y + (j - 2);
+                    int cur_off = v * we + u;
+                    float weight;
+                    f3 ctmp;
+                    if (cur_off < 0 || cur_off >= we * he) {
+                        weight = 0.f;
+                        ctmp = mk1(0.f);
+                    } else {
+                        int px = (cur_off / we) * W + (cur_off % we);
+                        ctmp = rad(px);
+                        f3 t = sub(cval, ctmp);
+                        float c_w = wgt(dot(t, t));
+                        t = sub(nval, nrm(px));
+                        double dn = (double)dot(t, t);
+                        float n_w = wgt((float)(dn > 0.0 ? dn : 0.0));
+                        float ptmp = depth[px];
+                        float p_w = wgt((pval - ptmp) * (pval - ptmp));
+                        weight = c_w * n_w * p_w;
+                    }
+                    sum = add(sum, mul(weight * kernel[i][j], ctmp));
+                    cum_w += weight * kernel[i][j];
+                }
+            f3 dn = divs(sum, cum_w);
+            f3 cl = mk(fmaxf(0.f, fminf(dn.x, 1.f)), fmaxf(0.f, fminf(dn.y, 1.f)), fmaxf(0.f, fminf(dn.z, 1.f)));
+            float* m = mix + 3 * (size_t)self;
+            f3 mv = mk(m[0], m[1], m[2]);
+            mv = add(mv, mul(inv_idx, sub(cl, mv)));
+            m[0] = mv.x; m[1] = mv.y; m[2] = mv.z;
+            out[4 * (size_t)self + 0] = (uint8_t)(255.99f * mv.z);
+            out[4 * (size_t)self + 1] = (uint8_t)(255.99f * mv.y);
+            out[4 * (size_t)self + 2] = (uint8_t)(255.99f * mv.x);
+        }
+}
+
 }  // extern "C"

@@ -1,0 +1,80 @@
+"""Row-tiled multi-rank rendering on CPU (gloo, world_size 2): the host logic bench.py runs
+on N GPUs over RCCL.  Each rank renders its interleaved 16-row blocks (the oracle stands in
+for the GPU in this CPU-only test), the fp32 tiles are all-gathered and stitched, and the
+result must equal a monolithic render bit for bit (per-pixel streams depend only on
+(seed, x, y), path_tracer.cu:36-42)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cpppathtracer_amd import scenes, texture_io, tiling
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, W, H, spp, depth, q):
+    import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sky = texture_io.load_cptex()
+    objs = scenes.scene_s1000()
+    cam = oracle.camera_get_copy(scenes.camera_for(W, H))
+    rows = tiling.partition_rows(H, world, rank)
+    rng = oracle.init_rng(1234, W, rows)
+    acc, st, _, _ = oracle.render(objs, cam, sky, rows, spp, depth, rng)
+    mr = tiling.max_rows(H, world)
+    send = torch.zeros((mr * W, 4), dtype=torch.float32)
+    send[: rows.size * W] = torch.from_numpy(acc)
+    gathered = torch.zeros((world * mr * W, 4), dtype=torch.float32)
+    dist.all_gather_into_tensor(gathered, send)
+    stv = torch.tensor([st["segments"], st["nodes"]], dtype=torch.float64)
+    dist.all_reduce(stv)
+    if rank == 0:
+        fb = tiling.stitch(gathered.numpy(), H, W, world)
+        idx = tiling.stitch_index(H, W, world)
+        fb2 = gathered.numpy().reshape(world * mr, W, 4)[idx].reshape(H * W, 4)
+        q.put((fb, fb2, stv.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,H", [(2, 40), (3, 37)])
+def test_tiled_render_equals_monolithic(oracle_mod, sky, world, H):
+    W, spp, depth = 24, 2, 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, W, H, spp, depth, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    fb, fb2, st = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    objs = scenes.scene_s1000()
+    cam = oracle_mod.camera_get_copy(scenes.camera_for(W, H))
+    rows = np.arange(H, dtype=np.int32)
+    rng = oracle_mod.init_rng(1234, W, rows)
+    mono, mst, _, _ = oracle_mod.render(objs, cam, sky, rows, spp, depth, rng)
+    np.testing.assert_array_equal(fb.view(np.uint32), mono.view(np.uint32))
+    np.testing.assert_array_equal(fb2, fb)
+    assert st[0] == mst["segments"] and st[1] == mst["nodes"]
+
+
+@pytest.mark.parametrize("H,world", [(1080, 1), (1080, 2), (1080, 4), (1080, 8), (2160, 8), (37, 3), (5, 8)])
+def test_partition_covers_rows_once(H, world):
+    allr = np.concatenate([tiling.partition_rows(H, world, r) for r in range(world)])
+    assert np.array_equal(np.sort(allr), np.arange(H))
+    sizes = [tiling.partition_rows(H, world, r).size for r in range(world)]
+    assert max(sizes) - min(sizes) <= tiling.BLOCK_ROWS
