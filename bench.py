@@ -34,12 +34,6 @@ def byte_model(st, paths):
             + 16 * paths)
 
 
-def partition_rows(height, world, rank, block=16):
-    """Interleaved row blocks: block b = rows [16b, 16b+16) goes to rank b % world."""
-    ys = np.arange(height, dtype=np.int32)
-    return ys[(ys // block) % world == rank]
-
-
 def cpu_baseline(cfg, objs, sky, cam, seconds_hint=15.0, threads=None):
     """The oracle (scalar C++ restatement, test infrastructure) on a bounded sample: 16 rows
     spread over the image, full width, `spp_sample` passes (a pixel's passes are sequential, so
@@ -89,7 +83,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from cpppathtracer_amd import Renderer, camera_get_copy, scenes, texture_io
+    from cpppathtracer_amd import Renderer, camera_get_copy, scenes, texture_io, tiling
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -114,7 +108,7 @@ def main():
     objs = scenes.SCENES[cfg["scene"]]()
     sky = texture_io.load_cptex()
     cam = camera_get_copy(scenes.camera_for(W, H))
-    rows = partition_rows(H, world, rank)
+    rows = tiling.partition_rows(H, world, rank)
 
     r = Renderer(torch.cuda.current_device())
     stream = torch.cuda.current_stream()
@@ -128,15 +122,28 @@ def main():
     t_init = time.perf_counter() - t_init
 
     npix_local = rows.size * W
-    max_rows = int(max(partition_rows(H, world, k).size for k in range(world)))
+    max_rows = tiling.max_rows(H, world)
     send = torch.zeros((max_rows * W, 4), dtype=torch.float32, device=dev)
     gathered = torch.zeros((world * max_rows * W, 4), dtype=torch.float32, device=dev) if world > 1 else None
+    stitch_idx = torch.from_numpy(tiling.stitch_index(H, W, world)).to(dev) if world > 1 else None
+    kernel_events = []
 
-    def step():
+    def step(timed=False):
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
         r.render(cam, spp, depth)
+        if timed:
+            e1.record(stream)
+            kernel_events.append((e0, e1))
         if world > 1:
+            # RCCL all-gather of the fp32 tiles over xGMI, then the on-device stitch into the
+            # full framebuffer (rank 0 keeps it; every rank holds a copy after all-gather)
             r.copy_accum_device(send.data_ptr(), npix_local * 16)
             dist.all_gather_into_tensor(gathered, send)
+            fb = gathered.view(world * max_rows, W, 4).index_select(0, stitch_idx)
+            return fb
+        return None
 
     # Counting pass (same config, same pixels) for the algorithmic byte model; not timed.
     r.reset_stats()
@@ -153,28 +160,20 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    kernel_ms = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-        kernel_ms.append(None)
+        step(timed=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    # kernel time of the last step's render, from HIP events recorded around the launch on the
-    # launch stream (same stream as above)
-    last_kernel_ms = r.last_render_ms()
-    # per-step kernel times: re-time each step individually (untimed region) for the average
-    ks = []
-    for _ in range(max(1, min(args.steps, 3))):
-        r.render(cam, spp, depth)
-        ks.append(r.last_render_ms())
-    avg_kernel_ms = float(np.mean(ks))
+    # k_megakernel's device time per launch: HIP events recorded around each render on the
+    # launch stream (the context launches on torch's current stream, set above)
+    avg_kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in kernel_events]))
 
     t = torch.tensor([elapsed, avg_kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
