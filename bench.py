@@ -111,8 +111,13 @@ def main():
     rows = tiling.partition_rows(H, world, rank)
 
     r = Renderer(torch.cuda.current_device())
-    stream = torch.cuda.current_stream()
-    r.set_stream(stream.cuda_stream)          # our kernels and torch's collectives share one stream
+    # One non-default HIP stream for everything: the render kernels (via cpt_set_stream), the
+    # RCCL all-gather and the timing events.  (The default stream's handle is 0, which the
+    # C-ABI reads as "use the context's own stream".)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    assert stream.cuda_stream != 0
+    r.set_stream(stream.cuda_stream)
     r.set_scene(objs)
     r.set_env(sky)
     r.set_frame(W, H, rows)
