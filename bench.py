@@ -74,6 +74,7 @@ def main():
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--path", default="megakernel", choices=["megakernel", "wavefront"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=None,
@@ -137,7 +138,7 @@ def main():
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        r.render(cam, spp, depth)
+        r.render(cam, spp, depth, path=args.path)
         if timed:
             e1.record(stream)
             kernel_events.append((e0, e1))
@@ -152,7 +153,7 @@ def main():
 
     # Counting pass (same config, same pixels) for the algorithmic byte model; not timed.
     r.reset_stats()
-    r.render(cam, spp, depth, stats=True)
+    r.render(cam, spp, depth, stats=True, path=args.path)
     torch.cuda.synchronize()
     st_local = r.stats()
     st_vec = torch.tensor([st_local[k] for k in ("segments", "nodes", "prims", "hits", "misses")],
@@ -215,7 +216,7 @@ def main():
             "config": {
                 "workload": f"{args.config}: {cfg['scene']} {W}x{H} {spp}spp depth {depth}",
                 "width": W, "height": H, "spp": spp, "max_depth": depth, "seed": cfg["seed"],
-                "rows_rendered": H, "path": "megakernel",
+                "rows_rendered": H, "path": args.path,
                 "parallelism": f"row-tiled x{world} (interleaved 16-row blocks)" + (", RCCL all-gather" if world > 1 else ""),
             },
             "roofline": {
@@ -225,7 +226,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_megakernel",
+                "kernel": "k_megakernel" if args.path == "megakernel" else "wavefront (k_wf_extend+k_wf_shade per bounce)",
                 "kernel_avg_ms": round(avg_kernel_ms, 3),
                 "bytes_per_launch": int(bytes_launch),
                 "byte_model": "SURVEY.md 8(d): 76 S + 32 nodes + 32 prims + 40 hits + 16 misses + 16 P",

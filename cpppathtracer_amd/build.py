@@ -14,12 +14,14 @@ LIB_PATH = os.path.join(PKG_DIR, "libcpt.so")
 
 SOURCES = [
     os.path.join(CSRC, "cpt_kernels.hip"),
+    os.path.join(CSRC, "cpt_wavefront.hip"),
     os.path.join(CSRC, "cpt_capi.cpp"),
     os.path.join(CSRC, "cpt_api.cpp"),
 ]
 HEADERS = [
     os.path.join(CSRC, "cpt_device.hpp"),
     os.path.join(CSRC, "cpt_internal.hpp"),
+    os.path.join(CSRC, "cpt_path.hpp"),
     os.path.join(REPO_DIR, "include", "cpt.h"),
 ]
 

@@ -300,6 +300,8 @@ struct cpt_ctx {
 
     unsigned long long* d_stats = nullptr;
     uint32_t* d_work = nullptr;
+    cpt::WfState wf{};           // wavefront path state (allocated on first use)
+    bool wf_ready = false;
     float* d_mix = nullptr;      // display running mean (Mix), rgb per pixel
     uint8_t* d_bgra = nullptr;   // display frame
     float last_kernel_ms = 0.f;
@@ -346,6 +348,15 @@ void free_frame(cpt_ctx* c) {
     (void)hipFree(c->d_normal); c->d_normal = nullptr;
     (void)hipFree(c->d_depth); c->d_depth = nullptr;
     (void)hipFree(c->d_mix); c->d_mix = nullptr;
+    for (float4** a : {&c->wf.ray_o, &c->wf.ray_d, &c->wf.att, &c->wf.rad, &c->wf.hit_p, &c->wf.hit_n, &c->wf.aux}) {
+        (void)hipFree(*a);
+        *a = nullptr;
+    }
+    (void)hipFree(c->wf.queue[0]); c->wf.queue[0] = nullptr;
+    (void)hipFree(c->wf.queue[1]); c->wf.queue[1] = nullptr;
+    (void)hipFree(c->wf.ident); c->wf.ident = nullptr;
+    (void)hipFree(c->wf.counts); c->wf.counts = nullptr;
+    c->wf_ready = false;
     (void)hipFree(c->d_bgra); c->d_bgra = nullptr;
     (void)hipFree(c->d_scratch_w); c->d_scratch_w = nullptr;
     (void)hipFree(c->d_scratch_m); c->d_scratch_m = nullptr;
@@ -697,7 +708,6 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     if (!c->frame_set || !c->rng_set) return fail(c, CPT_ERR_STATE, "cpt_render: cpt_set_frame + cpt_init_rng first");
     if (cam->width != c->width || cam->height != c->height)
         return fail(c, CPT_ERR_INVALID_ARG, "cpt_render: camera %dx%d vs frame %dx%d", cam->width, cam->height, c->width, c->height);
-    if (flags & CPT_PATH_WAVEFRONT) return fail(c, CPT_ERR_UNSUPPORTED, "cpt_render: wavefront path not built yet");
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t s = c->stream();
     const bool aux = (flags & CPT_RENDER_AUX) != 0;
@@ -738,11 +748,31 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     p.spp = spp;
     p.max_depth = max_depth;
     p.accumulate = (flags & CPT_RENDER_ACCUMULATE) ? 1 : 0;
+    const bool wavefront = (flags & CPT_PATH_WAVEFRONT) != 0;
+    if (wavefront && !c->wf_ready && c->n_rows > 0) {
+        const size_t npix = (size_t)c->n_rows * c->width;
+        for (float4** a : {&c->wf.ray_o, &c->wf.ray_d, &c->wf.att, &c->wf.rad, &c->wf.hit_p, &c->wf.hit_n, &c->wf.aux})
+            HIP_TRY(c, hipMalloc((void**)a, npix * sizeof(float4)));
+        HIP_TRY(c, hipMalloc((void**)&c->wf.queue[0], npix * sizeof(int32_t)));
+        HIP_TRY(c, hipMalloc((void**)&c->wf.queue[1], npix * sizeof(int32_t)));
+        HIP_TRY(c, hipMalloc((void**)&c->wf.ident, npix * sizeof(int32_t)));
+        HIP_TRY(c, hipMalloc((void**)&c->wf.counts, 8 * sizeof(uint32_t)));
+        HIP_TRY(c, cpt::wavefront_build_ident(p, c->wf, s));
+        c->wf_ready = true;
+    }
     HIP_TRY(c, hipEventRecord(c->ev_start, s));
-    HIP_TRY(c, cpt::launch_megakernel(p, (flags & CPT_RENDER_STATS) != 0, aux, s));
+    if (wavefront) {
+        if (!p.accumulate && c->n_rows > 0)
+            HIP_TRY(c, hipMemsetAsync(c->d_accum, 0, (size_t)c->n_rows * c->width * sizeof(float4), s));
+        int launches = 0;
+        HIP_TRY(c, cpt::launch_wavefront(p, c->wf, (flags & CPT_RENDER_STATS) != 0, aux, s, &launches));
+        c->last_launches = launches;
+    } else {
+        HIP_TRY(c, cpt::launch_megakernel(p, (flags & CPT_RENDER_STATS) != 0, aux, s));
+        c->last_launches = 1;
+    }
     HIP_TRY(c, hipEventRecord(c->ev_stop, s));
     c->have_timing = true;
-    c->last_launches = 1;
     if (flags & CPT_RENDER_SYNC) HIP_TRY(c, hipStreamSynchronize(s));
     return CPT_OK;
 }

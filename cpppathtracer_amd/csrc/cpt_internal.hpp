@@ -38,7 +38,17 @@ struct KParams {
     int spp, max_depth, accumulate;
 };
 
+// Wavefront path state (cpt_wavefront.hip): SoA float4 arrays indexed by pixel + queues.
+struct WfState {
+    float4 *ray_o, *ray_d, *att, *rad, *hit_p, *hit_n, *aux;
+    int32_t* queue[2];
+    int32_t* ident;       // tile-ordered identity queue (first bounce)
+    uint32_t* counts;     // [0], [1]: queue sizes; [3]: ident size
+};
+
 hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t stream);
+hipError_t launch_wavefront(const KParams& p, WfState& w, bool stats, bool aux, hipStream_t stream, int* launches);
+hipError_t wavefront_build_ident(const KParams& p, WfState& w, hipStream_t stream);
 hipError_t launch_prepare_materials(Mat* mats, int n, hipStream_t stream);
 hipError_t launch_init_rng(const uint32_t* jumps, const uint32_t seed_state[6], int width, const int32_t* rows,
                            int n_rows, uint32_t* scratch_w, uint32_t* scratch_mats, uint32_t* rng, hipStream_t stream);

@@ -13,549 +13,9 @@
 
 #include <algorithm>
 
-#include "cpt_device.hpp"
-#include "cpt_internal.hpp"
+#include "cpt_path.hpp"
 
 namespace cpt {
-
-// ======================================================================================
-// Environment texture (textures.cu:14-71): uchar4 cudaArray, normalized coordinates,
-// Mirror addressing, Linear filter, NormalizedFloat read.  Texels live as packed RGBA8
-// words, `cols` valid columns per row (the reference uploads width/4 texels per row,
-// textures.cu:32-33); texels at x >= cols read as 0.  Bilinear weights are rounded to
-// 1/256 (9-bit fixed point, 8 fractional bits), computed and blended in f32 in a fixed
-// order.
-// ======================================================================================
-__device__ __forceinline__ int mirror_index(int i, int n) {
-    int period = 2 * n;
-    int m = i % period;
-    if (m < 0) m += period;
-    if (m >= n) m = period - 1 - m;
-    return m;
-}
-
-__device__ __forceinline__ void texel(const KParams& p, int i, int j, float out[3]) {
-    int x = mirror_index(i, p.env_w), y = mirror_index(j, p.env_h);
-    if (x >= p.env_cols) { out[0] = out[1] = out[2] = 0.0f; return; }
-    uint32_t t = p.env[(size_t)y * p.env_cols + x];
-    out[0] = (float)(t & 0xffu) / 255.0f;
-    out[1] = (float)((t >> 8) & 0xffu) / 255.0f;
-    out[2] = (float)((t >> 16) & 0xffu) / 255.0f;
-}
-
-__device__ inline v3 tex2d(const KParams& p, float u, float v) {
-    float x = u * (float)p.env_w - 0.5f;
-    float y = v * (float)p.env_h - 0.5f;
-    if (!(x > -1e7f && x < 1e7f && y > -1e7f && y < 1e7f) || p.env_cols <= 0) return mk1(0.0f);
-    float fx = __builtin_floorf(x), fy = __builtin_floorf(y);
-    float a = __builtin_floorf((x - fx) * 256.0f + 0.5f) * 0.00390625f;
-    float b = __builtin_floorf((y - fy) * 256.0f + 0.5f) * 0.00390625f;
-    int i0 = (int)fx, j0 = (int)fy;
-    float t00[3], t10[3], t01[3], t11[3];
-    texel(p, i0, j0, t00);
-    texel(p, i0 + 1, j0, t10);
-    texel(p, i0, j0 + 1, t01);
-    texel(p, i0 + 1, j0 + 1, t11);
-    float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
-    float r[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) r[c] = ((w00 * t00[c] + w10 * t10[c]) + w01 * t01[c]) + w11 * t11[c];
-    return mk(r[0], r[1], r[2]);
-}
-
-// ======================================================================================
-// Per-segment ray with its exact reciprocals (see qdiv in cpt_device.hpp).
-// ======================================================================================
-struct RayK {
-    v3 o, d;
-    float tmin;
-    double yx, yy, yz;   // 1/d.x, 1/d.y, 1/d.z   (slab planes; d.y also for caps / platform)
-    double ya;           // 1/dot(d,d)            (sphere roots, object.cu:15-20)
-    double yc;           // 1/(dx*dx + dz*dz)     (cylinder side roots, object.cu:69-79)
-};
-
-__device__ __forceinline__ RayK make_rayk(const Ray& r) {
-    RayK k;
-    k.o = r.o;
-    k.d = r.d;
-    k.tmin = r.tmin;
-    k.yx = rcp_d(r.d.x);
-    k.yy = rcp_d(r.d.y);
-    k.yz = rcp_d(r.d.z);
-    k.ya = rcp_d(dot(r.d, r.d));
-    k.yc = rcp_d(r.d.x * r.d.x + r.d.z * r.d.z);
-    return k;
-}
-
-// ======================================================================================
-// Intersectors (object.cu:10-128) on an inline leaf.  `tmax` is the traversal's shrinking
-// closest distance (TraceRay's by-value ray, bvh.cu:167).
-// ======================================================================================
-struct Hit { v3 normal, pos; };
-
-__device__ __forceinline__ bool sphere_test(const Node& s, const RayK& ray, float& tmax, Hit& h) {
-    const v3 c = mk(s.a0, s.a1, s.a2);
-    const float radius = s.b0;
-    v3 A_C = ray.o - c;
-    float b = dot(A_C, ray.d);
-    float cc = dot(A_C, A_C) - radius * radius;
-    float a = dot(ray.d, ray.d);
-    float disc = b * b - a * cc;
-    if (disc > 0) {
-        float sq = __builtin_sqrtf(disc);
-        float temp = qdiv(-b - sq, a, ray.ya);
-        if (temp < tmax && temp > ray.tmin) {
-            tmax = temp;
-            h.pos = ray.o + temp * ray.d;
-            h.normal = (h.pos - c) / radius;        // first root: divided by the signed radius
-            return true;
-        }
-        temp = qdiv(-b + sq, a, ray.ya);
-        if (temp < tmax && temp > ray.tmin) {
-            tmax = temp;
-            h.pos = ray.o + temp * ray.d;
-            h.normal = normalize(h.pos - c);
-            return true;
-        }
-    }
-    return false;
-}
-
-__device__ __forceinline__ bool platform_test(const Node& pl, const RayK& ray, float& tmax, Hit& h) {
-    const float y_pos = pl.b1;
-    if ((ray.o.y < y_pos && ray.d.y > 0.f) || (ray.o.y > y_pos && ray.d.y < 0.f)) {
-        float temp = qdiv(y_pos - ray.o.y, ray.d.y, ray.yy);
-        if (temp < tmax && temp > ray.tmin) {
-            tmax = temp;
-            h.pos = ray.o + temp * ray.d;
-            h.normal = normalize(mk(0, -ray.d.y, 0));  // faces the ray
-            return true;
-        }
-    }
-    return false;
-}
-
-__device__ __forceinline__ bool cap_test(float cx, float cz, float radius, const RayK& ray, float& tmax, Hit& h,
-                                         float ypos) {
-    if ((ray.o.y < ypos && ray.d.y > 0.f) || (ray.o.y > ypos && ray.d.y < 0.f)) {
-        float temp = qdiv(ypos - ray.o.y, ray.d.y, ray.yy);
-        v3 hp = ray.o + temp * ray.d;
-        if (temp < tmax && temp > ray.tmin &&
-            __builtin_sqrtf((hp.x - cx) * (hp.x - cx) + (hp.z - cz) * (hp.z - cz)) < radius) {
-            tmax = temp;
-            h.pos = hp;
-            h.normal = normalize(mk(0, -ray.d.y, 0));
-            return true;
-        }
-    }
-    return false;
-}
-
-__device__ inline bool cylinder_test(const Node& cy, const RayK& ray, float& tmax, Hit& h) {
-    const float ccx = cy.a0, ccy = cy.a1, ccz = cy.a2, r = cy.b0, height = cy.b2;
-    bool ret = false;
-    float upper = ccy + height / 2;
-    if (cap_test(ccx, ccz, r, ray, tmax, h, upper)) ret = true;
-    float lower = ccy - height / 2;
-    if (cap_test(ccx, ccz, r, ray, tmax, h, lower)) ret = true;
-    float dx = ray.d.x, dz = ray.d.z;
-    float cx = ray.o.x - ccx;
-    float cz = ray.o.z - ccz;
-    float a = dx * dx + dz * dz;
-    float b = cx * dx + cz * dz;
-    float c = cx * cx + cz * cz - r * r;
-    float disc = b * b - a * c;
-    if (disc > 0.f) {
-        float sq = __builtin_sqrtf(disc);
-        float temp = qdiv(-b - sq, a, ray.yc);
-        v3 hp = ray.o + temp * ray.d;
-        if (temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper) {
-            tmax = temp;
-            h.pos = hp;
-            h.normal = normalize(mk(hp.x - ccx, 0.f, hp.z - ccz));
-            ret = true;
-        }
-        temp = qdiv(-b + sq, a, ray.yc);
-        hp = ray.o + temp * ray.d;
-        if (temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper) {
-            tmax = temp;
-            h.pos = hp;
-            h.normal = normalize(mk(hp.x - ccx, 0.f, hp.z - ccz));
-            ret = true;
-        }
-    }
-    return ret;
-}
-
-// Sphere (object.cu:10-35) and cylinder side (object.cu:81-111) share one quadratic: the
-// cylinder's 2-D terms are the sphere's 3-D ones with the y terms replaced by +0, which
-// leaves every rounding unchanged ((u + 0) + w == u + w for the squares and products here,
-// up to the sign of a zero b that cannot change the roots).  The cylinder's second root can
-// never replace an accepted first root (temp2 >= temp1 under monotone rounding), so both
-// shapes return after the first accepted root as the sphere does.
-__device__ __forceinline__ bool quad_test(const Node& nd, const RayK& ray, float& tmax, Hit& h, bool cyl,
-                                          float lower, float upper) {
-    const float cx = nd.a0, cy = nd.a1, cz = nd.a2, r = nd.b0;
-    const float ax = ray.o.x - cx, ay = ray.o.y - cy, az = ray.o.z - cz;
-    const float ay_dy = cyl ? 0.f : ay * ray.d.y;
-    const float ay_ay = cyl ? 0.f : ay * ay;
-    const float dy_dy = cyl ? 0.f : ray.d.y * ray.d.y;
-    const float a = (ray.d.x * ray.d.x + dy_dy) + ray.d.z * ray.d.z;
-    const float b = (ax * ray.d.x + ay_dy) + az * ray.d.z;
-    const float c = ((ax * ax + ay_ay) + az * az) - r * r;
-    const float disc = b * b - a * c;
-    if (!(disc > 0.f)) return false;
-    const double y = cyl ? ray.yc : ray.ya;
-    const float sq = __builtin_sqrtf(disc);
-    float temp = qdiv(-b - sq, a, y);
-    v3 hp = ray.o + temp * ray.d;
-    bool first = true;
-    if (!(temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper)) {
-        temp = qdiv(-b + sq, a, y);
-        hp = ray.o + temp * ray.d;
-        if (!(temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper)) return false;
-        first = false;
-    }
-    tmax = temp;
-    h.pos = hp;
-    const v3 v = mk(hp.x - cx, cyl ? 0.f : hp.y - cy, hp.z - cz);
-    // sphere first root: (p - c) / r with the signed radius; every other case normalizes
-    h.normal = (first && !cyl) ? v / r : normalize(v);
-    return true;
-}
-
-// ======================================================================================
-// SceneBVH::TraceRay (bvh.cu:167-205) as a stackless skip-link walk.  The nodes are stored
-// in the exact order the reference's stack DFS pops them (right child first), so visiting
-// n, then n+1 on a box hit or node.miss on a box miss / after a leaf, reproduces the
-// reference's visit sequence, leaf-before-box order and pruning against the shrinking tmax
-// one for one — no stack, no scratch memory.
-//
-// CPT_WHILEWHILE=1 selects a while-while loop (internal nodes until every lane of the wave
-// sits on a leaf, then the leaf tests together); per-lane visit order is the same either way.
-// ======================================================================================
-#ifndef CPT_WHILEWHILE
-#define CPT_WHILEWHILE 0
-#endif
-#ifndef CPT_WAVES_PER_SIMD
-#define CPT_WAVES_PER_SIMD 3   // occupancy target of k_megakernel (VGPR budget 168)
-#endif
-
-struct Counters { uint32_t segments, nodes, prims, hits, misses; };
-
-// Slab test of one internal node (bvh.cu:181-200).  The six plane distances use the exact
-// quotient; if any of them is zero/subnormal the node is redone with the IEEE divide.
-// FAST (rays without NaN): the plane distances of the axes that are used are never NaN
-// (finite box coordinate minus finite origin, times a finite reciprocal), so the ternary
-// MIN/MAX of the reference equal v_min/v_max_f32 up to the sign of a zero, which none of
-// the three comparisons can see.  Rays carrying a NaN take the exact ternary form.
-template <bool FAST>
-__device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, float tmax) {
-    float t0x = qdiv_raw(nd.a0 - ray.o.x, ray.yx), t1x = qdiv_raw(nd.b0 - ray.o.x, ray.yx);
-    float t0y = qdiv_raw(nd.a1 - ray.o.y, ray.yy), t1y = qdiv_raw(nd.b1 - ray.o.y, ray.yy);
-    float t0z = qdiv_raw(nd.a2 - ray.o.z, ray.yz), t1z = qdiv_raw(nd.b2 - ray.o.z, ray.yz);
-#if CPT_QDIV
-    float mn = __builtin_fminf(__builtin_fminf(__builtin_fminf(__builtin_fabsf(t0x), __builtin_fabsf(t1x)),
-                                               __builtin_fminf(__builtin_fabsf(t0y), __builtin_fabsf(t1y))),
-                               __builtin_fminf(__builtin_fabsf(t0z), __builtin_fabsf(t1z)));
-    if (__builtin_expect(mn < FLT_MIN_NORMAL, 0)) {
-#else
-    {
-#endif
-        t0x = (nd.a0 - ray.o.x) / ray.d.x; t1x = (nd.b0 - ray.o.x) / ray.d.x;
-        t0y = (nd.a1 - ray.o.y) / ray.d.y; t1y = (nd.b1 - ray.o.y) / ray.d.y;
-        t0z = (nd.a2 - ray.o.z) / ray.d.z; t1z = (nd.b2 - ray.o.z) / ray.d.z;
-    }
-    // axes with d == 0 are skipped (bvh.cu:182,188,194): selects, not branches
-    float lo = -DEFAULT_RAY_TMAX * 2, hi = DEFAULT_RAY_TMAX * 2;
-    float lx, hx, ly, hy, lz, hz;
-    if (FAST) {
-        lx = __builtin_fmaxf(lo, __builtin_fminf(t0x, t1x));
-        hx = __builtin_fminf(hi, __builtin_fmaxf(t0x, t1x));
-    } else {
-        lx = tmax_(lo, tmin_(t0x, t1x));
-        hx = tmin_(hi, tmax_(t0x, t1x));
-    }
-    lo = ray.d.x != 0.f ? lx : lo;
-    hi = ray.d.x != 0.f ? hx : hi;
-    if (FAST) {
-        ly = __builtin_fmaxf(lo, __builtin_fminf(t0y, t1y));
-        hy = __builtin_fminf(hi, __builtin_fmaxf(t0y, t1y));
-    } else {
-        ly = tmax_(lo, tmin_(t0y, t1y));
-        hy = tmin_(hi, tmax_(t0y, t1y));
-    }
-    lo = ray.d.y != 0.f ? ly : lo;
-    hi = ray.d.y != 0.f ? hy : hi;
-    if (FAST) {
-        lz = __builtin_fmaxf(lo, __builtin_fminf(t0z, t1z));
-        hz = __builtin_fminf(hi, __builtin_fmaxf(t0z, t1z));
-    } else {
-        lz = tmax_(lo, tmin_(t0z, t1z));
-        hz = tmin_(hi, tmax_(t0z, t1z));
-    }
-    lo = ray.d.z != 0.f ? lz : lo;
-    hi = ray.d.z != 0.f ? hz : hi;
-    return lo > hi || lo > tmax || hi < ray.tmin;
-}
-
-#ifndef CPT_UNIFIED_QUAD
-#define CPT_UNIFIED_QUAD 1
-#endif
-__device__ __forceinline__ bool leaf_test(const Node& nd, const RayK& ray, float& tmax, Hit& h) {
-    const int type = nd.code & 3;
-#if CPT_UNIFIED_QUAD
-    bool r = false;
-    float lower = -__builtin_inff(), upper = __builtin_inff();
-    if (type == 2) {
-        // Cylinder caps first (object.cu:52-77), then the side.
-        upper = nd.a1 + nd.b2 / 2;
-        if (cap_test(nd.a0, nd.a2, nd.b0, ray, tmax, h, upper)) r = true;
-        lower = nd.a1 - nd.b2 / 2;
-        if (cap_test(nd.a0, nd.a2, nd.b0, ray, tmax, h, lower)) r = true;
-    }
-    if (type == 0 || type == 2) {
-        if (quad_test(nd, ray, tmax, h, type == 2, lower, upper)) r = true;
-    } else if (type == 1) {
-        r = platform_test(nd, ray, tmax, h);
-    }
-    return r;
-#else
-    if (type == 0) return sphere_test(nd, ray, tmax, h);
-    if (type == 2) return cylinder_test(nd, ray, tmax, h);
-    if (type == 1) return platform_test(nd, ray, tmax, h);
-    return false;
-#endif
-}
-
-#ifndef CPT_LEAF_BATCH
-#define CPT_LEAF_BATCH 0   // K > 0: run the leaf phase when >= 1/K of the walking lanes wait on a leaf
-#endif
-#ifndef CPT_PREFETCH
-#define CPT_PREFETCH 1     // load both possible successors of a node while it is being tested
-#endif
-
-template <bool STATS, bool FAST>
-__device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_nodes, const RayK& ray, Hit& h,
-                                      int& code_out, Counters& cnt) {
-    float tmax = DEFAULT_RAY_TMAX;
-    bool hit = false;
-    int ni = 0;
-#if CPT_WHILEWHILE
-    while (ni < n_nodes) {
-        Node nd = nodes[ni];
-        while (nd.code < 0) {
-            if (STATS) cnt.nodes++;
-            ni = slab_reject<FAST>(nd, ray, tmax) ? nd.miss : ni + 1;
-            if (ni >= n_nodes) break;
-            nd = nodes[ni];
-        }
-        if (ni >= n_nodes) break;
-        if (STATS) { cnt.nodes++; cnt.prims++; }
-        if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
-        ni = nd.miss;
-    }
-#elif CPT_LEAF_BATCH > 0
-    // Lanes that reach a leaf park there until a leaf phase; a lane's own visit sequence (and
-    // so its tmax history, pruning and first-found tie rule) is unchanged — only the
-    // interleaving of lanes changes.
-    Node nd;
-    if (ni < n_nodes) nd = nodes[ni];
-    for (;;) {
-        const bool walking = ni < n_nodes;
-        const bool at_leaf = walking && nd.code >= 0;
-        const uint64_t lm = __ballot(at_leaf), wm = __ballot(walking);
-        if (wm == 0) break;
-        const bool leaf_phase = (lm == wm) || (__popcll(lm) * CPT_LEAF_BATCH >= __popcll(wm));
-        if (leaf_phase ? at_leaf : (walking && !at_leaf)) {
-            if (STATS) cnt.nodes++;
-            if (leaf_phase) {
-                if (STATS) cnt.prims++;
-                if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
-                ni = nd.miss;
-            } else {
-                ni = slab_reject<FAST>(nd, ray, tmax) ? nd.miss : ni + 1;
-            }
-            if (ni < n_nodes) nd = nodes[ni];
-        }
-    }
-#elif CPT_PREFETCH
-    // The successor of node ni is ni + 1 (box hit: its right child) or nd.miss; both loads are
-    // issued before the node's test so their latency hides under it (leaves: miss == ni + 1).
-    Node nd;
-    if (ni < n_nodes) nd = nodes[0];
-    const int last = n_nodes - 1;
-    while (ni < n_nodes) {
-        const int na = ni + 1, nb = nd.miss;
-        const Node pa = nodes[na < last ? na : last];
-        const Node pb = nodes[nb < last ? nb : last];
-        if (STATS) cnt.nodes++;
-        bool take_a;
-        if (nd.code >= 0) {
-            // leaf: IntersectionTest first (bvh.cu:175-180); its own box test is moot
-            if (STATS) cnt.prims++;
-            if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
-            take_a = false;
-        } else {
-            take_a = !slab_reject<FAST>(nd, ray, tmax);
-        }
-        ni = take_a ? na : nb;
-        nd = take_a ? pa : pb;
-    }
-#else
-    while (ni < n_nodes) {
-        const Node nd = nodes[ni];
-        if (STATS) cnt.nodes++;
-        if (nd.code >= 0) {
-            // leaf: IntersectionTest first (bvh.cu:175-180); its own box test is moot
-            if (STATS) cnt.prims++;
-            if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
-            ni = nd.miss;
-        } else {
-            ni = slab_reject<FAST>(nd, ray, tmax) ? nd.miss : ni + 1;
-        }
-    }
-#endif
-    return hit;
-}
-
-// ======================================================================================
-// BSDF sampling (material.cu:20-163).
-// ======================================================================================
-struct Shade { v3 radiance, attenuation, bounce; };
-
-// to_world (ray_tracing_math.hpp:51-63)
-__device__ __forceinline__ v3 to_world(v3 a, v3 N) {
-    v3 B, C;
-    if (__builtin_fabsf(N.x) > __builtin_fabsf(N.y)) {
-        float invLen = 1.0f / __builtin_sqrtf(N.x * N.x + N.z * N.z);
-        C = mk(N.z * invLen, 0.0f, -N.x * invLen);
-    } else {
-        float invLen = 1.0f / __builtin_sqrtf(N.y * N.y + N.z * N.z);
-        C = mk(0.f, N.z * invLen, -N.y * invLen);
-    }
-    B = cross(C, N);
-    return (a.x * B + a.y * C) + a.z * N;
-}
-
-// z = pow(x1, inv_alpha) (double pow), r = sqrtf(1 - z^2), phi = (float)(2*M_PI*x2).
-__device__ __forceinline__ v3 lobe(float x_1, float x_2, double inv_alpha) {
-    float z = (float)dm::pow((double)x_1, inv_alpha);
-    float r = __builtin_sqrtf(1.0f - z * z);
-    float phi = (float)(2 * REF_PI * (double)x_2);
-    float sp, cp;
-    dm::sincosf_(phi, &sp, &cp);
-    return mk(r * cp, r * sp, z);
-}
-
-// schlick (ray_tracing_math.hpp:65-69), pow(float,int) -> float overload in device code.
-__device__ __forceinline__ float schlick(float cosine, float ref_idx) {
-    float r0 = (1 - ref_idx) / (1 + ref_idx);
-    r0 *= r0;
-    return r0 + (1 - r0) * dm::powf_(1 - cosine, 5.0f);
-}
-
-// refract (ray_tracing_math.hpp:71-80), discriminant through double (1.0 literal).
-__device__ __forceinline__ bool refract(v3 v, v3 n, float ni_over_nt, v3& refracted) {
-    v3 uv = normalize(v);
-    float dt = dot(uv, n);
-    float discriminant = (float)(1.0 - (double)(ni_over_nt * ni_over_nt * (1 - dt * dt)));
-    if (discriminant > 0) {
-        refracted = normalize(ni_over_nt * (uv - n * dt) - n * __builtin_sqrtf(discriminant));
-        return true;
-    }
-    return false;
-}
-
-// Material::EvalAttenuationAndCreateRay (material.cu:145-163) with the Metal/Mirror swap.
-__device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow& rng, Shade& out) {
-    const v3 kd = mk(m.kd_x, m.kd_y, m.kd_z);
-    const v3 zero = mk(0.0f, 0.0f, 0.0f);
-    if (m.type == 1) {
-        // MaterialType::Metal -> MirrorHitShader (material.cu:40-64)
-        float x_1 = uniform(rng), x_2 = uniform(rng);
-        v3 local = lobe(x_1, x_2, m.inv_alpha);
-        v3 wo = to_world(local, reflect(in_dir, normal));
-        out.attenuation = dot(normal, wo) > 0.0f ? kd : zero;
-        out.bounce = wo;
-    } else if (m.type == 2) {
-        // MaterialType::Mirror -> MetalHitShader (material.cu:66-99)
-        float x_1 = uniform(rng), x_2 = uniform(rng);
-        if (uniform(rng) < m.reflectivity) {
-            v3 local = lobe(x_1, x_2, m.inv_alpha);
-            out.bounce = to_world(local, reflect(in_dir, normal));
-        } else {
-            v3 local = lobe(x_1, x_2, 1.0 / 2.0);
-            out.bounce = to_world(local, normal);
-        }
-        out.attenuation = dot(out.bounce, normal) < 0 ? zero : kd;
-    } else if (m.type == 3) {
-        // GlassHitShader (material.cu:101-143)
-        float x_1 = uniform(rng), x_2 = uniform(rng);
-        v3 local = lobe(x_1, x_2, m.inv_alpha);
-        v3 outward, refracted = mk1(0.0f);
-        float ni_over_nt, reflect_prob, cosine;
-        v3 in = normalize(in_dir);
-        if (dot(in, normal) > 0) {
-            outward = -normal;
-            ni_over_nt = m.ior;
-            cosine = dot(in, normal);
-            cosine = __builtin_sqrtf(1 - m.ior * m.ior * (1 - cosine * cosine));
-        } else {
-            outward = normal;
-            ni_over_nt = 1.f / m.ior;
-            cosine = -dot(in, normal);
-        }
-        if (refract(in, outward, ni_over_nt, refracted)) reflect_prob = schlick(cosine, m.ior);
-        else reflect_prob = 1.0f;
-        if (uniform(rng) < reflect_prob) out.bounce = to_world(local, reflect(in, normal));
-        else out.bounce = to_world(local, refracted);
-        out.attenuation = kd;
-    } else {
-        // Diffuse (and Test / unknown: default branch) -> DiffuseHitShader (material.cu:20-38)
-        float x_1 = uniform(rng), x_2 = uniform(rng);
-        v3 local = lobe(x_1, x_2, 1.0 / 2);
-        out.bounce = to_world(local, normal);
-        out.attenuation = dot(normal, out.bounce) > 0.0f ? kd : zero;
-    }
-    out.radiance = m.emit * kd;
-}
-
-// Miss (path_tracer.cu:117-122)
-__device__ __forceinline__ v3 miss_radiance(const KParams& p, v3 dir) {
-    v3 d = normalize(dir);
-    float v = (float)((double)dm::asinf_(d.z) / REF_PI + 0.5);
-    float u = (float)((double)(dm::atanf_(d.y / d.x) / 2) / REF_PI);
-    return tex2d(p, u, v);
-}
-
-// MotionalCamera::RayGen (motional_camera.cu:202-213)
-__device__ __forceinline__ Ray ray_gen(const KParams& p, int x, int y, Xorwow& rng) {
-    const CamK& c = p.cam;
-    float r1 = uniform(rng), r2 = uniform(rng), r3 = uniform(rng);
-    v3 rd = c.lens_radius * mk(r1, r2, r3);
-    v3 u = mk(c.u[0], c.u[1], c.u[2]), v = mk(c.v[0], c.v[1], c.v[2]);
-    v3 origin = mk(c.origin[0], c.origin[1], c.origin[2]);
-    v3 offset = u * rd.x + v * rd.y;
-    float dx = float(x) / float(c.width);
-    float dy = float(y) / float(c.height);
-    Ray ray;
-    ray.o = origin + offset;
-    v3 tl = mk(c.top_left[0], c.top_left[1], c.top_left[2]);
-    v3 hz = mk(c.horizontal[0], c.horizontal[1], c.horizontal[2]);
-    v3 vt = mk(c.vertical[0], c.vertical[1], c.vertical[2]);
-    ray.d = normalize((((tl + dx * hz) + dy * vt) - origin) - offset);
-    ray.tmin = 0.f;
-    ray.tmax = DEFAULT_RAY_TMAX;
-    return ray;
-}
-
-__device__ __forceinline__ uint64_t wave_sum(uint32_t v) {
-    uint64_t s = v;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-    return s;
-}
 
 // ======================================================================================
 // k_megakernel — SamplePixel (path_tracer.cu:124-175) for `spp` consecutive passes, as a

@@ -1,0 +1,297 @@
+// cpt_wavefront.hip — the SoA wavefront integrator (CPT_PATH_WAVEFRONT).
+//
+// The same SamplePixel semantics as k_megakernel (path_tracer.cu:124-175), split into
+// kernels that each do one uniform thing over a queue of live paths:
+//
+//   k_wf_raygen   pass start: RayGen for every pixel (motional_camera.cu:202-213)
+//   k_wf_extend   TraceRay for every queued ray (bvh.cu:167-205) -> hit record
+//   k_wf_shade    ClosetHit/Miss + path bookkeeping (path_tracer.cu:141-169); live paths are
+//                 re-compacted into the next queue with a wave64 ballot + mbcnt prefix and ONE
+//                 atomic per wave; finished paths add their radiance to the pixel accumulator
+//
+// Path state lives in HBM as SoA float4 arrays indexed by pixel (coalesced for the tile-
+// ordered first bounce, L2-gathered afterwards); queues hold pixel indices.  A pixel's
+// passes run in order (pass p for all pixels, then p+1), so every pixel consumes its XORWOW
+// stream exactly as in the megakernel and the results are bit-identical to it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "cpt_path.hpp"
+
+namespace cpt {
+
+// Packed per-pixel path state (all float4, 16-B aligned, SoA).
+//   ray_o  = (o.xyz, tmin)         ray_d = (d.xyz, depth as uint bits)
+//   att    = (attenuation.xyz, first-segment flag bits)
+//   rad    = (radiance.xyz, unused)
+//   hit_p  = (hit pos.xyz, code bits: material << 2 | type, or -1 = miss)
+//   hit_n  = (normal.xyz, unused)
+//   aux    = (first-hit normal sum.xyz, depth sum)          (AUX only)
+
+__device__ __forceinline__ uint32_t wave_append(bool alive, uint32_t* counter) {
+    const uint64_t m = __ballot(alive);
+    if (m == 0) return 0;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    return base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ void load_rng(const KParams& p, size_t npix, size_t pix, Xorwow& s) {
+    s.v0 = p.rng[pix];
+    s.v1 = p.rng[npix + pix];
+    s.v2 = p.rng[2 * npix + pix];
+    s.v3 = p.rng[3 * npix + pix];
+    s.v4 = p.rng[4 * npix + pix];
+    s.d = p.rng[5 * npix + pix];
+}
+
+__device__ __forceinline__ void store_rng(const KParams& p, size_t npix, size_t pix, const Xorwow& s) {
+    p.rng[pix] = s.v0;
+    p.rng[npix + pix] = s.v1;
+    p.rng[2 * npix + pix] = s.v2;
+    p.rng[3 * npix + pix] = s.v3;
+    p.rng[4 * npix + pix] = s.v4;
+    p.rng[5 * npix + pix] = s.d;
+}
+
+// Pass start.  The first queue is the tile-ordered identity (k_wf_ident), so nothing is
+// appended here.  max_depth == 0: the pass is RayGen's draws and a zero radiance.
+template <bool AUX>
+__global__ void __launch_bounds__(256) k_wf_raygen(const KParams p, WfState w) {
+    const size_t npix = (size_t)p.n_rows * p.width;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t pix = (size_t)blockIdx.x * blockDim.x + threadIdx.x; pix < npix; pix += stride) {
+        const int x = (int)(pix % p.width), ri = (int)(pix / p.width);
+        Xorwow s;
+        load_rng(p, npix, pix, s);
+        const Ray ray = ray_gen(p, x, p.rows[ri], s);
+        store_rng(p, npix, pix, s);
+        if (p.max_depth == 0) {
+            float4 a = p.accum[pix];
+            p.accum[pix] = make_float4(a.x + 0.f, a.y + 0.f, a.z + 0.f, a.w + 1.0f);
+            if (AUX) {
+                p.normal[3 * pix] = 0.f;
+                p.normal[3 * pix + 1] = 0.f;
+                p.normal[3 * pix + 2] = 0.f;
+                p.depth[pix] = 0.f;
+            }
+            continue;
+        }
+        w.ray_o[pix] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.tmin);
+        w.ray_d[pix] = make_float4(ray.d.x, ray.d.y, ray.d.z, __uint_as_float(0u));
+        w.att[pix] = make_float4(1.f, 1.f, 1.f, __uint_as_float(1u));
+        w.rad[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (AUX) w.aux[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+template <bool STATS>
+__global__ void __launch_bounds__(256) k_wf_extend(const KParams p, WfState w, const int32_t* __restrict__ qin,
+                                                  const uint32_t* __restrict__ nin) {
+    const uint32_t n = *nin;
+    Counters cnt{0, 0, 0, 0, 0};
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int pix = qin[i];
+        const float4 o = w.ray_o[pix], d = w.ray_d[pix];
+        Ray ray;
+        ray.o = mk(o.x, o.y, o.z);
+        ray.d = mk(d.x, d.y, d.z);
+        ray.tmin = o.w;
+        ray.tmax = DEFAULT_RAY_TMAX;
+        const RayK rk = make_rayk(ray);
+        const bool finite = !(ray.o.x != ray.o.x || ray.o.y != ray.o.y || ray.o.z != ray.o.z || ray.d.x != ray.d.x ||
+                              ray.d.y != ray.d.y || ray.d.z != ray.d.z);
+        Hit h;
+        int code = -1;
+        if (STATS) cnt.segments++;
+        bool hit;
+        if (__builtin_expect(finite, 1)) hit = trace<STATS, true>(p.nodes, p.n_nodes, rk, h, code, cnt);
+        else hit = trace<STATS, false>(p.nodes, p.n_nodes, rk, h, code, cnt);
+        w.hit_p[pix] = make_float4(h.pos.x, h.pos.y, h.pos.z, __int_as_float(hit ? code : -1));
+        if (hit) w.hit_n[pix] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.f);
+    }
+    if (STATS) {
+        const uint64_t a = wave_sum(cnt.segments), b = wave_sum(cnt.nodes), c = wave_sum(cnt.prims);
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd((unsigned long long*)&p.stats[0], (unsigned long long)a);
+            atomicAdd((unsigned long long*)&p.stats[1], (unsigned long long)b);
+            atomicAdd((unsigned long long*)&p.stats[2], (unsigned long long)c);
+        }
+    }
+}
+
+template <bool STATS, bool AUX>
+__global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, const int32_t* __restrict__ qin,
+                                                 const uint32_t* __restrict__ nin, int32_t* __restrict__ qout,
+                                                 uint32_t* __restrict__ nout) {
+    const uint32_t n = *nin;
+    const size_t npix = (size_t)p.n_rows * p.width;
+    const uint32_t max_depth = (uint32_t)p.max_depth;
+    uint32_t hits = 0, misses = 0;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    // all lanes run the same trip count so the wave-level append sees the whole wave
+    const uint32_t trips = (n + stride - 1) / stride;
+    for (uint32_t t = 0, i = blockIdx.x * blockDim.x + threadIdx.x; t < trips; ++t, i += stride) {
+        bool alive = false;
+        int pix = 0;
+        if (i < n) {
+            pix = qin[i];
+            Xorwow s;
+            load_rng(p, npix, pix, s);
+            const float4 o4 = w.ray_o[pix], d4 = w.ray_d[pix], a4 = w.att[pix], r4 = w.rad[pix];
+            const float4 hp = w.hit_p[pix];
+            v3 dir = mk(d4.x, d4.y, d4.z);
+            v3 att = mk(a4.x, a4.y, a4.z), rad = mk(r4.x, r4.y, r4.z);
+            uint32_t depth = __float_as_uint(d4.w);
+            const bool first = __float_as_uint(a4.w) != 0u;
+            const int code = __float_as_int(hp.w);
+            Shade sh;
+            v3 attr_normal;
+            v3 org = mk(o4.x, o4.y, o4.z);
+            if (code >= 0) {
+                hits++;
+                const float4 hn = w.hit_n[pix];
+                const v3 normal = mk(hn.x, hn.y, hn.z);
+                const Mat m = p.mats[code >> 2];
+                eval_material(m, normal, dir, s, sh);
+                attr_normal = normal;
+                org = mk(hp.x, hp.y, hp.z);              // payload.hit_pos = position
+            } else {
+                misses++;
+                sh.radiance = miss_radiance(p, dir);
+                sh.attenuation = mk1(0.f);
+                sh.bounce = dir;
+                attr_normal = -dir;
+                depth = MAX_RECURSION_DEPTH_SET;          // termination sentinel (path_tracer.cu:121)
+            }
+            rad = rad + att * sh.radiance;
+            att = att * sh.attenuation;
+            float4 aux4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (AUX) {
+                aux4 = w.aux[pix];
+                if (first) {
+                    const v3 nn = mk(aux4.x, aux4.y, aux4.z) + attr_normal;
+                    aux4 = make_float4(nn.x, nn.y, nn.z, aux4.w + DEFAULT_RAY_TMAX);
+                }
+            }
+            dir = normalize(sh.bounce);
+            depth++;
+            if (!(depth < max_depth)) {
+                // path done: the pass's radiance joins the pixel's sum (passes in order)
+                const float4 a = p.accum[pix];
+                p.accum[pix] = make_float4(a.x + rad.x, a.y + rad.y, a.z + rad.z, a.w + 1.0f);
+                if (AUX) {
+                    p.normal[3 * (size_t)pix] = aux4.x;
+                    p.normal[3 * (size_t)pix + 1] = aux4.y;
+                    p.normal[3 * (size_t)pix + 2] = aux4.z;
+                    p.depth[pix] = aux4.w;
+                }
+            } else {
+                alive = true;
+                w.ray_o[pix] = make_float4(org.x, org.y, org.z, BOUNCE_RAY_TMIN);
+                w.ray_d[pix] = make_float4(dir.x, dir.y, dir.z, __uint_as_float(depth));
+                w.att[pix] = make_float4(att.x, att.y, att.z, __uint_as_float(0u));
+                w.rad[pix] = make_float4(rad.x, rad.y, rad.z, 0.f);
+                if (AUX) w.aux[pix] = aux4;
+            }
+            store_rng(p, npix, pix, s);
+        }
+        const uint32_t slot = wave_append(alive, nout);
+        if (alive) qout[slot] = pix;
+    }
+    if (STATS) {
+        const uint64_t a = wave_sum(hits), b = wave_sum(misses);
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd((unsigned long long*)&p.stats[3], (unsigned long long)a);
+            atomicAdd((unsigned long long*)&p.stats[4], (unsigned long long)b);
+        }
+    }
+}
+
+// Tile-ordered identity queue: entry k = the k-th pixel when the frame is walked in 8x8
+// tiles, so each wave's first-bounce rays are coherent.
+__global__ void k_wf_ident(int width, int n_rows, int32_t* q, uint32_t* count) {
+    const int tiles_x = (width + 7) / 8;
+    const uint32_t n_work = (uint32_t)tiles_x * ((n_rows + 7) / 8) * 64u;
+    for (uint32_t id = blockIdx.x * blockDim.x + threadIdx.x; id < n_work; id += gridDim.x * blockDim.x) {
+        const uint32_t tile = id >> 6, k = id & 63;
+        const int x = (int)(tile % tiles_x) * 8 + (int)(k & 7);
+        const int ri = (int)(tile / tiles_x) * 8 + (int)(k >> 3);
+        if (x < width && ri < n_rows) {
+            // rank of this pixel among valid pixels in tile order = its slot
+            const uint32_t slot = atomicAdd(count, 1u);
+            q[slot] = ri * width + x;
+        }
+    }
+}
+
+// ======================================================================================
+// Host driver: spp passes x (raygen, max_depth x (extend, shade)).
+// ======================================================================================
+static int persistent_grid(const void* fn, int block, size_t items) {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (cus <= 0) cus = 256;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    const long long want = (long long)((items + block - 1) / block);
+    return (int)std::max<long long>(1, std::min<long long>(want, (long long)per_cu * cus));
+}
+
+hipError_t wavefront_build_ident(const KParams& p, WfState& w, hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(w.counts + 3, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const size_t npix = (size_t)p.n_rows * p.width;
+    hipLaunchKernelGGL(k_wf_ident, dim3((unsigned)std::min<size_t>(4096, (npix + 255) / 256 + 1)), dim3(256), 0, stream,
+                       p.width, p.n_rows, w.ident, w.counts + 3);
+    return hipGetLastError();
+}
+
+template <bool S, bool A>
+static hipError_t wf_render_t(const KParams& p, WfState& w, hipStream_t stream, int* launches) {
+    const size_t npix = (size_t)p.n_rows * p.width;
+    const int gr = persistent_grid((const void*)k_wf_raygen<A>, 256, npix);
+    const int ge = persistent_grid((const void*)k_wf_extend<S>, 256, npix);
+    const int gs = persistent_grid((const void*)k_wf_shade<S, A>, 256, npix);
+    hipError_t e = hipSuccess;
+    int n = 0;
+    for (int pass = 0; pass < p.spp && e == hipSuccess; ++pass) {
+        hipLaunchKernelGGL(k_wf_raygen<A>, dim3(gr), dim3(256), 0, stream, p, w);
+        ++n;
+        const int32_t* cur = w.ident;
+        const uint32_t* cur_n = w.counts + 3;
+        for (int b = 0; b < p.max_depth; ++b) {
+            int32_t* nxt = w.queue[b & 1];
+            uint32_t* nxt_n = w.counts + (b & 1);
+            e = hipMemsetAsync(nxt_n, 0, sizeof(uint32_t), stream);
+            if (e != hipSuccess) break;
+            hipLaunchKernelGGL(k_wf_extend<S>, dim3(ge), dim3(256), 0, stream, p, w, cur, cur_n);
+            hipLaunchKernelGGL((k_wf_shade<S, A>), dim3(gs), dim3(256), 0, stream, p, w, cur, cur_n, nxt, nxt_n);
+            n += 2;
+            cur = nxt;
+            cur_n = nxt_n;
+        }
+        if (e == hipSuccess) e = hipGetLastError();
+    }
+    if (launches) *launches = n;
+    return e;
+}
+
+hipError_t launch_wavefront(const KParams& p, WfState& w, bool stats, bool aux, hipStream_t stream, int* launches) {
+    if (p.width <= 0 || p.n_rows <= 0) return hipSuccess;
+    if (stats && aux) return wf_render_t<true, true>(p, w, stream, launches);
+    if (stats) return wf_render_t<true, false>(p, w, stream, launches);
+    if (aux) return wf_render_t<false, true>(p, w, stream, launches);
+    return wf_render_t<false, false>(p, w, stream, launches);
+}
+
+}  // namespace cpt

@@ -9,7 +9,10 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import (CPT_RENDER_ACCUMULATE, CPT_RENDER_AUX, CPT_RENDER_STATS, CPT_RENDER_SYNC, CptError, check)
+from ._lib import (CPT_PATH_WAVEFRONT, CPT_RENDER_ACCUMULATE, CPT_RENDER_AUX, CPT_RENDER_STATS, CPT_RENDER_SYNC,
+                   CptError, check)
+
+PATHS = ("megakernel", "wavefront")
 from .types import CAMERA_DTYPE, OBJECT_DTYPE
 
 
@@ -108,9 +111,14 @@ class Renderer:
         self._check(self._L.cpt_init_rng(self._ctx, ctypes.c_uint64(seed)))
 
     # -- render ----------------------------------------------------------------------
-    def render(self, cam, spp, max_depth, accumulate=False, aux=False, stats=False, sync=False, flags=0):
+    def render(self, cam, spp, max_depth, accumulate=False, aux=False, stats=False, sync=False, flags=0,
+               path="megakernel"):
+        """path: "megakernel" (per-lane regeneration, state in VGPRs) or "wavefront" (SoA state in
+        HBM, extend/shade kernels with ballot compaction).  Both give identical results."""
+        if path not in PATHS:
+            raise ValueError(f"path must be one of {PATHS}")
         c = np.ascontiguousarray(np.array(cam, dtype=CAMERA_DTYPE))
-        f = flags
+        f = flags | (CPT_PATH_WAVEFRONT if path == "wavefront" else 0)
         f |= CPT_RENDER_ACCUMULATE if accumulate else 0
         f |= CPT_RENDER_AUX if aux else 0
         f |= CPT_RENDER_STATS if stats else 0

@@ -76,7 +76,8 @@ def test_rng_init_bitexact(gpu, oracle_mod, w, rows):
 
 
 # ------------------------------------------------------------------------- integrator
-def _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, rows=None, seed=1234, aux=False, env=True):
+def _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, rows=None, seed=1234, aux=False, env=True,
+              path="megakernel"):
     rows = np.arange(H, dtype=np.int32) if rows is None else np.asarray(rows, np.int32)
     cam = camera_get_copy(scenes.camera_for(W, H))
     gpu.set_scene(objs)
@@ -84,7 +85,7 @@ def _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, rows=None, seed=1234
     gpu.set_frame(W, H, rows)
     gpu.init_rng(seed)
     gpu.reset_stats()
-    gpu.render(cam, spp, depth, aux=aux, stats=True, sync=True)
+    gpu.render(cam, spp, depth, aux=aux, stats=True, sync=True, path=path)
     g_acc, g_rng, g_st = gpu.read_accum(), gpu.read_rng(), gpu.stats()
     g_aux = gpu.read_aux() if aux else None
     rng = oracle_mod.init_rng(seed, W, rows, threads=8)
@@ -103,49 +104,58 @@ CASES = [
 ]
 
 
+PATHS = ["megakernel", "wavefront"]
+
+
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name,W,H,spp,depth", CASES)
-def test_render_bitexact(gpu, oracle_mod, sky, name, W, H, spp, depth):
+def test_render_bitexact(gpu, oracle_mod, sky, name, W, H, spp, depth, path):
     objs = scenes.SCENES[name]()
-    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth)
+    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, path=path)
     np.testing.assert_array_equal(gr, orng)
     assert gs == os_
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
     assert np.isfinite(ga).all() and (ga[:, 3] == spp).all()
 
 
-def test_render_aux_bitexact(gpu, oracle_mod, sky):
+@pytest.mark.parametrize("path", PATHS)
+def test_render_aux_bitexact(gpu, oracle_mod, sky, path):
     objs = scenes.scene_s4()
-    (ga, gr, gs, (gn, gd)), (oa, orng, os_, (on, od)) = _run_both(gpu, oracle_mod, sky, objs, 48, 32, 2, 8, aux=True)
+    (ga, gr, gs, (gn, gd)), (oa, orng, os_, (on, od)) = _run_both(gpu, oracle_mod, sky, objs, 48, 32, 2, 8, aux=True,
+                                                                  path=path)
     np.testing.assert_array_equal(gn.view(np.uint32), on.view(np.uint32))
     np.testing.assert_array_equal(gd, od)
     assert (gd == np.float32(1e30)).all()   # depth quirk (a18): TraceRay gets the ray by value
 
 
-def test_row_subset_and_order(gpu, oracle_mod, sky):
+@pytest.mark.parametrize("path", PATHS)
+def test_row_subset_and_order(gpu, oracle_mod, sky, path):
     """Any row list (tiles, interleaved blocks, unsorted, repeated) gives per-row results
     identical to the monolithic render: a pixel's stream depends only on (seed, x, y)."""
     objs = scenes.scene_s1000()
     W, H = 48, 40
-    (ga, gr, _, _), _ = _run_both(gpu, oracle_mod, sky, objs, W, H, 2, 8)
+    (ga, gr, _, _), _ = _run_both(gpu, oracle_mod, sky, objs, W, H, 2, 8, path=path)
     rows = [39, 0, 17, 17, 5]
-    (sa, sr, _, _), (oa, orng, _, _) = _run_both(gpu, oracle_mod, sky, objs, W, H, 2, 8, rows=rows)
+    (sa, sr, _, _), (oa, orng, _, _) = _run_both(gpu, oracle_mod, sky, objs, W, H, 2, 8, rows=rows, path=path)
     np.testing.assert_array_equal(sa, oa)
     full = ga.reshape(H, W, 4)
     np.testing.assert_array_equal(sa.reshape(len(rows), W, 4), full[rows])
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("depth", [0, 1])
-def test_tiny_depths(gpu, oracle_mod, sky, depth):
+def test_tiny_depths(gpu, oracle_mod, sky, depth, path):
     objs = scenes.scene_s4()
-    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, objs, 32, 16, 3, depth)
+    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, objs, 32, 16, 3, depth, path=path)
     np.testing.assert_array_equal(gr, orng)
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
     assert gs == os_
 
 
-def test_empty_scene_and_no_env(gpu, oracle_mod, sky):
+@pytest.mark.parametrize("path", PATHS)
+def test_empty_scene_and_no_env(gpu, oracle_mod, sky, path):
     empty = np.zeros(0, dtype=types.OBJECT_DTYPE)
-    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, empty, 32, 16, 2, 8)
+    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, empty, 32, 16, 2, 8, path=path)
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
     np.testing.assert_array_equal(gr, orng)
     assert gs["hits"] == 0 and gs == os_
@@ -162,7 +172,8 @@ def test_single_object_and_cylinders(gpu, oracle_mod, sky):
         assert gs == os_
 
 
-def test_accumulate_and_spp0(gpu, oracle_mod, sky):
+@pytest.mark.parametrize("path", PATHS)
+def test_accumulate_and_spp0(gpu, oracle_mod, sky, path):
     objs = scenes.scene_s3()
     W, H = 32, 32
     cam = camera_get_copy(scenes.camera_for(W, H))
@@ -170,10 +181,10 @@ def test_accumulate_and_spp0(gpu, oracle_mod, sky):
     gpu.set_env(sky)
     gpu.set_frame(W, H)
     gpu.init_rng(99)
-    gpu.render(cam, 0, 4, sync=True)
+    gpu.render(cam, 0, 4, sync=True, path=path)
     assert (gpu.read_accum() == 0).all()
-    gpu.render(cam, 2, 4, sync=True)
-    gpu.render(cam, 3, 4, accumulate=True, sync=True)
+    gpu.render(cam, 2, 4, sync=True, path=path)
+    gpu.render(cam, 3, 4, accumulate=True, sync=True, path=path)
     a = gpu.read_accum()
     rng = oracle_mod.init_rng(99, W, np.arange(H, dtype=np.int32))
     acc, _, _, _ = oracle_mod.render(objs, cam, sky, np.arange(H, dtype=np.int32), 2, 4, rng)
