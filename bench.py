@@ -194,11 +194,15 @@ def main():
         share = npix_local / float(W * H)
         bytes_launch = byte_model(st, paths_total) * share
         achieved = bytes_launch / (avg_kernel_ms / 1e3) / 1e9
+        # HBM traffic per launch from rocprofv3 PMC passes of this same workload (committed under
+        # profiles/, made by tools/profile.sh + tools/pmc_traffic.py); null when none matches.
         traffic = None
-        if args.traffic_json and os.path.exists(args.traffic_json):
-            with open(args.traffic_json) as f:
+        tpath = args.traffic_json or os.path.join(REPO, "profiles", f"traffic_{args.config}_{args.path}.json")
+        if os.path.exists(tpath):
+            with open(tpath) as f:
                 tj = json.load(f)
-            if tj.get("config") == args.config and tj.get("n_rows") == int(rows.size):
+            if (tj.get("config") == args.config and tj.get("n_rows") == int(rows.size) and tj.get("spp") == spp
+                    and tj.get("path") == args.path):
                 traffic = tj.get("hbm_bytes_per_launch")
         out = {
             "metric": METRIC,
