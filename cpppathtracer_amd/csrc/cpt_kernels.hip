@@ -31,21 +31,6 @@ namespace cpt {
 // wave starts coherent.  LDS variant: the BVH (32 B nodes, leaves inline) is staged in LDS
 // once per resident block.
 // ======================================================================================
-#ifndef CPT_STAMPS
-#define CPT_STAMPS 0   // diagnostic build: per-phase s_memtime sums into stats[5..7] (never timed)
-#endif
-__device__ __forceinline__ unsigned long long stamp() {
-#if CPT_STAMPS
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-#else
-    return 0;
-#endif
-}
-
 struct Lane {
     int x, y;
     size_t pix;
@@ -77,7 +62,7 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
     const size_t npix = (size_t)p.n_rows * p.width;
     const uint32_t n_work = (uint32_t)(((p.width + 7) >> 3) * ((p.n_rows + 7) >> 3)) * 64u;
     const uint32_t max_depth = (uint32_t)p.max_depth;
-    Counters cnt{0, 0, 0, 0, 0};
+    Counters cnt{};
 
     Lane L;
     bool busy = false;
@@ -201,7 +186,7 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
                 }
             }
         }
-        if (CPT_STAMPS) {
+        if (CPT_STAMPS == 1) {
             const unsigned long long t3 = stamp();
             st_refill += t1 - t0;
             st_trace += t2 - t1;
@@ -225,6 +210,11 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             busy = false;
         }
     }
+#if CPT_STAMPS == 2
+    st_refill = cnt.st_leaf;
+    st_trace = cnt.st_slab;
+    st_shade = cnt.st_iter;
+#endif
     if (CPT_STAMPS && lane == 0) {
         atomicAdd(&p.stats[5], st_refill);
         atomicAdd(&p.stats[6], st_trace);

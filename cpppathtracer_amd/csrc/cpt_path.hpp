@@ -86,135 +86,129 @@ __device__ __forceinline__ RayK make_rayk(const Ray& r) {
 // ======================================================================================
 struct Hit { v3 normal, pos; };
 
-__device__ __forceinline__ bool sphere_test(const Node& s, const RayK& ray, float& tmax, Hit& h) {
+// Deferred hit attributes: a leaf test only decides whether the primitive replaces the
+// current closest hit (and shrinks tmax); the hit position and normal of the WINNER are
+// computed once after the walk from (t, node, kind), with the reference's own formulas.
+// The position is ray.origin + temp * ray.dir in every intersector (object.cu:21,29,44,...),
+// and the normal depends only on which case accepted:
+enum : int {
+    HK_SPHERE_ROOT1 = 0,   // (p - c) / radius           (object.cu:23-24, signed radius)
+    HK_SPHERE_ROOT2 = 1,   // normalize(p - c)            (object.cu:30)
+    HK_CYL_SIDE = 2,       // normalize(p.x-cx, 0, p.z-cz) (object.cu:97-99,105-107)
+    HK_FACING_Y = 3        // normalize(0, -d.y, 0): caps and platform (object.cu:43,62,75)
+};
+
+// Sphere (object.cu:10-35)
+__device__ __forceinline__ bool sphere_test(const Node& s, const RayK& ray, float& tmax, int& kind) {
     const v3 c = mk(s.a0, s.a1, s.a2);
     const float radius = s.b0;
-    v3 A_C = ray.o - c;
-    float b = dot(A_C, ray.d);
-    float cc = dot(A_C, A_C) - radius * radius;
-    float a = dot(ray.d, ray.d);
-    float disc = b * b - a * cc;
-    if (disc > 0) {
-        float sq = __builtin_sqrtf(disc);
-        float temp = qdiv(-b - sq, a, ray.ya);
-        if (temp < tmax && temp > ray.tmin) {
-            tmax = temp;
-            h.pos = ray.o + temp * ray.d;
-            h.normal = (h.pos - c) / radius;        // first root: divided by the signed radius
-            return true;
-        }
-        temp = qdiv(-b + sq, a, ray.ya);
-        if (temp < tmax && temp > ray.tmin) {
-            tmax = temp;
-            h.pos = ray.o + temp * ray.d;
-            h.normal = normalize(h.pos - c);
-            return true;
-        }
+    const v3 A_C = ray.o - c;
+    const float b = dot(A_C, ray.d);
+    const float cc = dot(A_C, A_C) - radius * radius;
+    const float a = dot(ray.d, ray.d);
+    const float disc = b * b - a * cc;
+    if (!(disc > 0)) return false;
+    const float sq = __builtin_sqrtf(disc);
+    float temp = qdiv(-b - sq, a, ray.ya);
+    if (temp < tmax && temp > ray.tmin) {
+        tmax = temp;
+        kind = HK_SPHERE_ROOT1;
+        return true;
+    }
+    temp = qdiv(-b + sq, a, ray.ya);
+    if (temp < tmax && temp > ray.tmin) {
+        tmax = temp;
+        kind = HK_SPHERE_ROOT2;
+        return true;
     }
     return false;
 }
 
-__device__ __forceinline__ bool platform_test(const Node& pl, const RayK& ray, float& tmax, Hit& h) {
+// Platform: the plane y = y_pos, only when the ray approaches it (object.cu:37-48)
+__device__ __forceinline__ bool platform_test(const Node& pl, const RayK& ray, float& tmax, int& kind) {
     const float y_pos = pl.b1;
     if ((ray.o.y < y_pos && ray.d.y > 0.f) || (ray.o.y > y_pos && ray.d.y < 0.f)) {
-        float temp = qdiv(y_pos - ray.o.y, ray.d.y, ray.yy);
+        const float temp = qdiv(y_pos - ray.o.y, ray.d.y, ray.yy);
         if (temp < tmax && temp > ray.tmin) {
             tmax = temp;
-            h.pos = ray.o + temp * ray.d;
-            h.normal = normalize(mk(0, -ray.d.y, 0));  // faces the ray
+            kind = HK_FACING_Y;
             return true;
         }
     }
     return false;
 }
 
-__device__ __forceinline__ bool cap_test(float cx, float cz, float radius, const RayK& ray, float& tmax, Hit& h,
+// One cylinder cap disk (object.cu:52-77)
+__device__ __forceinline__ bool cap_test(float cx, float cz, float radius, const RayK& ray, float& tmax, int& kind,
                                          float ypos) {
     if ((ray.o.y < ypos && ray.d.y > 0.f) || (ray.o.y > ypos && ray.d.y < 0.f)) {
-        float temp = qdiv(ypos - ray.o.y, ray.d.y, ray.yy);
-        v3 hp = ray.o + temp * ray.d;
-        if (temp < tmax && temp > ray.tmin &&
-            __builtin_sqrtf((hp.x - cx) * (hp.x - cx) + (hp.z - cz) * (hp.z - cz)) < radius) {
-            tmax = temp;
-            h.pos = hp;
-            h.normal = normalize(mk(0, -ray.d.y, 0));
-            return true;
+        const float temp = qdiv(ypos - ray.o.y, ray.d.y, ray.yy);
+        if (temp < tmax && temp > ray.tmin) {
+            const float hx = ray.o.x + temp * ray.d.x, hz = ray.o.z + temp * ray.d.z;
+            if (__builtin_sqrtf((hx - cx) * (hx - cx) + (hz - cz) * (hz - cz)) < radius) {
+                tmax = temp;
+                kind = HK_FACING_Y;
+                return true;
+            }
         }
     }
     return false;
 }
 
-__device__ inline bool cylinder_test(const Node& cy, const RayK& ray, float& tmax, Hit& h) {
+// Cylinder: caps, then the side quadratic with the y-range check (object.cu:50-112).  The
+// second root can never replace an accepted first root (temp2 >= temp1 under monotone
+// rounding), so the side returns after the first accepted root.
+__device__ __forceinline__ bool cylinder_test(const Node& cy, const RayK& ray, float& tmax, int& kind) {
     const float ccx = cy.a0, ccy = cy.a1, ccz = cy.a2, r = cy.b0, height = cy.b2;
     bool ret = false;
-    float upper = ccy + height / 2;
-    if (cap_test(ccx, ccz, r, ray, tmax, h, upper)) ret = true;
-    float lower = ccy - height / 2;
-    if (cap_test(ccx, ccz, r, ray, tmax, h, lower)) ret = true;
-    float dx = ray.d.x, dz = ray.d.z;
-    float cx = ray.o.x - ccx;
-    float cz = ray.o.z - ccz;
-    float a = dx * dx + dz * dz;
-    float b = cx * dx + cz * dz;
-    float c = cx * cx + cz * cz - r * r;
-    float disc = b * b - a * c;
+    const float upper = ccy + height / 2;
+    if (cap_test(ccx, ccz, r, ray, tmax, kind, upper)) ret = true;
+    const float lower = ccy - height / 2;
+    if (cap_test(ccx, ccz, r, ray, tmax, kind, lower)) ret = true;
+    const float dx = ray.d.x, dz = ray.d.z;
+    const float cx = ray.o.x - ccx, cz = ray.o.z - ccz;
+    const float a = dx * dx + dz * dz;
+    const float b = cx * dx + cz * dz;
+    const float c = cx * cx + cz * cz - r * r;
+    const float disc = b * b - a * c;
     if (disc > 0.f) {
-        float sq = __builtin_sqrtf(disc);
+        const float sq = __builtin_sqrtf(disc);
         float temp = qdiv(-b - sq, a, ray.yc);
-        v3 hp = ray.o + temp * ray.d;
-        if (temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper) {
+        float hy = ray.o.y + temp * ray.d.y;
+        if (temp < tmax && temp > ray.tmin && hy > lower && hy < upper) {
             tmax = temp;
-            h.pos = hp;
-            h.normal = normalize(mk(hp.x - ccx, 0.f, hp.z - ccz));
-            ret = true;
+            kind = HK_CYL_SIDE;
+            return true;
         }
         temp = qdiv(-b + sq, a, ray.yc);
-        hp = ray.o + temp * ray.d;
-        if (temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper) {
+        hy = ray.o.y + temp * ray.d.y;
+        if (temp < tmax && temp > ray.tmin && hy > lower && hy < upper) {
             tmax = temp;
-            h.pos = hp;
-            h.normal = normalize(mk(hp.x - ccx, 0.f, hp.z - ccz));
-            ret = true;
+            kind = HK_CYL_SIDE;
+            return true;
         }
     }
     return ret;
 }
 
-// Sphere (object.cu:10-35) and cylinder side (object.cu:81-111) share one quadratic: the
-// cylinder's 2-D terms are the sphere's 3-D ones with the y terms replaced by +0, which
-// leaves every rounding unchanged ((u + 0) + w == u + w for the squares and products here,
-// up to the sign of a zero b that cannot change the roots).  The cylinder's second root can
-// never replace an accepted first root (temp2 >= temp1 under monotone rounding), so both
-// shapes return after the first accepted root as the sphere does.
-__device__ __forceinline__ bool quad_test(const Node& nd, const RayK& ray, float& tmax, Hit& h, bool cyl,
-                                          float lower, float upper) {
-    const float cx = nd.a0, cy = nd.a1, cz = nd.a2, r = nd.b0;
-    const float ax = ray.o.x - cx, ay = ray.o.y - cy, az = ray.o.z - cz;
-    const float ay_dy = cyl ? 0.f : ay * ray.d.y;
-    const float ay_ay = cyl ? 0.f : ay * ay;
-    const float dy_dy = cyl ? 0.f : ray.d.y * ray.d.y;
-    const float a = (ray.d.x * ray.d.x + dy_dy) + ray.d.z * ray.d.z;
-    const float b = (ax * ray.d.x + ay_dy) + az * ray.d.z;
-    const float c = ((ax * ax + ay_ay) + az * az) - r * r;
-    const float disc = b * b - a * c;
-    if (!(disc > 0.f)) return false;
-    const double y = cyl ? ray.yc : ray.ya;
-    const float sq = __builtin_sqrtf(disc);
-    float temp = qdiv(-b - sq, a, y);
-    v3 hp = ray.o + temp * ray.d;
-    bool first = true;
-    if (!(temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper)) {
-        temp = qdiv(-b + sq, a, y);
-        hp = ray.o + temp * ray.d;
-        if (!(temp < tmax && temp > ray.tmin && hp.y > lower && hp.y < upper)) return false;
-        first = false;
-    }
-    tmax = temp;
-    h.pos = hp;
-    const v3 v = mk(hp.x - cx, cyl ? 0.f : hp.y - cy, hp.z - cz);
-    // sphere first root: (p - c) / r with the signed radius; every other case normalizes
-    h.normal = (first && !cyl) ? v / r : normalize(v);
-    return true;
+__device__ __forceinline__ bool leaf_test(const Node& nd, const RayK& ray, float& tmax, int& kind) {
+    const int type = nd.code & 3;
+    if (type == 0) return sphere_test(nd, ray, tmax, kind);
+    if (type == 2) return cylinder_test(nd, ray, tmax, kind);
+    if (type == 1) return platform_test(nd, ray, tmax, kind);
+    return false;                        // unknown PrimitiveType: IntersectionTest -> false
+}
+
+// Attributes of the winning primitive (see HK_*).
+__device__ __forceinline__ Hit hit_attributes(const Node& nd, const RayK& ray, float t, int kind) {
+    Hit h;
+    h.pos = ray.o + t * ray.d;
+    const v3 c = mk(nd.a0, nd.a1, nd.a2);
+    if (kind == HK_SPHERE_ROOT1) h.normal = (h.pos - c) / nd.b0;
+    else if (kind == HK_SPHERE_ROOT2) h.normal = normalize(h.pos - c);
+    else if (kind == HK_CYL_SIDE) h.normal = normalize(mk(h.pos.x - c.x, 0.f, h.pos.z - c.z));
+    else h.normal = normalize(mk(0, -ray.d.y, 0));
+    return h;
 }
 
 // ======================================================================================
@@ -223,18 +217,33 @@ __device__ __forceinline__ bool quad_test(const Node& nd, const RayK& ray, float
 // n, then n+1 on a box hit or node.miss on a box miss / after a leaf, reproduces the
 // reference's visit sequence, leaf-before-box order and pruning against the shrinking tmax
 // one for one — no stack, no scratch memory.
-//
-// CPT_WHILEWHILE=1 selects a while-while loop (internal nodes until every lane of the wave
-// sits on a leaf, then the leaf tests together); per-lane visit order is the same either way.
 // ======================================================================================
-#ifndef CPT_WHILEWHILE
-#define CPT_WHILEWHILE 0
-#endif
 #ifndef CPT_WAVES_PER_SIMD
 #define CPT_WAVES_PER_SIMD 3   // occupancy target of k_megakernel (VGPR budget 168)
 #endif
 
-struct Counters { uint32_t segments, nodes, prims, hits, misses; };
+#ifndef CPT_STAMPS
+#define CPT_STAMPS 0   // diagnostic builds (never timed): 1 = per-phase s_memtime sums of the
+                       // megakernel (refill / trace / shade), 2 = inside the BVH walk (leaf / slab / rest)
+#endif
+__device__ __forceinline__ unsigned long long stamp() {
+#if CPT_STAMPS
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+#else
+    return 0;
+#endif
+}
+
+struct Counters {
+    uint32_t segments, nodes, prims, hits, misses;
+#if CPT_STAMPS == 2
+    unsigned long long st_leaf, st_slab, st_iter;
+#endif
+};
 
 // Slab test of one internal node (bvh.cu:181-200).  The six plane distances use the exact
 // quotient; if any of them is zero/subnormal the node is redone with the IEEE divide.
@@ -292,124 +301,90 @@ __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, flo
     return lo > hi || lo > tmax || hi < ray.tmin;
 }
 
-#ifndef CPT_UNIFIED_QUAD
-#define CPT_UNIFIED_QUAD 1
-#endif
-__device__ __forceinline__ bool leaf_test(const Node& nd, const RayK& ray, float& tmax, Hit& h) {
-    const int type = nd.code & 3;
-#if CPT_UNIFIED_QUAD
-    bool r = false;
-    float lower = -__builtin_inff(), upper = __builtin_inff();
-    if (type == 2) {
-        // Cylinder caps first (object.cu:52-77), then the side.
-        upper = nd.a1 + nd.b2 / 2;
-        if (cap_test(nd.a0, nd.a2, nd.b0, ray, tmax, h, upper)) r = true;
-        lower = nd.a1 - nd.b2 / 2;
-        if (cap_test(nd.a0, nd.a2, nd.b0, ray, tmax, h, lower)) r = true;
-    }
-    if (type == 0 || type == 2) {
-        if (quad_test(nd, ray, tmax, h, type == 2, lower, upper)) r = true;
-    } else if (type == 1) {
-        r = platform_test(nd, ray, tmax, h);
-    }
-    return r;
-#else
-    if (type == 0) return sphere_test(nd, ray, tmax, h);
-    if (type == 2) return cylinder_test(nd, ray, tmax, h);
-    if (type == 1) return platform_test(nd, ray, tmax, h);
-    return false;
-#endif
-}
-
 #ifndef CPT_LEAF_BATCH
-#define CPT_LEAF_BATCH 0   // K > 0: run the leaf phase when >= 1/K of the walking lanes wait on a leaf
-#endif
-#ifndef CPT_PREFETCH
-#define CPT_PREFETCH 1     // load both possible successors of a node while it is being tested
+#define CPT_LEAF_BATCH 0   // K > 0: leaf tests run in wave-uniform leaf phases (see trace)
 #endif
 
 template <bool STATS, bool FAST>
 __device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_nodes, const RayK& ray, Hit& h,
                                       int& code_out, Counters& cnt) {
     float tmax = DEFAULT_RAY_TMAX;
-    bool hit = false;
+    int best = -1, kind = 0;
     int ni = 0;
-#if CPT_WHILEWHILE
-    while (ni < n_nodes) {
-        Node nd = nodes[ni];
-        while (nd.code < 0) {
-            if (STATS) cnt.nodes++;
-            ni = slab_reject<FAST>(nd, ray, tmax) ? nd.miss : ni + 1;
-            if (ni >= n_nodes) break;
-            nd = nodes[ni];
-        }
-        if (ni >= n_nodes) break;
-        if (STATS) { cnt.nodes++; cnt.prims++; }
-        if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
-        ni = nd.miss;
-    }
-#elif CPT_LEAF_BATCH > 0
-    // Lanes that reach a leaf park there until a leaf phase; a lane's own visit sequence (and
-    // so its tmax history, pruning and first-found tie rule) is unchanged — only the
-    // interleaving of lanes changes.
     Node nd;
-    if (ni < n_nodes) nd = nodes[ni];
+    if (n_nodes > 0) nd = nodes[0];
+    const int last = n_nodes - 1;
+#if CPT_LEAF_BATCH > 0
+    // Leaf batching: a lane that reaches a leaf parks there; leaf tests run in a wave-uniform
+    // leaf phase once >= 1/K of the walking lanes are parked (or nobody can slab-test).  A
+    // lane's own visit sequence — and so its tmax history, pruning and first-found tie rule —
+    // is unchanged; only the interleaving of lanes changes.
     for (;;) {
         const bool walking = ni < n_nodes;
         const bool at_leaf = walking && nd.code >= 0;
         const uint64_t lm = __ballot(at_leaf), wm = __ballot(walking);
         if (wm == 0) break;
-        const bool leaf_phase = (lm == wm) || (__popcll(lm) * CPT_LEAF_BATCH >= __popcll(wm));
-        if (leaf_phase ? at_leaf : (walking && !at_leaf)) {
-            if (STATS) cnt.nodes++;
-            if (leaf_phase) {
-                if (STATS) cnt.prims++;
-                if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
-                ni = nd.miss;
-            } else {
-                ni = slab_reject<FAST>(nd, ray, tmax) ? nd.miss : ni + 1;
+        const int leaf_phase = __builtin_amdgcn_readfirstlane(
+            (lm == wm || __popcll(lm) * CPT_LEAF_BATCH >= __popcll(wm)) ? 1 : 0);
+        if (leaf_phase) {
+            if (at_leaf) {
+                const Node nx = nodes[ni + 1 < last ? ni + 1 : last];   // leaf: miss == ni + 1
+                if (STATS) { cnt.nodes++; cnt.prims++; }
+                int k;
+                if (leaf_test(nd, ray, tmax, k)) { best = ni; kind = k; }
+                ni = ni + 1;
+                nd = nx;
             }
-            if (ni < n_nodes) nd = nodes[ni];
+        } else if (walking && !at_leaf) {
+            const int na = ni + 1, nb = nd.miss;
+            const Node pa = nodes[na < last ? na : last];
+            const Node pb = nodes[nb < last ? nb : last];
+            if (STATS) cnt.nodes++;
+            const bool take_a = !slab_reject<FAST>(nd, ray, tmax);
+            ni = take_a ? na : nb;
+            nd = take_a ? pa : pb;
         }
     }
-#elif CPT_PREFETCH
+#else
     // The successor of node ni is ni + 1 (box hit: its right child) or nd.miss; both loads are
     // issued before the node's test so their latency hides under it (leaves: miss == ni + 1).
-    Node nd;
-    if (ni < n_nodes) nd = nodes[0];
-    const int last = n_nodes - 1;
     while (ni < n_nodes) {
+#if CPT_STAMPS == 2
+        const unsigned long long t0 = stamp();
+#endif
         const int na = ni + 1, nb = nd.miss;
         const Node pa = nodes[na < last ? na : last];
         const Node pb = nodes[nb < last ? nb : last];
         if (STATS) cnt.nodes++;
-        bool take_a;
-        if (nd.code >= 0) {
-            // leaf: IntersectionTest first (bvh.cu:175-180); its own box test is moot
+        bool take_a = false;
+        const bool leaf = nd.code >= 0;
+        if (leaf) {
+            // IntersectionTest first (bvh.cu:175-180); the leaf's own box test is moot
             if (STATS) cnt.prims++;
-            if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
-            take_a = false;
-        } else {
-            take_a = !slab_reject<FAST>(nd, ray, tmax);
+            int k;
+            if (leaf_test(nd, ray, tmax, k)) { best = ni; kind = k; }
         }
+#if CPT_STAMPS == 2
+        const unsigned long long t1 = stamp();
+#endif
+        if (!leaf) take_a = !slab_reject<FAST>(nd, ray, tmax);
+#if CPT_STAMPS == 2
+        const unsigned long long t2 = stamp();
+        cnt.st_leaf += t1 - t0;
+        cnt.st_slab += t2 - t1;
+#endif
         ni = take_a ? na : nb;
         nd = take_a ? pa : pb;
-    }
-#else
-    while (ni < n_nodes) {
-        const Node nd = nodes[ni];
-        if (STATS) cnt.nodes++;
-        if (nd.code >= 0) {
-            // leaf: IntersectionTest first (bvh.cu:175-180); its own box test is moot
-            if (STATS) cnt.prims++;
-            if (leaf_test(nd, ray, tmax, h)) { hit = true; code_out = nd.code; }
-            ni = nd.miss;
-        } else {
-            ni = slab_reject<FAST>(nd, ray, tmax) ? nd.miss : ni + 1;
-        }
+#if CPT_STAMPS == 2
+        cnt.st_iter += stamp() - t0;
+#endif
     }
 #endif
-    return hit;
+    if (best < 0) return false;
+    const Node w = nodes[best];
+    h = hit_attributes(w, ray, tmax, kind);
+    code_out = w.code;
+    return true;
 }
 
 // ======================================================================================

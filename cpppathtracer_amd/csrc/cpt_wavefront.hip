@@ -93,7 +93,7 @@ template <bool STATS>
 __global__ void __launch_bounds__(256) k_wf_extend(const KParams p, WfState w, const int32_t* __restrict__ qin,
                                                   const uint32_t* __restrict__ nin) {
     const uint32_t n = *nin;
-    Counters cnt{0, 0, 0, 0, 0};
+    Counters cnt{};
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const int pix = qin[i];
