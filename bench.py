@@ -75,6 +75,9 @@ def main():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--path", default="megakernel", choices=["megakernel", "wavefront"])
+    ap.add_argument("--walk", default="ordered", choices=["reference", "ordered"],
+                    help="BVH node order: the reference's right-first DFS, or near-first per ray octant "
+                         "(CPT_TRAVERSAL_ORDERED, same closest hits; DESIGN.md §Ordered walk)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=None,
@@ -133,12 +136,13 @@ def main():
     gathered = torch.zeros((world * max_rows * W, 4), dtype=torch.float32, device=dev) if world > 1 else None
     stitch_idx = torch.from_numpy(tiling.stitch_index(H, W, world)).to(dev) if world > 1 else None
     kernel_events = []
+    ordered = args.walk == "ordered"
 
     def step(timed=False):
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        r.render(cam, spp, depth, path=args.path)
+        r.render(cam, spp, depth, path=args.path, ordered=ordered)
         if timed:
             e1.record(stream)
             kernel_events.append((e0, e1))
@@ -151,16 +155,39 @@ def main():
             return fb
         return None
 
-    # Counting pass (same config, same pixels) for the algorithmic byte model; not timed.
-    r.reset_stats()
-    r.render(cam, spp, depth, stats=True, path=args.path)
-    torch.cuda.synchronize()
-    st_local = r.stats()
-    st_vec = torch.tensor([st_local[k] for k in ("segments", "nodes", "prims", "hits", "misses")],
-                          dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(st_vec)
-    st = dict(zip(("segments", "nodes", "prims", "hits", "misses"), (int(x) for x in st_vec.tolist())))
+    # Counting pass (same config, same pixels) for the algorithmic byte model; not timed.  It
+    # always walks the reference order: the byte model prices the reference algorithm's node
+    # and primitive fetches, whatever walk the timed steps use.
+    KEYS = ("segments", "nodes", "prims", "hits", "misses")
+
+    def count_pass(walk_ordered):
+        r.init_rng(cfg["seed"])     # both counting passes trace the same paths
+        r.reset_stats()
+        r.render(cam, spp, depth, stats=True, path=args.path, ordered=walk_ordered)
+        torch.cuda.synchronize()
+        loc = r.stats()
+        v = torch.tensor([loc[k] for k in KEYS], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(v)
+        return dict(zip(KEYS, (int(x) for x in v.tolist())))
+
+    st = count_pass(False)
+    walk_counts, walk_diff = None, None
+    if ordered:
+        # full-size parity of the ordered walk against the reference walk: the two counting
+        # passes trace the same paths, so their framebuffers must be bit-identical
+        fb_ref = torch.empty((npix_local, 4), dtype=torch.float32, device=dev)
+        r.copy_accum_device(fb_ref.data_ptr(), npix_local * 16)
+        walk_counts = count_pass(True)
+        fb_ord = torch.empty_like(fb_ref)
+        r.copy_accum_device(fb_ord.data_ptr(), npix_local * 16)
+        torch.cuda.synchronize()
+        nd = (fb_ref.view(torch.int32) != fb_ord.view(torch.int32)).any(dim=1).sum().to(torch.float64)
+        if world > 1:
+            dist.all_reduce(nd)
+        walk_diff = int(nd.item())
+        del fb_ref, fb_ord
+    r.init_rng(cfg["seed"])
 
     for _ in range(args.warmup):
         step()
@@ -194,15 +221,19 @@ def main():
         share = npix_local / float(W * H)
         bytes_launch = byte_model(st, paths_total) * share
         achieved = bytes_launch / (avg_kernel_ms / 1e3) / 1e9
+        # the same per-unit byte model on the executed walk's own node/prim counts (the ordered
+        # walk visits fewer nodes than the reference algorithm for the same closest hits)
+        achieved_walk = (byte_model(walk_counts, paths_total) * share / (avg_kernel_ms / 1e3) / 1e9
+                         if walk_counts else achieved)
         # HBM traffic per launch from rocprofv3 PMC passes of this same workload (committed under
         # profiles/, made by tools/profile.sh + tools/pmc_traffic.py); null when none matches.
         traffic = None
-        tpath = args.traffic_json or os.path.join(REPO, "profiles", f"traffic_{args.config}_{args.path}.json")
+        tpath = args.traffic_json or os.path.join(REPO, "profiles", f"traffic_{args.config}_{args.path}_{args.walk}.json")
         if os.path.exists(tpath):
             with open(tpath) as f:
                 tj = json.load(f)
             if (tj.get("config") == args.config and tj.get("n_rows") == int(rows.size) and tj.get("spp") == spp
-                    and tj.get("path") == args.path):
+                    and tj.get("path") == args.path and tj.get("walk", "reference") == args.walk):
                 traffic = tj.get("hbm_bytes_per_launch")
         out = {
             "metric": METRIC,
@@ -220,7 +251,7 @@ def main():
             "config": {
                 "workload": f"{args.config}: {cfg['scene']} {W}x{H} {spp}spp depth {depth}",
                 "width": W, "height": H, "spp": spp, "max_depth": depth, "seed": cfg["seed"],
-                "rows_rendered": H, "path": args.path,
+                "rows_rendered": H, "path": args.path, "walk": args.walk,
                 "parallelism": f"row-tiled x{world} (interleaved 16-row blocks)" + (", RCCL all-gather" if world > 1 else ""),
             },
             "roofline": {
@@ -230,11 +261,14 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "achieved_walk": round(achieved_walk, 2),
                 "kernel": "k_megakernel" if args.path == "megakernel" else "wavefront (k_wf_extend+k_wf_shade per bounce)",
                 "kernel_avg_ms": round(avg_kernel_ms, 3),
                 "bytes_per_launch": int(bytes_launch),
                 "byte_model": "SURVEY.md 8(d): 76 S + 32 nodes + 32 prims + 40 hits + 16 misses + 16 P",
                 "counts": st,
+                "walk_counts": walk_counts,
+                "walk_vs_reference_pixels_differing": walk_diff,
             },
             "rng_init_ms": round(t_init * 1e3, 2),
         }

@@ -73,6 +73,7 @@ struct BNode {            // bvh.h:32-38, object stored as an index
     F3 bmin, bmax;
     bool is_object;
     int left, right, obj, parent;
+    int axis;              // split axis of an internal node (its children's centroid order)
 };
 
 struct HostBvh {
@@ -124,6 +125,7 @@ int divide(HostBvh& b, const std::vector<cpt_object>& objs, std::vector<int>& id
     n.bmax = F3{maxx, maxy, maxz};
     n.is_object = false;
     n.obj = -1;
+    n.axis = axis;
     b.nodes[left].parent = ret;
     b.nodes[right].parent = ret;
     return ret;
@@ -159,34 +161,49 @@ Node make_node(const BNode& n, const std::vector<cpt_object>& objs, const std::v
 }
 
 // Right-first preorder = the order the reference's stack DFS pops nodes (left pushed first,
-// bvh.cu:201-202).  miss[i] = position after node i's subtree.
+// bvh.cu:201-202).  Internal nodes: miss = position after the node's subtree.  Leaves: the
+// walk always continues at position + 1, so `miss` carries the leaf's position in this
+// reference order instead (the tie rank of the ordered walk, cpt_path.hpp trace).
+//
+// octant >= 0 builds the near-first order for rays whose direction signs are the octant's
+// bits (bit a set = negative along axis a): at each internal node the child on the near side
+// of its split axis comes first.  ref_pos gives the leaves' reference positions.
 void linearise(const HostBvh& b, const std::vector<cpt_object>& objs, const std::vector<int>& mat_of_obj,
-               std::vector<Node>& out, std::vector<int>& pos_of_node) {
-    out.clear();
+               std::vector<Node>& out, std::vector<int>& pos_of_node, int octant, const std::vector<int>* ref_pos,
+               int root = 0, const std::vector<int>& prefix = {}) {
+    const size_t base = out.size();
     pos_of_node.assign(b.nodes.size(), -1);
-    if (b.nodes.empty()) return;
+    for (int leaf : prefix) {            // unbounded leaves, tested before the tree
+        pos_of_node[leaf] = (int)(out.size() - base);
+        out.push_back(make_node(b.nodes[leaf], objs, mat_of_obj));
+        out.back().miss = (*ref_pos)[leaf];
+    }
+    if (b.nodes.empty() || root < 0) return;
     struct Frame { int node; int stage; };
     std::vector<Frame> st;
-    st.push_back({0, 0});
-    out.reserve(b.nodes.size());
+    st.push_back({root, 0});
     while (!st.empty()) {
         Frame& f = st.back();
         const BNode& n = b.nodes[f.node];
         if (f.stage == 0) {
-            pos_of_node[f.node] = (int)out.size();
+            pos_of_node[f.node] = (int)(out.size() - base);
             out.push_back(make_node(n, objs, mat_of_obj));
             if (n.is_object) {
-                out[pos_of_node[f.node]].miss = (int)out.size();
+                out.back().miss = ref_pos ? (*ref_pos)[f.node] : pos_of_node[f.node];
                 st.pop_back();
                 continue;
             }
             f.stage = 1;
-            st.push_back({n.right, 0});
+            // the reference pops the right child first; a ray moving +axis meets the left
+            // (lower-centroid) child first
+            const bool right_first = octant < 0 || ((octant >> n.axis) & 1);
+            st.push_back({right_first ? n.right : n.left, 0});
         } else if (f.stage == 1) {
             f.stage = 2;
-            st.push_back({n.left, 0});
+            const bool right_first = octant < 0 || ((octant >> n.axis) & 1);
+            st.push_back({right_first ? n.left : n.right, 0});
         } else {
-            out[pos_of_node[f.node]].miss = (int)out.size();
+            out[base + pos_of_node[f.node]].miss = (int)(out.size() - base);
             st.pop_back();
         }
     }
@@ -269,8 +286,10 @@ struct cpt_ctx {
     // scene
     std::vector<cpt_object> objs;
     HostBvh bvh;
-    std::vector<Node> lin;
-    std::vector<int> pos_of_node;
+    std::vector<Node> lin;             // 9 orders of n_bvh nodes: reference, then octants 0..7
+    std::vector<int> pos_of_node;      // BNode -> position in the reference order
+    int n_bvh = 0;                     // nodes of the reference order
+    int n_walk = 0;                    // nodes of each octant order (walk tree + unbounded leaves)
     std::vector<Mat> mats_h;           // deduplicated materials
     std::vector<int> mat_of_obj;       // object index -> material index
     Node* d_nodes = nullptr;
@@ -382,6 +401,59 @@ int material_slot(cpt_ctx* c, const cpt_material& m) {
         if (std::memcmp(&c->mats_h[i], &g, sizeof(Mat)) == 0) return (int)i;
     c->mats_h.push_back(g);
     return (int)c->mats_h.size() - 1;
+}
+
+// Walk tree of the ordered walk (CPT_TRAVERSAL_ORDERED): the reference tree with every
+// platform leaf spliced out (its sibling takes the parent's place, the ancestors' boxes are
+// refit with MIN/MAX of their children).  A platform's box spans +-5e30 in x and z, so in the
+// reference tree every ancestor of the floor passes its slab test; without it those nodes
+// cull.  All other boxes stay the reference's.  The spliced leaves (by reference rank) are
+// returned in `unbounded`; the ordered walk tests them first.
+int build_walk_tree(const HostBvh& b, const std::vector<cpt_object>& objs, const std::vector<int>& ref_pos,
+                    HostBvh& w, std::vector<int>& unbounded) {
+    w = b;
+    unbounded.clear();
+    if (w.nodes.empty()) return -1;
+    int root = 0;
+    std::vector<int> order(w.nodes.size());
+    for (size_t i = 0; i < order.size(); ++i) order[ref_pos[i]] = (int)i;
+    for (int i : order) {
+        BNode& n = w.nodes[i];
+        if (!n.is_object || objs[n.obj].type != CPT_PRIM_PLATFORM) continue;
+        unbounded.push_back(i);
+        int p = n.parent;
+        if (p < 0) { root = -1; continue; }
+        int sib = w.nodes[p].left == i ? w.nodes[p].right : w.nodes[p].left;
+        int gp = w.nodes[p].parent;
+        w.nodes[sib].parent = gp;
+        if (gp < 0) root = sib;
+        else if (w.nodes[gp].left == p) w.nodes[gp].left = sib;
+        else w.nodes[gp].right = sib;
+        for (int a = gp; a >= 0; a = w.nodes[a].parent) {
+            BNode& A = w.nodes[a];
+            const BNode &L = w.nodes[A.left], &R = w.nodes[A.right];
+            A.bmin = F3{MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z)};
+            A.bmax = F3{MAX_(L.bmax.x, R.bmax.x), MAX_(L.bmax.y, R.bmax.y), MAX_(L.bmax.z, R.bmax.z)};
+        }
+    }
+    return root;
+}
+
+// The reference order followed by the eight octant orders of the walk tree (one array,
+// n_bvh nodes each: the unbounded leaves, then the tree).
+void linearise_all(cpt_ctx* c) {
+    c->lin.clear();
+    c->n_walk = 0;
+    c->lin.reserve(9 * c->bvh.nodes.size());
+    linearise(c->bvh, c->objs, c->mat_of_obj, c->lin, c->pos_of_node, -1, nullptr);
+    c->n_bvh = (int)c->lin.size();
+    if (c->n_bvh == 0) return;
+    HostBvh w;
+    std::vector<int> unbounded, pos;
+    const int root = build_walk_tree(c->bvh, c->objs, c->pos_of_node, w, unbounded);
+    for (int o = 0; o < 8; ++o)
+        linearise(w, c->objs, c->mat_of_obj, c->lin, pos, o, &c->pos_of_node, root, unbounded);
+    c->n_walk = (int)(c->lin.size() - c->n_bvh) / 8;
 }
 
 int upload_scene(cpt_ctx* c) {
@@ -531,7 +603,7 @@ int cpt_set_scene(cpt_ctx* c, const cpt_object* objs, int n) {
         c->mats_h.clear();
         c->mat_of_obj.assign(n, 0);
         for (int i = 0; i < n; ++i) c->mat_of_obj[i] = material_slot(c, c->objs[i].material);
-        linearise(c->bvh, c->objs, c->mat_of_obj, c->lin, c->pos_of_node);
+        linearise_all(c);
     } catch (const std::bad_alloc&) {
         return fail(c, CPT_ERR_OUT_OF_MEMORY, "cpt_set_scene: host allocation failed");
     }
@@ -559,12 +631,9 @@ int cpt_update_object(cpt_ctx* c, int index, const cpt_object* obj) {
             n.bmax = F3{MAX_(L.bmax.x, R.bmax.x), MAX_(L.bmax.y, R.bmax.y), MAX_(L.bmax.z, R.bmax.z)};
             n.bmin = F3{MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z)};
         }
-        Node& g = c->lin[c->pos_of_node[ni]];
-        int miss = g.miss;
-        g = make_node(n, c->objs, c->mat_of_obj);
-        g.miss = miss;
         ni = n.parent;
     }
+    linearise_all(c);   // same topology, new boxes and leaf contents in all nine orders
     return upload_scene(c);
 }
 
@@ -720,7 +789,9 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     std::memset(&p, 0, sizeof(p));
     p.nodes = c->d_nodes;
     p.mats = c->d_mats;
-    p.n_nodes = (int)c->lin.size();
+    p.n_nodes = c->n_bvh;
+    p.n_walk = c->n_walk;
+    p.ordered = (flags & CPT_TRAVERSAL_ORDERED) ? 1 : 0;
     p.env = c->d_env;
     p.env_w = c->env_w;
     p.env_h = c->env_h;

@@ -274,13 +274,16 @@ __device__ __forceinline__ float uniform(Xorwow& s) {
 // Scene data in HBM (DESIGN.md §Data layout)
 // ------------------------------------------------------------------------------------
 // BVH node, 32 B, right-first preorder ("skip-link" order): the node after n in memory is
-// its right child (the child the reference's DFS pops first, bvh.cu:201-202); `miss` is the
-// next node in that order once n's subtree is skipped or finished.
-//   internal (code < 0): a = AABB min, b = AABB max
+// its right child (the child the reference's DFS pops first, bvh.cu:201-202).  The eight
+// octant orders (CPT_TRAVERSAL_ORDERED) put the near child of each split first instead.
+//   internal (code < 0): a = AABB min, b = AABB max, miss = next node once n's subtree is
+//            skipped or finished
 //   leaf     (code >= 0): the primitive inline (a leaf's own box is never tested: in the
 //            reference its slab test only decides whether to push two -1 sentinels):
 //            a = center, b = {radius, y_pos, height}, code = material << 2 | type
-//            (type 3 = unknown PrimitiveType: IntersectionTest returns false, object.cu:126)
+//            (type 3 = unknown PrimitiveType: IntersectionTest returns false, object.cu:126);
+//            the walk continues at n + 1, and miss = the leaf's position in the reference
+//            order (its rank for equal hit distances)
 struct __attribute__((aligned(16))) Node {
     float a0, a1, a2;
     int32_t miss;

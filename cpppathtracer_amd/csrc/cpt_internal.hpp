@@ -21,9 +21,11 @@ struct CamK {
 // Kernel arguments (passed by value: they land in the kernarg segment and are read with
 // scalar loads).
 struct KParams {
-    const Node* nodes;      // skip-link order, leaves inline (cpt_device.hpp)
+    const Node* nodes;      // skip-link orders, leaves inline: the reference order (n_nodes), then
+                            // the walk tree's eight octant orders (n_walk each)
     const Mat* mats;        // deduplicated materials, indexed by Node::code >> 2
-    int n_nodes;
+    int n_nodes, n_walk;
+    int ordered;            // CPT_TRAVERSAL_ORDERED: walk the ray's octant order
     const uint32_t* env;    // packed RGBA8, env_cols x env_h
     int env_w, env_h, env_cols;
     CamK cam;

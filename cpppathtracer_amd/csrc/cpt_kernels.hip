@@ -141,8 +141,11 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             const bool finite_ray = !(ray.o.x != ray.o.x || ray.o.y != ray.o.y || ray.o.z != ray.o.z ||
                                       ray.d.x != ray.d.x || ray.d.y != ray.d.y || ray.d.z != ray.d.z);
             bool hit;
-            if (__builtin_expect(finite_ray, 1)) hit = trace<STATS, true>(nodes, p.n_nodes, rk, h, code, cnt);
-            else hit = trace<STATS, false>(nodes, p.n_nodes, rk, h, code, cnt);
+            int n_order;
+            const Node* order = LDS ? nodes : walk_order(p, rk.d, n_order);
+            if (LDS) n_order = p.n_nodes;
+            if (__builtin_expect(finite_ray, 1)) hit = trace<STATS, true>(order, n_order, rk, h, code, cnt);
+            else hit = trace<STATS, false>(order, n_order, rk, h, code, cnt);
             t2 = stamp();
             Shade sh;
             v3 attr_normal;
@@ -501,7 +504,7 @@ hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t
     if (p.width <= 0 || p.n_rows <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(p.work, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    const bool lds = p.n_nodes > 0 && p.n_nodes <= lds_node_capacity();
+    const bool lds = !p.ordered && p.n_nodes > 0 && p.n_nodes <= lds_node_capacity();
     if (lds) {
         if (stats && aux) return launch_mk<true, true, true>(p, stream);
         if (stats) return launch_mk<true, false, true>(p, stream);

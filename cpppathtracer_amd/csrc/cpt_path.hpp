@@ -147,7 +147,7 @@ __device__ __forceinline__ bool cap_test(float cx, float cz, float radius, const
             const float hx = ray.o.x + temp * ray.d.x, hz = ray.o.z + temp * ray.d.z;
             if (__builtin_sqrtf((hx - cx) * (hx - cx) + (hz - cz) * (hz - cz)) < radius) {
                 tmax = temp;
-                kind = HK_FACING_Y;
+                    kind = HK_FACING_Y;
                 return true;
             }
         }
@@ -305,11 +305,36 @@ __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, flo
 #define CPT_LEAF_BATCH 0   // K > 0: leaf tests run in wave-uniform leaf phases (see trace)
 #endif
 
+// The node order a ray walks: the reference order, or with CPT_TRAVERSAL_ORDERED the walk
+// tree's order for its direction octant (near child of every split first, DESIGN.md
+// §Ordered walk).  Returns the first node and sets the order's length.
+__device__ __forceinline__ const Node* walk_order(const KParams& p, v3 d, int& n) {
+    if (!p.ordered) { n = p.n_nodes; return p.nodes; }
+    const int oct = (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
+    n = p.n_walk;
+    return p.nodes + p.n_nodes + (size_t)oct * p.n_walk;
+}
+
+// Leaf test with the reference's first-found rule for equal distances.  `rank` is the leaf's
+// position in the reference order, best_rank the current closest primitive's.  A primitive the
+// reference meets earlier (rank < best_rank; only possible in the ordered walk) must win a
+// tie, so it is tested against next_up(tmax): "temp < next_up(tmax)" == "temp <= tmax".  Its
+// first accepted case sets tmax = temp, so its later cases compare strictly, as in the
+// reference.  tmax > 0 always (hits need temp > tmin >= 0), so next_up is the bit pattern + 1.
+__device__ __forceinline__ bool ranked_leaf_test(const Node& nd, const RayK& ray, float& tmax, int& kind, int& best_rank) {
+    float tm = nd.miss < best_rank ? __int_as_float(__float_as_int(tmax) + 1) : tmax;
+    if (!leaf_test(nd, ray, tm, kind)) return false;
+    tmax = tm;
+    best_rank = nd.miss;
+    return true;
+}
+
 template <bool STATS, bool FAST>
 __device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_nodes, const RayK& ray, Hit& h,
                                       int& code_out, Counters& cnt) {
     float tmax = DEFAULT_RAY_TMAX;
     int best = -1, kind = 0;
+    int best_rank = 0x7fffffff;   // reference-order position of the current closest primitive
     int ni = 0;
     Node nd;
     if (n_nodes > 0) nd = nodes[0];
@@ -328,10 +353,10 @@ __device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_node
             (lm == wm || __popcll(lm) * CPT_LEAF_BATCH >= __popcll(wm)) ? 1 : 0);
         if (leaf_phase) {
             if (at_leaf) {
-                const Node nx = nodes[ni + 1 < last ? ni + 1 : last];   // leaf: miss == ni + 1
+                const Node nx = nodes[ni + 1 < last ? ni + 1 : last];
                 if (STATS) { cnt.nodes++; cnt.prims++; }
                 int k;
-                if (leaf_test(nd, ray, tmax, k)) { best = ni; kind = k; }
+                if (ranked_leaf_test(nd, ray, tmax, k, best_rank)) { best = ni; kind = k; }
                 ni = ni + 1;
                 nd = nx;
             }
@@ -346,23 +371,23 @@ __device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_node
         }
     }
 #else
-    // The successor of node ni is ni + 1 (box hit: its right child) or nd.miss; both loads are
-    // issued before the node's test so their latency hides under it (leaves: miss == ni + 1).
+    // The successor of node ni is ni + 1 (box hit: its first child; after a leaf) or nd.miss
+    // (box miss); both loads are issued before the node's test so their latency hides under it.
     while (ni < n_nodes) {
 #if CPT_STAMPS == 2
         const unsigned long long t0 = stamp();
 #endif
-        const int na = ni + 1, nb = nd.miss;
+        const bool leaf = nd.code >= 0;
+        const int na = ni + 1, nb = leaf ? na : nd.miss;
         const Node pa = nodes[na < last ? na : last];
         const Node pb = nodes[nb < last ? nb : last];
         if (STATS) cnt.nodes++;
         bool take_a = false;
-        const bool leaf = nd.code >= 0;
         if (leaf) {
             // IntersectionTest first (bvh.cu:175-180); the leaf's own box test is moot
             if (STATS) cnt.prims++;
             int k;
-            if (leaf_test(nd, ray, tmax, k)) { best = ni; kind = k; }
+            if (ranked_leaf_test(nd, ray, tmax, k, best_rank)) { best = ni; kind = k; }
         }
 #if CPT_STAMPS == 2
         const unsigned long long t1 = stamp();

@@ -110,8 +110,10 @@ __global__ void __launch_bounds__(256) k_wf_extend(const KParams p, WfState w, c
         int code = -1;
         if (STATS) cnt.segments++;
         bool hit;
-        if (__builtin_expect(finite, 1)) hit = trace<STATS, true>(p.nodes, p.n_nodes, rk, h, code, cnt);
-        else hit = trace<STATS, false>(p.nodes, p.n_nodes, rk, h, code, cnt);
+        int n_order;
+        const Node* order = walk_order(p, rk.d, n_order);
+        if (__builtin_expect(finite, 1)) hit = trace<STATS, true>(order, n_order, rk, h, code, cnt);
+        else hit = trace<STATS, false>(order, n_order, rk, h, code, cnt);
         w.hit_p[pix] = make_float4(h.pos.x, h.pos.y, h.pos.z, __int_as_float(hit ? code : -1));
         if (hit) w.hit_n[pix] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.f);
     }

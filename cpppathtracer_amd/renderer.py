@@ -9,7 +9,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import (CPT_PATH_WAVEFRONT, CPT_RENDER_ACCUMULATE, CPT_RENDER_AUX, CPT_RENDER_STATS, CPT_RENDER_SYNC,
+from ._lib import (CPT_PATH_WAVEFRONT, CPT_TRAVERSAL_ORDERED, CPT_RENDER_ACCUMULATE, CPT_RENDER_AUX, CPT_RENDER_STATS, CPT_RENDER_SYNC,
                    CptError, check)
 
 PATHS = ("megakernel", "wavefront")
@@ -112,13 +112,16 @@ class Renderer:
 
     # -- render ----------------------------------------------------------------------
     def render(self, cam, spp, max_depth, accumulate=False, aux=False, stats=False, sync=False, flags=0,
-               path="megakernel"):
+               path="megakernel", ordered=False):
         """path: "megakernel" (per-lane regeneration, state in VGPRs) or "wavefront" (SoA state in
-        HBM, extend/shade kernels with ballot compaction).  Both give identical results."""
+        HBM, extend/shade kernels with ballot compaction).  Both give identical results.
+        ordered: near-first BVH walk per direction octant (CPT_TRAVERSAL_ORDERED); same closest
+        hits as the reference order up to box/primitive rounding (DESIGN.md §Ordered walk)."""
         if path not in PATHS:
             raise ValueError(f"path must be one of {PATHS}")
         c = np.ascontiguousarray(np.array(cam, dtype=CAMERA_DTYPE))
         f = flags | (CPT_PATH_WAVEFRONT if path == "wavefront" else 0)
+        f |= CPT_TRAVERSAL_ORDERED if ordered else 0
         f |= CPT_RENDER_ACCUMULATE if accumulate else 0
         f |= CPT_RENDER_AUX if aux else 0
         f |= CPT_RENDER_STATS if stats else 0

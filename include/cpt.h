@@ -126,6 +126,13 @@ typedef struct cpt_ctx cpt_ctx;
 #define CPT_RENDER_SYNC       0x8u   /* block until the render finished                        */
 #define CPT_PATH_MEGAKERNEL   0x000u /* per-lane path regeneration megakernel (default)        */
 #define CPT_PATH_WAVEFRONT    0x100u /* SoA wavefront: extend / shade / compact per bounce      */
+/* Near-first BVH walk: each ray walks the node order of its direction octant (near child of
+ * every split first), and equal distances go to the primitive the reference order meets
+ * first.  It finds the same closest hit as the reference's right-first DFS
+ * (bvh.cu:167-205) unless a primitive's computed hit distance lies outside its own box's
+ * computed slab interval by rounding (DESIGN.md §Ordered walk).  Node/prim counts
+ * (CPT_RENDER_STATS) are then this walk's counts, not the reference's. */
+#define CPT_TRAVERSAL_ORDERED 0x200u
 
 int cpt_abi_version(void);
 const char* cpt_status_string(int status);

@@ -67,6 +67,10 @@ def lib():
         L.or_denoise_mix.restype = None
         L.or_render.argtypes = [P, i32, P, P, i32, i32, i32, P, i32, i32, i32, P, P, P, P, P, i32, i32]
         L.or_render.restype = i32
+        L.or_render_edited.argtypes = [P, i32, P, P, i32, P, P, i32, i32, i32, P, i32, i32, i32, P, P, P, i32]
+        L.or_render_edited.restype = i32
+        L.or_set_walk.argtypes = [i32]
+        L.or_set_walk.restype = None
         _lib = L
     return _lib
 
@@ -151,6 +155,33 @@ def render(objs, cam, env, rows, spp, max_depth, rng, accum=None, want_aux=False
         raise ValueError(f"or_render failed: {rc}")
     st = dict(zip(("segments", "nodes", "prims", "hits", "misses"), (int(x) for x in stats)))
     return accum, st, normal, depth
+
+
+def set_walk(ordered: bool):
+    """DIAGNOSTIC: make render() walk the BVH the way CPT_TRAVERSAL_ORDERED does (near child
+    first, reference-rank tie rule) instead of the reference's right-first DFS.  Process-wide."""
+    lib().or_set_walk(1 if ordered else 0)
+
+
+def render_edited(objs, edits, cam, env, rows, spp, max_depth, rng, threads=1):
+    """render() on the BVH of `objs` after SceneBVH::UpdateObject edits [(index, new_object), ...]
+    (refit, same topology, bvh.cu:122-157).  Returns (accum, stats)."""
+    objs = np.ascontiguousarray(objs)
+    cam = np.ascontiguousarray(cam)
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    idx = np.ascontiguousarray([i for i, _ in edits], dtype=np.int32)
+    new = np.ascontiguousarray(np.array([o for _, o in edits], dtype=objs.dtype))
+    npix = rows.size * int(cam["width"])
+    assert rng.dtype == np.uint32 and rng.shape == (6, npix) and rng.flags.c_contiguous
+    accum = np.zeros((npix, 4), dtype=np.float32)
+    stats = np.zeros(5, dtype=np.uint64)
+    env_ptr = _ptr(env.rgba) if env is not None else None
+    ew, eh, ec = (env.width, env.height, env.valid_cols) if env is not None else (1, 1, 0)
+    rc = lib().or_render_edited(_ptr(objs), len(objs), _ptr(idx), _ptr(new), idx.size, _ptr(cam), env_ptr, ew, eh, ec,
+                                _ptr(rows), rows.size, spp, max_depth, _ptr(rng), _ptr(accum), _ptr(stats), threads)
+    if rc != 0:
+        raise ValueError(f"or_render_edited failed: {rc}")
+    return accum, dict(zip(("segments", "nodes", "prims", "hits", "misses"), (int(x) for x in stats)))
 
 
 def denoise_mix(accum, normal, depth, mix, out, width, height, cur_sample_idx):

@@ -494,6 +494,12 @@ f3 aabb_min(const Object& o) {                                  // object.cu:153
 struct Bvh {
     std::vector<Node> nodes;
     const Object* objs;
+    // diagnostic ordered walk only (trace_ray_ordered):
+    std::vector<int> axis;       // split axis per internal node
+    std::vector<int> rank;       // right-first preorder position
+    std::vector<Node> walk;      // the tree with the unbounded (platform) leaves spliced out
+    int walk_root = -1;
+    std::vector<int> unbounded;  // spliced-out leaves, by rank
 };
 
 // std::sort in the reference (bvh.cu:67-80) is unstable; ties between equal centroids are
@@ -530,6 +536,8 @@ int divide(Bvh& bvh, std::vector<int>& idx, int l, int r) {      // bvh.cu:31-90
     };
     std::stable_sort(idx.begin() + l, idx.begin() + r, [&](int a, int b) { return centroid(a) < centroid(b); });
     int mid = (l + r) / 2;
+    if ((int)bvh.axis.size() <= ret) bvh.axis.resize(ret + 1, 0);
+    bvh.axis[ret] = axis;
     int left = divide(bvh, idx, l, mid);
     int right = divide(bvh, idx, mid, r);
     Node& n = bvh.nodes[ret];
@@ -541,12 +549,59 @@ int divide(Bvh& bvh, std::vector<int>& idx, int l, int r) {      // bvh.cu:31-90
     return ret;
 }
 
+void build_walk_tree(Bvh& bvh);
+
 void build_bvh(Bvh& bvh, const Object* objs, int n) {
     bvh.objs = objs;
     bvh.nodes.clear();
     std::vector<int> idx(n);
     for (int i = 0; i < n; ++i) idx[i] = i;
     divide(bvh, idx, 0, n);
+    bvh.axis.resize(bvh.nodes.size(), 0);
+    bvh.rank.assign(bvh.nodes.size(), 0);
+    int pos = 0;
+    std::vector<int> st;
+    if (n > 0) st.push_back(0);
+    while (!st.empty()) {                 // the reference's pop order: right child first
+        int ni = st.back();
+        st.pop_back();
+        bvh.rank[ni] = pos++;
+        if (!bvh.nodes[ni].is_object) { st.push_back(bvh.nodes[ni].left); st.push_back(bvh.nodes[ni].right); }
+    }
+    build_walk_tree(bvh);
+}
+
+// Walk tree of the diagnostic ordered walk: each platform leaf is removed, its sibling takes
+// its parent's place and the ancestors' boxes are refit (MIN/MAX of the children).
+void build_walk_tree(Bvh& bvh) {
+    const Object* objs = bvh.objs;
+    const int n = (int)bvh.nodes.size();
+    bvh.walk = bvh.nodes;
+    bvh.walk_root = n > 0 ? 0 : -1;
+    bvh.unbounded.clear();
+    std::vector<int> parent(bvh.walk.size(), -1);
+    for (size_t i = 0; i < bvh.walk.size(); ++i)
+        if (!bvh.walk[i].is_object) { parent[bvh.walk[i].left] = (int)i; parent[bvh.walk[i].right] = (int)i; }
+    std::vector<int> order(bvh.walk.size());
+    for (size_t i = 0; i < order.size(); ++i) order[bvh.rank[i]] = (int)i;
+    for (int i : order) {
+        if (!bvh.walk[i].is_object || objs[bvh.walk[i].obj].type != PRIM_PLATFORM) continue;
+        bvh.unbounded.push_back(i);
+        int p = parent[i];
+        if (p < 0) { bvh.walk_root = -1; continue; }
+        int sib = bvh.walk[p].left == i ? bvh.walk[p].right : bvh.walk[p].left;
+        int gp = parent[p];
+        parent[sib] = gp;
+        if (gp < 0) bvh.walk_root = sib;
+        else if (bvh.walk[gp].left == p) bvh.walk[gp].left = sib;
+        else bvh.walk[gp].right = sib;
+        for (int a = gp; a >= 0; a = parent[a]) {
+            Node& A = bvh.walk[a];
+            const Node &L = bvh.walk[A.left], &R = bvh.walk[A.right];
+            A.bmin = mk(MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z));
+            A.bmax = mk(MAX_(L.bmax.x, R.bmax.x), MAX_(L.bmax.y, R.bmax.y), MAX_(L.bmax.z, R.bmax.z));
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -658,8 +713,22 @@ struct Stats { uint64_t segments, nodes, prims, hits, misses; };
 
 // SceneBVH::TraceRay (bvh.cu:167-205): DFS, explicit stack, leaf test before slab test,
 // left pushed before right (right popped first), ray taken BY VALUE.
+bool slab_pass(const Node& n, const Ray& ray);
+bool trace_ray_ordered(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st);
+static int g_walk_ordered = 0;
+// Diagnostic hook for walk experiments compiled against this file (never set by the library).
+static bool (*g_trace_hook)(const Bvh&, Ray, Attr&, int&, Stats&) = nullptr;
+
+bool trace_ray_ref(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st);
+
 bool trace_ray(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st) {
     if (bvh.nodes.empty()) return false;
+    if (g_trace_hook) return g_trace_hook(bvh, ray, attr, hit_obj, st);
+    if (g_walk_ordered) return trace_ray_ordered(bvh, ray, attr, hit_obj, st);
+    return trace_ray_ref(bvh, ray, attr, hit_obj, st);
+}
+
+bool trace_ray_ref(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st) {
     int stack[512];
     int top = 0;
     stack[top++] = 0;
@@ -696,6 +765,68 @@ bool trace_ray(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st) {
         if (top + 2 > 512) return ret;   // reference would overflow; unreachable for sane trees
         stack[top++] = n.left;
         stack[top++] = n.right;
+    }
+    return ret;
+}
+
+// ---------------------------------------------------------------------------------------
+// DIAGNOSTIC ONLY (or_set_walk(1)); not the reference algorithm.  A restatement of this
+// build's CPT_TRAVERSAL_ORDERED walk, used by tests/tools to compare the ordered walk's own
+// node/primitive counts and to study where it can part from the reference.  The unbounded
+// (platform) leaves are tested first, then the walk tree (bvh.walk) is walked with the child
+// nearer along the split axis (by the ray's direction sign) first.  A leaf the reference
+// meets earlier than the current closest primitive (lower right-first preorder rank) is
+// tested against next_up(tmax), i.e. wins ties.
+// ---------------------------------------------------------------------------------------
+bool slab_pass(const Node& n, const Ray& ray) {                 // bvh.cu:181-200
+    float local_tmin = -DEFAULT_RAY_TMAX * 2, local_tmax = DEFAULT_RAY_TMAX * 2;
+    const float o[3] = {ray.origin.x, ray.origin.y, ray.origin.z}, d[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
+    const float lo[3] = {n.bmin.x, n.bmin.y, n.bmin.z}, hi[3] = {n.bmax.x, n.bmax.y, n.bmax.z};
+    for (int a = 0; a < 3; ++a) {
+        if (d[a] == 0.f) continue;
+        float t0 = (lo[a] - o[a]) / d[a], t1 = (hi[a] - o[a]) / d[a];
+        local_tmin = MAX_(local_tmin, MIN_(t0, t1));
+        local_tmax = MIN_(local_tmax, MAX_(t0, t1));
+    }
+    return !(local_tmin > local_tmax || local_tmin > ray.tmax || local_tmax < ray.tmin);
+}
+
+bool trace_ray_ordered(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st) {
+    bool ret = false;
+    int best_rank = 0x7fffffff;
+    auto leaf = [&](int ni) {
+        st.nodes++;
+        st.prims++;
+        Ray r2 = ray;
+        if (bvh.rank[ni] < best_rank) {
+            uint32_t u;
+            std::memcpy(&u, &r2.tmax, 4);
+            u += 1;
+            std::memcpy(&r2.tmax, &u, 4);
+        }
+        if (intersection_test(bvh.objs[bvh.walk[ni].obj], r2, attr)) {
+            ray.tmax = r2.tmax;
+            hit_obj = bvh.walk[ni].obj;
+            best_rank = bvh.rank[ni];
+            ret = true;
+        }
+    };
+    for (int ni : bvh.unbounded) leaf(ni);
+    if (bvh.walk_root < 0) return ret;
+    int stack[512];
+    int top = 0;
+    stack[top++] = bvh.walk_root;
+    const float d[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
+    while (top > 0) {
+        int ni = stack[--top];
+        const Node& n = bvh.walk[ni];
+        if (n.is_object) { leaf(ni); continue; }
+        st.nodes++;
+        if (!slab_pass(n, ray)) continue;
+        if (top + 2 > 512) return ret;
+        const bool right_first = d[bvh.axis[ni]] < 0.f;
+        stack[top++] = right_first ? n.left : n.right;
+        stack[top++] = right_first ? n.right : n.left;
     }
     return ret;
 }
@@ -956,6 +1087,8 @@ extern "C" {
 
 int or_abi_version(void) { return 1; }
 
+void or_set_walk(int ordered) { g_walk_ordered = ordered ? 1 : 0; }   // diagnostic, see trace_ray_ordered
+
 int or_sizeof(int which) {
     switch (which) {
         case 0: return (int)sizeof(Material);
@@ -1100,12 +1233,10 @@ int or_build_bvh(const void* objs, int n, float* out_box, int32_t* out_link, int
 // [6][n_rows*W] (in/out), accum is [n_rows*W][4] rgb-sum + pass count (in/out when
 // accumulate != 0).  stats5 (optional) receives segments, node visits, primitive tests,
 // hits, misses.  Returns 0 on success.
-int or_render(const void* objs, int n_objs, const void* camera, const uint8_t* env_rgba, int env_w, int env_h,
-              int env_valid_cols, const int32_t* rows, int n_rows, int spp, int max_depth, uint32_t* rng_planar,
-              float* accum, float* normal_out, float* depth_out, uint64_t* stats5, int accumulate, int nthreads) {
-    if (max_depth < 0 || max_depth > (int)MAX_RECURSION_DEPTH_SET) return -1;
-    Bvh bvh;
-    build_bvh(bvh, reinterpret_cast<const Object*>(objs), n_objs);
+static int render_with(Bvh& bvh, const void* camera, const uint8_t* env_rgba, int env_w, int env_h,
+                       int env_valid_cols, const int32_t* rows, int n_rows, int spp, int max_depth,
+                       uint32_t* rng_planar, float* accum, float* normal_out, float* depth_out, uint64_t* stats5,
+                       int accumulate, int nthreads) {
     RenderJob J;
     J.bvh = &bvh;
     J.env = Env{env_rgba, env_w, env_h, env_valid_cols};
@@ -1125,6 +1256,57 @@ int or_render(const void* objs, int n_objs, const void* camera, const uint8_t* e
         stats5[0] = s.segments; stats5[1] = s.nodes; stats5[2] = s.prims; stats5[3] = s.hits; stats5[4] = s.misses;
     }
     return 0;
+}
+
+int or_render(const void* objs, int n_objs, const void* camera, const uint8_t* env_rgba, int env_w, int env_h,
+              int env_valid_cols, const int32_t* rows, int n_rows, int spp, int max_depth, uint32_t* rng_planar,
+              float* accum, float* normal_out, float* depth_out, uint64_t* stats5, int accumulate, int nthreads) {
+    if (max_depth < 0 || max_depth > (int)MAX_RECURSION_DEPTH_SET) return -1;
+    Bvh bvh;
+    build_bvh(bvh, reinterpret_cast<const Object*>(objs), n_objs);
+    return render_with(bvh, camera, env_rgba, env_w, env_h, env_valid_cols, rows, n_rows, spp, max_depth, rng_planar,
+                       accum, normal_out, depth_out, stats5, accumulate, nthreads);
+}
+
+// Same as or_render, on a BVH built from `objs` and then edited by SceneBVH::UpdateObject
+// (bvh.cu:122-157): edit k replaces object edit_idx[k] by edit_objs[k], then refits the
+// leaf's box and every ancestor's box (MIN/MAX of its two children) up to the root.  The
+// topology (and so the traversal order) stays the one of the original build.
+int or_render_edited(const void* objs, int n_objs, const int32_t* edit_idx, const void* edit_objs, int n_edits,
+                     const void* camera, const uint8_t* env_rgba, int env_w, int env_h, int env_valid_cols,
+                     const int32_t* rows, int n_rows, int spp, int max_depth, uint32_t* rng_planar, float* accum,
+                     uint64_t* stats5, int nthreads) {
+    if (max_depth < 0 || max_depth > (int)MAX_RECURSION_DEPTH_SET) return -1;
+    std::vector<Object> cur(reinterpret_cast<const Object*>(objs), reinterpret_cast<const Object*>(objs) + n_objs);
+    Bvh bvh;
+    build_bvh(bvh, cur.data(), n_objs);
+    std::vector<int> parent(bvh.nodes.size(), -1), leaf_of(n_objs, -1);
+    for (size_t i = 0; i < bvh.nodes.size(); ++i) {
+        const Node& n = bvh.nodes[i];
+        if (n.is_object) leaf_of[n.obj] = (int)i;
+        else { parent[n.left] = (int)i; parent[n.right] = (int)i; }
+    }
+    const Object* E = reinterpret_cast<const Object*>(edit_objs);
+    for (int k = 0; k < n_edits; ++k) {
+        int o = edit_idx[k];
+        if (o < 0 || o >= n_objs) return -2;
+        cur[o] = E[k];
+        for (int ni = leaf_of[o]; ni != -1; ni = parent[ni]) {      // UpdateSceneBVH (bvh.cu:122-141)
+            Node& n = bvh.nodes[ni];
+            if (n.is_object) {
+                n.bmax = aabb_max(cur[n.obj]);
+                n.bmin = aabb_min(cur[n.obj]);
+            } else {
+                const Node& L = bvh.nodes[n.left];
+                const Node& R = bvh.nodes[n.right];
+                n.bmax = mk(MAX_(L.bmax.x, R.bmax.x), MAX_(L.bmax.y, R.bmax.y), MAX_(L.bmax.z, R.bmax.z));
+                n.bmin = mk(MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z));
+            }
+        }
+    }
+    build_walk_tree(bvh);   // diagnostic ordered walk: splice the refit tree
+    return render_with(bvh, camera, env_rgba, env_w, env_h, env_valid_cols, rows, n_rows, spp, max_depth, rng_planar,
+                       accum, nullptr, nullptr, stats5, 0, nthreads);
 }
 
 // Denoising + Mix (path_tracer.cu:177-254) for a full W x H frame.  radiance = accum rgb /

@@ -85,13 +85,30 @@ def _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, rows=None, seed=1234
     gpu.set_frame(W, H, rows)
     gpu.init_rng(seed)
     gpu.reset_stats()
-    gpu.render(cam, spp, depth, aux=aux, stats=True, sync=True, path=path)
+    gpu.render(cam, spp, depth, aux=aux, stats=True, sync=True, **_kw(path))
     g_acc, g_rng, g_st = gpu.read_accum(), gpu.read_rng(), gpu.stats()
     g_aux = gpu.read_aux() if aux else None
     rng = oracle_mod.init_rng(seed, W, rows, threads=8)
     o_acc, o_st, o_n, o_d = oracle_mod.render(objs, cam, sky if env else None, rows, spp, depth, rng,
                                              want_aux=aux, threads=8)
+    if _kw(path)["ordered"]:
+        # node/prim counts of the ordered walk come from the oracle's diagnostic restatement of
+        # that walk; its image must equal the reference walk's too
+        rng2 = oracle_mod.init_rng(seed, W, rows, threads=8)
+        oracle_mod.set_walk(True)
+        try:
+            w_acc, w_st, _, _ = oracle_mod.render(objs, cam, sky if env else None, rows, spp, depth, rng2, threads=8)
+        finally:
+            oracle_mod.set_walk(False)
+        np.testing.assert_array_equal(w_acc.view(np.uint32), o_acc.view(np.uint32))
+        np.testing.assert_array_equal(rng2, rng)
+        o_st = dict(o_st, walk=w_st)
     return (g_acc, g_rng, g_st, g_aux), (o_acc, rng, o_st, (o_n, o_d))
+
+
+def _kw(path):
+    base, _, mode = path.partition(":")
+    return dict(path=base, ordered=(mode == "ordered"))
 
 
 CASES = [
@@ -104,7 +121,19 @@ CASES = [
 ]
 
 
-PATHS = ["megakernel", "wavefront"]
+# "<path>:ordered" = the near-first octant walk (CPT_TRAVERSAL_ORDERED): same closest hits,
+# so the same images, RNG end states and segment/hit/miss counts; its node/prim counts are its
+# own and equal the oracle's diagnostic restatement of the ordered walk (oracle.set_walk).
+PATHS = ["megakernel", "wavefront", "megakernel:ordered", "wavefront:ordered"]
+
+
+def _check_stats(gs, os_, path):
+    if path.endswith(":ordered"):
+        for k in ("segments", "hits", "misses"):
+            assert gs[k] == os_[k], k
+        assert gs == os_["walk"]
+    else:
+        assert gs == os_
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -113,9 +142,28 @@ def test_render_bitexact(gpu, oracle_mod, sky, name, W, H, spp, depth, path):
     objs = scenes.SCENES[name]()
     (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, path=path)
     np.testing.assert_array_equal(gr, orng)
-    assert gs == os_
+    _check_stats(gs, os_, path)
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
     assert np.isfinite(ga).all() and (ga[:, 3] == spp).all()
+
+
+@pytest.mark.parametrize("path", PATHS)
+def test_exact_ties_between_primitives(gpu, oracle_mod, sky, path):
+    """Every primitive duplicated with a different material (and the copies shuffled through
+    the object list): all hits are exact ties between two primitives, and the reference keeps
+    the one its right-first DFS tests first (strict `temp < tmax`, object.cu).  The ordered
+    walk must pick the same one through its reference-rank tie rule."""
+    objs = scenes.scene_s1000(n=60)
+    twins = objs.copy()
+    mats = twins["material"].copy()
+    twins["material"] = np.roll(mats, 7)
+    both = np.concatenate([objs, twins]).astype(types.OBJECT_DTYPE)   # concatenate drops the padded layout
+    perm = np.random.default_rng(5).permutation(both.size)
+    both = np.ascontiguousarray(both[perm])
+    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, both, 64, 40, 2, 8, path=path)
+    np.testing.assert_array_equal(gr, orng)
+    _check_stats(gs, os_, path)
+    np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -149,7 +197,7 @@ def test_tiny_depths(gpu, oracle_mod, sky, depth, path):
     (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, objs, 32, 16, 3, depth, path=path)
     np.testing.assert_array_equal(gr, orng)
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
-    assert gs == os_
+    _check_stats(gs, os_, path)
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -158,18 +206,20 @@ def test_empty_scene_and_no_env(gpu, oracle_mod, sky, path):
     (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, empty, 32, 16, 2, 8, path=path)
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
     np.testing.assert_array_equal(gr, orng)
-    assert gs["hits"] == 0 and gs == os_
+    assert gs["hits"] == 0
+    _check_stats(gs, os_, path)
     (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, scenes.scene_s3(), 32, 16, 2, 8, env=False)
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
 
 
-def test_single_object_and_cylinders(gpu, oracle_mod, sky):
+@pytest.mark.parametrize("path", ["megakernel", "megakernel:ordered"])
+def test_single_object_and_cylinders(gpu, oracle_mod, sky, path):
     objs = scenes.scene_s1000(n=3)
     for sl in (slice(0, 1), slice(1, 2), slice(0, 4)):
         o = np.ascontiguousarray(objs[sl])
-        (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, o, 40, 24, 2, 8)
+        (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, o, 40, 24, 2, 8, path=path)
         np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
-        assert gs == os_
+        _check_stats(gs, os_, path)
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -181,10 +231,11 @@ def test_accumulate_and_spp0(gpu, oracle_mod, sky, path):
     gpu.set_env(sky)
     gpu.set_frame(W, H)
     gpu.init_rng(99)
-    gpu.render(cam, 0, 4, sync=True, path=path)
+    kw = _kw(path)
+    gpu.render(cam, 0, 4, sync=True, **kw)
     assert (gpu.read_accum() == 0).all()
-    gpu.render(cam, 2, 4, sync=True, path=path)
-    gpu.render(cam, 3, 4, accumulate=True, sync=True, path=path)
+    gpu.render(cam, 2, 4, sync=True, **kw)
+    gpu.render(cam, 3, 4, accumulate=True, sync=True, **kw)
     a = gpu.read_accum()
     rng = oracle_mod.init_rng(99, W, np.arange(H, dtype=np.int32))
     acc, _, _, _ = oracle_mod.render(objs, cam, sky, np.arange(H, dtype=np.int32), 2, 4, rng)
@@ -206,3 +257,72 @@ def test_invalid_arguments(gpu):
         gpu.render(camera_get_copy(scenes.camera_for(8, 16)), 1, 4)
     with pytest.raises(CptError):
         gpu.set_frame(16, 16, [16])
+
+
+@pytest.mark.parametrize("path", ["megakernel", "wavefront", "megakernel:ordered"])
+def test_update_object_refit(gpu, oracle_mod, sky, path):
+    """SceneBVH::UpdateObject (bvh.cu:122-157): the leaf takes the new object, its ancestors'
+    boxes are refit and the topology is kept.  Moves a sphere far out (boxes grow), shrinks a
+    cylinder, swaps a material; the render after the edits matches the oracle's refit BVH."""
+    objs = scenes.scene_s1000(n=40)
+    W, H, spp, depth = 48, 32, 2, 8
+    cam = camera_get_copy(scenes.camera_for(W, H))
+    edits = []
+    sph = int(np.flatnonzero(objs["type"] == 0)[3])
+    o = objs[sph].copy()
+    o["center"][1] += 25.0
+    o["center"][0] -= 40.0
+    edits.append((sph, o))
+    cyl = np.flatnonzero(objs["type"] == 2)
+    if cyl.size:
+        o = objs[int(cyl[0])].copy()
+        o["radius"] *= 0.5
+        o["height"] *= 1.5
+        edits.append((int(cyl[0]), o))
+    o = objs[5].copy()
+    o["material"] = objs[7]["material"]
+    edits.append((5, o))
+    gpu.set_scene(objs)
+    for i, ob in edits:
+        gpu.update_object(i, ob)
+    gpu.set_env(sky)
+    gpu.set_frame(W, H)
+    gpu.init_rng(11)
+    gpu.reset_stats()
+    gpu.render(cam, spp, depth, stats=True, sync=True, **_kw(path))
+    ga, gs = gpu.read_accum(), gpu.stats()
+    rows = np.arange(H, dtype=np.int32)
+    rng = oracle_mod.init_rng(11, W, rows, threads=8)
+    oa, os_ = oracle_mod.render_edited(objs, edits, cam, sky, rows, spp, depth, rng, threads=8)
+    if _kw(path)["ordered"]:
+        oracle_mod.set_walk(True)
+        try:
+            _, w_st = oracle_mod.render_edited(objs, edits, cam, sky, rows, spp, depth,
+                                               oracle_mod.init_rng(11, W, rows, threads=8), threads=8)
+        finally:
+            oracle_mod.set_walk(False)
+        os_ = dict(os_, walk=w_st)
+    np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
+    np.testing.assert_array_equal(gpu.read_rng(), rng)
+    _check_stats(gs, os_, path)
+
+
+@pytest.mark.parametrize("path", ["megakernel:ordered", "wavefront:ordered"])
+def test_ordered_walk_platform_only_and_multiple_platforms(gpu, oracle_mod, sky, path):
+    """Walk-tree edge cases: a scene that is only a platform (no tree left after splicing),
+    and several platforms (floor, a ceiling plane, a duplicate floor) mixed with primitives."""
+    objs = scenes.scene_s1000(n=20)
+    floor = objs[objs["type"] == 1][0].copy()
+    only = np.ascontiguousarray(np.array([floor], dtype=types.OBJECT_DTYPE))
+    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, only, 32, 16, 2, 8, path=path)
+    np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
+    _check_stats(gs, os_, path)
+    ceil = floor.copy()
+    ceil["y_pos"] = 60.0
+    twin = floor.copy()
+    twin["material"] = objs[3]["material"]
+    many = np.concatenate([objs, np.array([ceil, twin], dtype=types.OBJECT_DTYPE)]).astype(types.OBJECT_DTYPE)
+    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, many, 48, 32, 2, 8, path=path)
+    np.testing.assert_array_equal(gr, orng)
+    np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
+    _check_stats(gs, os_, path)
