@@ -30,6 +30,7 @@ PROTOTYPES = {
     "cpt_scene_bvh_export": (_I, [_P, _P, _P, _I, _P]),
     "cpt_bvh_build_host": (_I, [_P, _I, _P, _P, _I, _P]),
     "cpt_set_env_texture": (_I, [_P, _P, _I, _I, _I]),
+    "cpt_bind_texture": (_I, [_P, _U64, _P, _I, _I, _I, _I, _I]),
     "cpt_set_frame": (_I, [_P, _I, _I, _P, _I]),
     "cpt_init_rng": (_I, [_P, _U64]),
     "cpt_read_rng": (_I, [_P, _P]),

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <set>
@@ -251,6 +252,15 @@ static bool load_ppm(const std::string& path, PocaTextureData& t) {
     return true;
 }
 
+static int address_mode_of(PocaAddressMode m) {
+    switch (m) {
+        case PocaAddressMode::Wrap: return CPT_ADDRESS_WRAP;
+        case PocaAddressMode::Clamp: return CPT_ADDRESS_CLAMP;
+        case PocaAddressMode::Border: return CPT_ADDRESS_BORDER;
+        default: return CPT_ADDRESS_MIRROR;
+    }
+}
+
 PocaTexture PocaTextureUtils::AddTexByFile(std::string file_path, PocaAddressMode addr_mode, PocaFilterMode filter_mode) {
     PocaTextureData t;
     t.addr = addr_mode;
@@ -362,6 +372,19 @@ bool PathTracer::SyncScene() {
             std::lock_guard<std::mutex> lk(bvh_mutex);
             objs = bvh_snapshot;
         }
+        // material textures (Material::tex_ holds an AddTexByFile handle, material.h:21-25)
+        std::vector<uint64_t> bound;
+        for (const cpt_object& o : objs) {
+            if (!o.material.have_tex) continue;
+            const uint64_t h = o.material.u.tex;
+            if (std::find(bound.begin(), bound.end(), h) != bound.end()) continue;
+            const PocaTextureData* t = PocaTextureUtils::Get(h);
+            if (!t) { err_ = "textured material uses an unknown PocaTexture handle"; return false; }
+            if (cpt_bind_texture(ctx_, h, t->rgba.data(), t->width, t->height, t->valid_cols, address_mode_of(t->addr),
+                                 t->filter == PocaFilterMode::Point ? CPT_FILTER_POINT : CPT_FILTER_LINEAR) != CPT_OK)
+                return Fail("cpt_bind_texture");
+            bound.push_back(h);
+        }
         if (cpt_set_scene(ctx_, objs.empty() ? nullptr : objs.data(), (int)objs.size()) != CPT_OK)
             return Fail("cpt_set_scene");
         scene_build_ = build;
@@ -406,7 +429,8 @@ bool PathTracer::EnsureFrame(const MotionalCamera& cam) {
 
 bool PathTracer::RenderPass(MotionalCamera& cam, int spp, bool accumulate) {
     if (!SyncScene() || !EnsureFrame(cam)) return false;
-    uint32_t flags = CPT_RENDER_AUX | (accumulate ? CPT_RENDER_ACCUMULATE : 0u) | CPT_RENDER_SYNC;
+    uint32_t flags = CPT_RENDER_AUX | (accumulate ? CPT_RENDER_ACCUMULATE : 0u) | CPT_RENDER_SYNC |
+                     (ordered_walk_ ? CPT_TRAVERSAL_ORDERED : 0u);
     if (cpt_render(ctx_, reinterpret_cast<const cpt_camera*>(&cam), spp, (int)max_recursion_depth_, flags) != CPT_OK)
         return Fail("cpt_render");
     return true;

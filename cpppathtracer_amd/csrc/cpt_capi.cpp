@@ -28,6 +28,7 @@ namespace {
 
 using cpt::Mat;
 using cpt::Node;
+using cpt::TexDesc;
 
 std::string g_create_error;
 
@@ -290,12 +291,21 @@ struct cpt_ctx {
     std::vector<int> pos_of_node;      // BNode -> position in the reference order
     int n_bvh = 0;                     // nodes of the reference order
     int n_walk = 0;                    // nodes of each octant order (walk tree + unbounded leaves)
-    std::vector<Mat> mats_h;           // deduplicated materials
+    std::vector<Mat> mats_h;           // deduplicated materials (host-staged, see Mat)
+    std::vector<int> mat_have_tex;     // per material slot: textured?
+    std::vector<uint64_t> mat_tex;     // per material slot: texture handle (textured slots)
     std::vector<int> mat_of_obj;       // object index -> material index
     Node* d_nodes = nullptr;
     Mat* d_mats = nullptr;
     size_t cap_nodes = 0, cap_mats = 0;
     bool scene_set = false;
+
+    // material textures (cpt_bind_texture)
+    struct Texture { uint64_t handle; uint32_t* d_texels; int w, h, cols, addr, filter; };
+    std::vector<Texture> textures;
+    TexDesc* d_texdescs = nullptr;
+    int32_t* d_tex_of_mat = nullptr;
+    size_t cap_texdescs = 0, cap_tex_of_mat = 0;
 
     // environment
     uint32_t* d_env = nullptr;
@@ -382,24 +392,31 @@ void free_frame(cpt_ctx* c) {
     c->frame_set = c->rng_set = false;
 }
 
+// Host staging of a Mat (cpt_device.hpp): att = kd_ (the union's bits: the handle's for a
+// textured material), rad.x = emit_intensity_; k_prepare_materials completes it.
 Mat to_mat(const cpt_material& m) {
     Mat g;
-    g.kd_x = m.u.kd.x; g.kd_y = m.u.kd.y; g.kd_z = m.u.kd.z;
-    g.emit = m.emit_intensity;
-    g.ior = m.refractive_index;
-    g.smoothness = m.smoothness;
-    g.reflectivity = m.reflectivity;
+    std::memset(&g, 0, sizeof(g));
+    g.att_x = m.u.kd.x; g.att_y = m.u.kd.y; g.att_z = m.u.kd.z;
     g.type = m.type;
-    g.inv_alpha = 0.0;   // filled on the device (k_prepare_materials)
-    g.pad_ = 0.0;
+    g.rad_x = m.emit_intensity;
+    g.ior = m.refractive_index;
+    g.reflectivity = m.reflectivity;
+    g.smoothness = m.smoothness;
+    g.inv_alpha = 0.0;
     return g;
 }
 
 int material_slot(cpt_ctx* c, const cpt_material& m) {
     Mat g = to_mat(m);
+    const int tex = m.have_tex ? 1 : 0;
     for (size_t i = 0; i < c->mats_h.size(); ++i)
-        if (std::memcmp(&c->mats_h[i], &g, sizeof(Mat)) == 0) return (int)i;
+        if (std::memcmp(&c->mats_h[i], &g, sizeof(Mat)) == 0 && c->mat_have_tex[i] == tex &&
+            (!tex || c->mat_tex[i] == m.u.tex))
+            return (int)i;
     c->mats_h.push_back(g);
+    c->mat_have_tex.push_back(tex);
+    c->mat_tex.push_back(tex ? m.u.tex : 0);
     return (int)c->mats_h.size() - 1;
 }
 
@@ -465,8 +482,35 @@ int upload_scene(cpt_ctx* c) {
     if (!c->lin.empty())
         HIP_TRY(c, hipMemcpyAsync(c->d_nodes, c->lin.data(), c->lin.size() * sizeof(Node), hipMemcpyHostToDevice, s));
     if (!c->mats_h.empty()) {
+        // textured materials: resolve their handles against the bound textures
+        std::vector<int32_t> tex_of_mat(c->mats_h.size(), -1);
+        bool any = false;
+        for (size_t i = 0; i < c->mats_h.size(); ++i) {
+            if (!c->mat_have_tex[i]) continue;
+            for (size_t t = 0; t < c->textures.size(); ++t)
+                if (c->textures[t].handle == c->mat_tex[i]) tex_of_mat[i] = (int32_t)t;
+            if (tex_of_mat[i] < 0)
+                return fail(c, CPT_ERR_INVALID_ARG, "textured material uses handle %llu, which is not bound (cpt_bind_texture)",
+                            (unsigned long long)c->mat_tex[i]);
+            any = true;
+        }
+        if (any) {
+            std::vector<TexDesc> descs(c->textures.size());
+            for (size_t t = 0; t < descs.size(); ++t) {
+                const auto& x = c->textures[t];
+                descs[t] = TexDesc{x.d_texels, x.w, x.h, x.cols, x.addr, x.filter, 0};
+            }
+            if ((rc = ensure(c, &c->d_texdescs, &c->cap_texdescs, descs.size())) != CPT_OK) return rc;
+            if ((rc = ensure(c, &c->d_tex_of_mat, &c->cap_tex_of_mat, tex_of_mat.size())) != CPT_OK) return rc;
+            HIP_TRY(c, hipMemcpyAsync(c->d_texdescs, descs.data(), descs.size() * sizeof(TexDesc), hipMemcpyHostToDevice, s));
+            HIP_TRY(c, hipMemcpyAsync(c->d_tex_of_mat, tex_of_mat.data(), tex_of_mat.size() * sizeof(int32_t),
+                                      hipMemcpyHostToDevice, s));
+            // the staging vectors must outlive the async copies
+            HIP_TRY(c, hipStreamSynchronize(s));
+        }
         HIP_TRY(c, hipMemcpyAsync(c->d_mats, c->mats_h.data(), c->mats_h.size() * sizeof(Mat), hipMemcpyHostToDevice, s));
-        HIP_TRY(c, cpt::launch_prepare_materials(c->d_mats, (int)c->mats_h.size(), s));
+        HIP_TRY(c, cpt::launch_prepare_materials(c->d_mats, any ? c->d_tex_of_mat : nullptr, any ? c->d_texdescs : nullptr,
+                                                 (int)c->mats_h.size(), s));
     }
     HIP_TRY(c, hipStreamSynchronize(s));
     c->scene_set = true;
@@ -540,6 +584,9 @@ int cpt_destroy(cpt_ctx* c) {
     (void)hipFree(c->d_nodes);
     (void)hipFree(c->d_mats);
     (void)hipFree(c->d_env);
+    for (auto& t : c->textures) (void)hipFree(t.d_texels);
+    (void)hipFree(c->d_texdescs);
+    (void)hipFree(c->d_tex_of_mat);
     (void)hipFree(c->d_jumps);
     (void)hipFree(c->d_stats);
     (void)hipFree(c->d_work);
@@ -592,15 +639,14 @@ int cpt_camera_get_copy(cpt_camera* cam) {
 
 int cpt_set_scene(cpt_ctx* c, const cpt_object* objs, int n) {
     if (!c || n < 0 || (n > 0 && !objs)) return c ? fail(c, CPT_ERR_INVALID_ARG, "cpt_set_scene: bad arguments") : CPT_ERR_INVALID_ARG;
+    c->scene_set = false;   // until the new scene is uploaded
     try {
-        for (int i = 0; i < n; ++i) {
-            if (objs[i].material.have_tex)
-                return fail(c, CPT_ERR_UNSUPPORTED, "cpt_set_scene: object %d has a textured material (not supported yet)", i);
-        }
         c->objs.assign(objs, objs + n);
         build_host_bvh(c->bvh, c->objs);
         // Objects carry their Material by value (bvh.cu:43); identical materials share one slot.
         c->mats_h.clear();
+        c->mat_have_tex.clear();
+        c->mat_tex.clear();
         c->mat_of_obj.assign(n, 0);
         for (int i = 0; i < n; ++i) c->mat_of_obj[i] = material_slot(c, c->objs[i].material);
         linearise_all(c);
@@ -616,7 +662,6 @@ int cpt_update_object(cpt_ctx* c, int index, const cpt_object* obj) {
     if (!c || !obj) return CPT_ERR_INVALID_ARG;
     if (!c->scene_set || index < 0 || index >= (int)c->objs.size())
         return fail(c, CPT_ERR_INVALID_ARG, "cpt_update_object: index %d out of range", index);
-    if (obj->material.have_tex) return fail(c, CPT_ERR_UNSUPPORTED, "cpt_update_object: textured material");
     c->objs[index] = *obj;
     c->mat_of_obj[index] = material_slot(c, obj->material);
     int ni = c->bvh.leaf_of_object[index];
@@ -693,6 +738,30 @@ int cpt_set_env_texture(cpt_ctx* c, const uint8_t* rgba, int logical_width, int 
     c->env_h = height;
     c->env_cols = valid_cols;
     return CPT_OK;
+}
+
+int cpt_bind_texture(cpt_ctx* c, uint64_t handle, const uint8_t* rgba, int logical_width, int height, int valid_cols,
+                     int address_mode, int filter_mode) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    if (logical_width <= 0 || height <= 0 || valid_cols < 0 || valid_cols > logical_width || (valid_cols > 0 && !rgba) ||
+        address_mode < CPT_ADDRESS_WRAP || address_mode > CPT_ADDRESS_BORDER || filter_mode < CPT_FILTER_POINT ||
+        filter_mode > CPT_FILTER_LINEAR)
+        return fail(c, CPT_ERR_INVALID_ARG, "cpt_bind_texture: bad geometry %dx%d cols %d or mode %d/%d", logical_width,
+                    height, valid_cols, address_mode, filter_mode);
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t n = (size_t)valid_cols * height;
+    uint32_t* d = nullptr;
+    HIP_TRY(c, hipMalloc((void**)&d, std::max<size_t>(1, n) * 4));
+    if (n) {
+        hipError_t e = hipMemcpy(d, rgba, n * 4, hipMemcpyHostToDevice);
+        if (e != hipSuccess) { (void)hipFree(d); return fail(c, CPT_ERR_HIP, "cpt_bind_texture: %s", hipGetErrorString(e)); }
+    }
+    cpt_ctx::Texture t{handle, d, logical_width, height, valid_cols, address_mode, filter_mode};
+    bool replaced = false;
+    for (auto& x : c->textures)
+        if (x.handle == handle) { (void)hipFree(x.d_texels); x = t; replaced = true; }
+    if (!replaced) c->textures.push_back(t);
+    return c->scene_set ? upload_scene(c) : CPT_OK;   // re-prepare the materials
 }
 
 int cpt_set_frame(cpt_ctx* c, int width, int height, const int32_t* rows, int n_rows) {

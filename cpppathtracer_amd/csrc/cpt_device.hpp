@@ -292,15 +292,29 @@ struct __attribute__((aligned(16))) Node {
 };
 static_assert(sizeof(Node) == 32, "Node is 32 B");
 
-// Material, 48 B: Material (material.h:17-35) + per-material constants prepared once on the
-// device (alpha = powf(1000, smoothness) and 1.0/(double)alpha, material.cu:43,69,103).
+// Material, 48 B: Material (material.h:17-35) reduced to what the shaders read, prepared once
+// per material on the device (k_prepare_materials):
+//   att   = GetKd(0, 0) (material.cu:11-18): kd_, or a textured material's (0, 0) sample
+//   rad   = emit_intensity_ * kd_ (material.cu:36,62,97,141); in a textured material kd_
+//           aliases tex_, so these are the handle's bits, as in the reference's union
+//   inv_alpha = 1.0 / (double)powf(1000, smoothness_) (material.cu:43,69,103)
+// The host stages {att = kd_ bits, rad.x = emit_intensity_} and the kernel completes it.
 struct __attribute__((aligned(16))) Mat {
-    float kd_x, kd_y, kd_z, emit;
-    float ior, smoothness, reflectivity;
+    float att_x, att_y, att_z;
     int32_t type;
+    float rad_x, rad_y, rad_z;
+    float ior;
+    float reflectivity, smoothness;
     double inv_alpha;
-    double pad_;
 };
+static_assert(sizeof(Mat) == 48, "Mat is 48 B");
+
+// A material texture bound with cpt_bind_texture: packed RGBA8 words, `cols` valid columns.
+struct TexDesc {
+    const uint32_t* texels;
+    int32_t w, h, cols, addr, filter, pad_;
+};
+static_assert(sizeof(TexDesc) == 32, "TexDesc is 32 B");
 
 struct Ray { v3 o, d; float tmin, tmax; };
 

@@ -51,7 +51,8 @@ struct WfState {
 hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t stream);
 hipError_t launch_wavefront(const KParams& p, WfState& w, bool stats, bool aux, hipStream_t stream, int* launches);
 hipError_t wavefront_build_ident(const KParams& p, WfState& w, hipStream_t stream);
-hipError_t launch_prepare_materials(Mat* mats, int n, hipStream_t stream);
+hipError_t launch_prepare_materials(Mat* mats, const int32_t* tex_of_mat, const TexDesc* texs, int n,
+                                    hipStream_t stream);
 hipError_t launch_init_rng(const uint32_t* jumps, const uint32_t seed_state[6], int width, const int32_t* rows,
                            int n_rows, uint32_t* scratch_w, uint32_t* scratch_mats, uint32_t* rng, hipStream_t stream);
 hipError_t launch_math_batch(int op, const float* a, const float* b, float* out, size_t n, hipStream_t stream);

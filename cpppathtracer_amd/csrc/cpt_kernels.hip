@@ -1,6 +1,6 @@
 // cpt_kernels.hip — HIP kernels of the MI355X integrator (gfx950, wave64).
 //
-//   k_prepare_materials  per-material constants (alpha, 1/alpha) — material.cu:43,69,103
+//   k_prepare_materials  per-material constants: GetKd(0,0), emission, 1/alpha — material.cu
 //   k_rng_*              InitCuRand (path_tracer.cu:36-42) as three GF(2) kernels
 //   k_megakernel         SamplePixel (path_tracer.cu:124-175), all spp passes per launch,
 //                        per-lane path regeneration, state in registers
@@ -276,11 +276,24 @@ __global__ void k_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned l
 // Per-material constants: alpha = pow(1000.0f, s) (float pow), 1.0 / alpha in double
 // (material.cu:43-45, 69-70, 103-104).
 // ======================================================================================
-__global__ void k_prepare_materials(Mat* mats, int n) {
+// Completes the host-staged materials (cpt_device.hpp Mat): emission colour, GetKd(0, 0) of
+// textured materials (tex_of_mat[i] >= 0: index into texs), 1/alpha.
+__global__ void k_prepare_materials(Mat* mats, const int32_t* tex_of_mat, const TexDesc* texs, int n) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    float alpha = dm::powf_(1000.0f, mats[i].smoothness);
-    mats[i].inv_alpha = 1.0 / (double)alpha;
+    Mat m = mats[i];
+    const v3 kd = mk(m.att_x, m.att_y, m.att_z);   // staged: kd_ (the union's bits)
+    const v3 rad = m.rad_x * kd;                    // staged: rad_x = emit_intensity_
+    m.rad_x = rad.x; m.rad_y = rad.y; m.rad_z = rad.z;
+    const int t = tex_of_mat ? tex_of_mat[i] : -1;
+    if (t >= 0) {
+        const TexDesc d = texs[t];
+        const v3 c = tex_fetch_dyn(TexView{d.texels, d.w, d.h, d.cols}, d.addr, d.filter, 0.0f, 0.0f);
+        m.att_x = c.x; m.att_y = c.y; m.att_z = c.z;
+    }
+    float alpha = dm::powf_(1000.0f, m.smoothness);
+    m.inv_alpha = 1.0 / (double)alpha;
+    mats[i] = m;
 }
 
 // ======================================================================================
@@ -517,9 +530,10 @@ hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t
     return launch_mk<false, false, false>(p, stream);
 }
 
-hipError_t launch_prepare_materials(Mat* mats, int n, hipStream_t stream) {
+hipError_t launch_prepare_materials(Mat* mats, const int32_t* tex_of_mat, const TexDesc* texs, int n,
+                                    hipStream_t stream) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_prepare_materials, dim3((n + 63) / 64), dim3(64), 0, stream, mats, n);
+    hipLaunchKernelGGL(k_prepare_materials, dim3((n + 63) / 64), dim3(64), 0, stream, mats, tex_of_mat, texs, n);
     return hipGetLastError();
 }
 

@@ -27,33 +27,72 @@ __device__ __forceinline__ int mirror_index(int i, int n) {
     return m;
 }
 
-__device__ __forceinline__ void texel(const KParams& p, int i, int j, float out[3]) {
-    int x = mirror_index(i, p.env_w), y = mirror_index(j, p.env_h);
-    if (x >= p.env_cols) { out[0] = out[1] = out[2] = 0.0f; return; }
-    uint32_t t = p.env[(size_t)y * p.env_cols + x];
-    out[0] = (float)(t & 0xffu) / 255.0f;
-    out[1] = (float)((t >> 8) & 0xffu) / 255.0f;
-    out[2] = (float)((t >> 16) & 0xffu) / 255.0f;
+// Texel index after addressing (cudaTextureAddressMode values, cpt.h); -1 = outside the
+// texture under Border (border colour 0).
+template <int ADDR>
+__device__ __forceinline__ int address_index(int i, int n) {
+    if (ADDR == 0) { int m = i % n; return m < 0 ? m + n : m; }         // wrap
+    if (ADDR == 1) return i < 0 ? 0 : (i >= n ? n - 1 : i);           // clamp
+    if (ADDR == 3) return (i < 0 || i >= n) ? -1 : i;                 // border
+    return mirror_index(i, n);                                        // mirror
 }
 
-__device__ inline v3 tex2d(const KParams& p, float u, float v) {
-    float x = u * (float)p.env_w - 0.5f;
-    float y = v * (float)p.env_h - 0.5f;
-    if (!(x > -1e7f && x < 1e7f && y > -1e7f && y < 1e7f) || p.env_cols <= 0) return mk1(0.0f);
+struct TexView { const uint32_t* texels; int w, h, cols; };
+
+template <int ADDR>
+__device__ __forceinline__ void texel(const TexView& t, int i, int j, float out[3]) {
+    int x = address_index<ADDR>(i, t.w), y = address_index<ADDR>(j, t.h);
+    if (x < 0 || y < 0 || x >= t.cols) { out[0] = out[1] = out[2] = 0.0f; return; }
+    uint32_t v = t.texels[(size_t)y * t.cols + x];
+    out[0] = (float)(v & 0xffu) / 255.0f;
+    out[1] = (float)((v >> 8) & 0xffu) / 255.0f;
+    out[2] = (float)((v >> 16) & 0xffu) / 255.0f;
+}
+
+// tex2D<float4> at normalized (u, v), rgb (textures.cu:68-71).  Linear: taps at
+// floor(u*w - 0.5) and +1, weights rounded to 1/256; point: the texel at floor(u*w).
+template <int ADDR, bool LINEAR>
+__device__ inline v3 tex_fetch(const TexView& t, float u, float v) {
+    if (t.cols <= 0) return mk1(0.0f);
+    if (!LINEAR) {
+        float x = u * (float)t.w, y = v * (float)t.h;
+        if (!(x > -1e7f && x < 1e7f && y > -1e7f && y < 1e7f)) return mk1(0.0f);
+        float c[3];
+        texel<ADDR>(t, (int)__builtin_floorf(x), (int)__builtin_floorf(y), c);
+        return mk(c[0], c[1], c[2]);
+    }
+    float x = u * (float)t.w - 0.5f;
+    float y = v * (float)t.h - 0.5f;
+    if (!(x > -1e7f && x < 1e7f && y > -1e7f && y < 1e7f)) return mk1(0.0f);
     float fx = __builtin_floorf(x), fy = __builtin_floorf(y);
     float a = __builtin_floorf((x - fx) * 256.0f + 0.5f) * 0.00390625f;
     float b = __builtin_floorf((y - fy) * 256.0f + 0.5f) * 0.00390625f;
     int i0 = (int)fx, j0 = (int)fy;
     float t00[3], t10[3], t01[3], t11[3];
-    texel(p, i0, j0, t00);
-    texel(p, i0 + 1, j0, t10);
-    texel(p, i0, j0 + 1, t01);
-    texel(p, i0 + 1, j0 + 1, t11);
+    texel<ADDR>(t, i0, j0, t00);
+    texel<ADDR>(t, i0 + 1, j0, t10);
+    texel<ADDR>(t, i0, j0 + 1, t01);
+    texel<ADDR>(t, i0 + 1, j0 + 1, t11);
     float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
     float r[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) r[c] = ((w00 * t00[c] + w10 * t10[c]) + w01 * t01[c]) + w11 * t11[c];
     return mk(r[0], r[1], r[2]);
+}
+
+__device__ inline v3 tex_fetch_dyn(const TexView& t, int addr, int filter, float u, float v) {
+    const bool lin = filter != 0;
+    switch (addr) {
+        case 0: return lin ? tex_fetch<0, true>(t, u, v) : tex_fetch<0, false>(t, u, v);
+        case 1: return lin ? tex_fetch<1, true>(t, u, v) : tex_fetch<1, false>(t, u, v);
+        case 3: return lin ? tex_fetch<3, true>(t, u, v) : tex_fetch<3, false>(t, u, v);
+        default: return lin ? tex_fetch<2, true>(t, u, v) : tex_fetch<2, false>(t, u, v);
+    }
+}
+
+// The sky: AddTexByFile's defaults, mirror + linear (textures.h:9-11).
+__device__ inline v3 tex2d(const KParams& p, float u, float v) {
+    return tex_fetch<2, true>(TexView{p.env, p.env_w, p.env_h, p.env_cols}, u, v);
 }
 
 // ======================================================================================
@@ -462,7 +501,7 @@ __device__ __forceinline__ bool refract(v3 v, v3 n, float ni_over_nt, v3& refrac
 
 // Material::EvalAttenuationAndCreateRay (material.cu:145-163) with the Metal/Mirror swap.
 __device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow& rng, Shade& out) {
-    const v3 kd = mk(m.kd_x, m.kd_y, m.kd_z);
+    const v3 kd = mk(m.att_x, m.att_y, m.att_z);   // GetKd(0, 0)
     const v3 zero = mk(0.0f, 0.0f, 0.0f);
     if (m.type == 1) {
         // MaterialType::Metal -> MirrorHitShader (material.cu:40-64)
@@ -511,7 +550,7 @@ __device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow&
         out.bounce = to_world(local, normal);
         out.attenuation = dot(normal, out.bounce) > 0.0f ? kd : zero;
     }
-    out.radiance = m.emit * kd;
+    out.radiance = mk(m.rad_x, m.rad_y, m.rad_z);   // emit_intensity_ * kd_
 }
 
 // Miss (path_tracer.cu:117-122)

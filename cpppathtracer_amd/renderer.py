@@ -97,6 +97,13 @@ class Renderer:
         rgba = np.ascontiguousarray(env.rgba, dtype=np.uint8)
         self._check(self._L.cpt_set_env_texture(self._ctx, _p(rgba), env.width, env.height, env.valid_cols))
 
+    def bind_texture(self, handle, tex, address_mode=2, filter_mode=1):
+        """Bind texels (texture_io.EnvTexture) to a material texture handle (cpt_bind_texture);
+        defaults = AddTexByFile's mirror + linear."""
+        rgba = np.ascontiguousarray(tex.rgba, dtype=np.uint8)
+        self._check(self._L.cpt_bind_texture(self._ctx, handle, _p(rgba), tex.width, tex.height, tex.valid_cols,
+                                             address_mode, filter_mode))
+
     def set_frame(self, width, height, rows=None):
         if rows is None:
             self._check(self._L.cpt_set_frame(self._ctx, width, height, None, 0))

@@ -73,6 +73,26 @@ def scene_s4():
     return objs
 
 
+def scene_s4_textured(handles=(1, 2, 3)):
+    """scene_s4 with textured materials (§8(f) rank 4): the floor (Diffuse), the Metal and the
+    Glass sphere take their kd from the textures bound to `handles`."""
+    from .types import set_material_texture
+    objs = scene_s4()
+    for i, h in zip((0, 2, 1), handles):
+        m = objs[i]["material"].copy()
+        objs[i]["material"] = set_material_texture(m, h)
+    return objs
+
+
+def synthetic_texture(seed, width=16, height=8, full=False):
+    """A random RGBA8 texture; `full` keeps all columns, else the AddTexByFile upload quirk
+    (width/4 valid columns, textures.cu:32-33)."""
+    from .texture_io import EnvTexture
+    rng = np.random.default_rng(seed)
+    cols = width if full else width // 4
+    return EnvTexture(rng.integers(0, 256, size=(height, cols, 4), dtype=np.uint8), width, height)
+
+
 def scene_s1000(seed=20250124, n=1000):
     """Floor + n random spheres / cylinders (video_renderer.cpp:41-117 distributions)."""
     rng = MsvcRand(seed)

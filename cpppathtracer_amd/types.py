@@ -72,6 +72,23 @@ def make_material(mtype=DIFFUSE, kd=(0.0, 0.0, 0.0), refractive_index=0.0, emit_
     return m
 
 
+# cudaTextureAddressMode / cudaTextureFilterMode values (cpt.h CPT_ADDRESS_*, CPT_FILTER_*)
+ADDRESS_WRAP, ADDRESS_CLAMP, ADDRESS_MIRROR, ADDRESS_BORDER = 0, 1, 2, 3
+FILTER_POINT, FILTER_LINEAR = 0, 1
+
+
+def set_material_texture(m, handle):
+    """Make a Material textured (have_tex_ = true, tex_ = handle).  tex_ shares bytes 8..15
+    with kd_ (material.h:21-25), so kd.x/kd.y become the handle's low/high 32 bits as floats
+    (the emission colour the reference computes from kd_); kd.z is left as it was."""
+    m["have_tex"] = 1
+    bits = np.array([handle & 0xFFFFFFFF, (handle >> 32) & 0xFFFFFFFF], dtype=np.uint32).view(np.float32)
+    kd = np.array(m["kd"], dtype=np.float32)
+    kd[0], kd[1] = bits[0], bits[1]
+    m["kd"] = kd
+    return m
+
+
 def make_object(ptype, material, center=(0.0, 0.0, 0.0), radius=0.0, y_pos=0.0, height=0.0):
     o = np.zeros((), dtype=OBJECT_DTYPE)
     o["type"] = ptype

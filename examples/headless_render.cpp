@@ -3,6 +3,10 @@
 //
 //   cpt_headless [--scene s3|s4] [--width W] [--height H] [--spp N] [--depth D] [--seed S]
 //                [--out radiance.bin] [--dispatch K --bgra frame.bin] [--pfm image.pfm]
+//                [--texture file.ppm|file.cptex]
+//
+// --texture makes the floor, the Glass and the Metal sphere of s4 textured materials
+// (Material::have_tex_/tex_, material.h:21-25) sampling that file (AddTexByFile defaults).
 //
 // --out writes the raw accumulator mean as float32 rgb (row-major); --dispatch runs K passes
 // through the asynchronous DispatchRay pipeline (1 spp + denoise + mix per pass, callback on
@@ -56,7 +60,7 @@ void on_frame(uint8_t* data, int width, int height, void* param) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    std::string scene = "s4", out, bgra_out, pfm;
+    std::string scene = "s4", out, bgra_out, pfm, texture;
     int W = 64, H = 36, spp = 2, depth = 8, dispatch = 0;
     unsigned long long seed = 1234;
     for (int i = 1; i + 1 < argc; i += 2) {
@@ -71,6 +75,7 @@ int main(int argc, char** argv) {
         else if (k == "--dispatch") dispatch = std::stoi(v);
         else if (k == "--bgra") bgra_out = v;
         else if (k == "--pfm") pfm = v;
+        else if (k == "--texture") texture = v;
         else { fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
     }
 
@@ -87,16 +92,26 @@ int main(int argc, char** argv) {
         tracer.AddObject(make_sphere(make_material(MaterialType::Diffuse, make_float3(0.3f, 0.8f, 0.3f)), make_float3(0.f, 15.f, 0.f), 15.f));
         tracer.AddObject(make_sphere(make_material(MaterialType::Diffuse, make_float3(0.3f, 0.3f, 0.8f)), make_float3(35.f, 15.f, 0.f), 15.f));
     } else {
+        PocaTexture tex = 0;
+        if (!texture.empty()) {
+            tex = PocaTextureUtils::AddTexByFile(texture);
+            if (!tex) return 1;
+            printf("texture handle %llu\n", (unsigned long long)tex);
+        }
+        auto textured = [tex](Material m) {
+            if (tex) { m.have_tex_ = true; m.tex_ = tex; }
+            return m;
+        };
         Object* floor = new Object();
         std::memset(floor, 0, sizeof(Object));
-        floor->material_ = make_material(MaterialType::Diffuse, make_float3(0.95f, 0.95f, 0.95f));
+        floor->material_ = textured(make_material(MaterialType::Diffuse, make_float3(0.95f, 0.95f, 0.95f)));
         floor->type_ = PrimitiveType::Platform;
         floor->y_pos_ = 0.f;
         floor->center_ = make_float3(0, -10000.f, 0);
         floor->radius_ = 10000.f;
         tracer.AddObject(floor);
-        tracer.AddObject(make_sphere(make_material(MaterialType::Glass, make_float3(1.f), 1.5f, 4.f), make_float3(-35.f, 15.f, 0.f), 15.f));
-        tracer.AddObject(make_sphere(make_material(MaterialType::Metal, make_float3(0.8f, 0.6f, 0.2f), 0.f, 2.5f), make_float3(0.f, 15.f, 0.f), 15.f));
+        tracer.AddObject(make_sphere(textured(make_material(MaterialType::Glass, make_float3(1.f), 1.5f, 4.f)), make_float3(-35.f, 15.f, 0.f), 15.f));
+        tracer.AddObject(make_sphere(textured(make_material(MaterialType::Metal, make_float3(0.8f, 0.6f, 0.2f), 0.f, 2.5f)), make_float3(0.f, 15.f, 0.f), 15.f));
         tracer.AddObject(make_sphere(make_material(MaterialType::Mirror, make_float3(0.9f), 0.f, 3.f, 0.6f), make_float3(35.f, 15.f, 0.f), 15.f));
     }
 

@@ -22,7 +22,7 @@ public:
     bool have_tex_;
     union {
         float3 kd_;
-        PocaTexture tex_;     // textured materials: rejected by the renderer for now
+        PocaTexture tex_;     // have_tex_: kd = the texture sampled at (0, 0) (material.cu:11-18)
     };
     float refractive_index_;
     float emit_intensity_;

@@ -48,6 +48,9 @@ public:
     void SetSeed(uint64_t seed);                // reference seeds with clock() (path_tracer.cu:107)
     bool SetDevice(int device);                 // before the first render
     bool SetEnvTexture(PocaTexture tex);        // default: textures/sky (assets/sky.cptex)
+    // BVH walk: true (default) = CPT_TRAVERSAL_ORDERED (same image, fewer node visits);
+    // false = the reference's right-first DFS order (its node/prim counts in GetStats).
+    void SetOrderedTraversal(bool on) { ordered_walk_ = on; }
     // Synchronous `spp` passes into the radiance accumulator (accumulate=false restarts it).
     bool Render(int spp, bool accumulate = true);
     // Per-pixel mean radiance, rgb float[width*height*3] (row-major, y down).
@@ -71,6 +74,7 @@ private:
     int device_ = 0;
     uint64_t seed_ = 1234;
     uint max_recursion_depth_ = 8;
+    bool ordered_walk_ = true;
     int width_ = 0, height_ = 0;
     uint64_t scene_build_ = 0;      // SceneBVH::BuildId() uploaded to the context
     size_t updates_applied_ = 0;    // prefix of SceneBVH::UpdateLog() refitted on the context

@@ -4,8 +4,8 @@
 // decodes PNG with OpenCV (textures.cu:15-17); this build reads the raw `.cptex` format
 // (tools/make_sky_fixture.py) and binary PPM (P6), since no image codec ships here.  The
 // reference's upload quirk (only width/4 texels per row reach the texture, textures.cu:32-33)
-// is applied to full-width images.  Sampling modes: Mirror + Linear (the reference's
-// defaults, the only ones it uses) are supported; other modes are rejected.
+// is applied to full-width images.  The sky is always sampled mirror + linear (the
+// reference's defaults); material textures honour the handle's address and filter modes.
 #pragma once
 
 #include <stdint.h>

@@ -18,6 +18,9 @@
  *   cpt_update_object               SceneBVH::UpdateObject (bvh.cu:144-157).
  *   cpt_set_env_texture             PocaTextureUtils::AddTexByFile (textures.cu:14-62) +
  *                                   the sky load in InitBuffers (path_tracer.cu:47).
+ *   cpt_bind_texture                AddTexByFile for a material texture: the handle the app
+ *                                   stores in Material::tex_ (material.h:21-25), sampled by
+ *                                   Material::GetKd (material.cu:11-18).
  *   cpt_set_frame                   InitBuffers' per-pixel buffers (path_tracer.cu:44-115),
  *                                   plus a row window/list for multi-GPU row tiling.
  *   cpt_init_rng                    InitCuRand kernel (path_tracer.cu:36-42, 99-107).
@@ -67,7 +70,7 @@ typedef struct cpt_float3 { float x, y, z; } cpt_float3;
 /* Material (material.h:17-35), 40 bytes. */
 typedef struct cpt_material {
     int32_t type;              /* @0  cpt_material_type */
-    uint8_t have_tex;          /* @4  textured materials: not supported yet (CPT_ERR_UNSUPPORTED) */
+    uint8_t have_tex;          /* @4  nonzero: kd = the texture bound to u.tex (cpt_bind_texture) */
     uint8_t pad_[3];
     union {                    /* @8  union { float3 kd_; cudaTextureObject_t tex_; } */
         cpt_float3 kd;
@@ -164,6 +167,25 @@ int cpt_bvh_build_host(const cpt_object* objs, int n_objs, float* boxes, int32_t
  * logical_width/4 texels per row, textures.cu:32-33; texels at x >= valid_cols read 0).
  * Sampler: normalized coords, mirror addressing, bilinear, c/255 (textures.cu:36-44). */
 int cpt_set_env_texture(cpt_ctx* ctx, const uint8_t* rgba, int logical_width, int height, int valid_cols);
+
+/* cudaTextureAddressMode / cudaTextureFilterMode values of AddTexByFile's arguments. */
+#define CPT_ADDRESS_WRAP   0
+#define CPT_ADDRESS_CLAMP  1
+#define CPT_ADDRESS_MIRROR 2   /* AddTexByFile's default */
+#define CPT_ADDRESS_BORDER 3   /* border colour 0 */
+#define CPT_FILTER_POINT   0
+#define CPT_FILTER_LINEAR  1   /* AddTexByFile's default */
+
+/* Binds texels to a material texture handle (replacing an earlier binding).  A textured
+ * material (have_tex != 0) takes its diffuse colour from the texture bound to u.tex:
+ * GetKd is always called at normalized (0, 0) (material.cu:31,56,95,140 pass no uv), so
+ * the colour is that one sample, taken once per material when the scene is prepared.
+ * Emission keeps reading kd_, i.e. the bits of the handle, as the reference's union does
+ * (material.cu:36).  Layout as cpt_set_env_texture; a material whose handle is unbound
+ * makes cpt_set_scene / cpt_render fail with CPT_ERR_INVALID_ARG.  Binding after
+ * cpt_set_scene re-prepares the materials. */
+int cpt_bind_texture(cpt_ctx* ctx, uint64_t handle, const uint8_t* rgba, int logical_width, int height,
+                     int valid_cols, int address_mode, int filter_mode);
 
 /* Per-pixel buffers for a width x height frame; the context renders the global image rows
  * listed in `rows` (n_rows of them; rows == NULL means 0..height-1).  Pixel i of the

@@ -69,6 +69,10 @@ def lib():
         L.or_render.restype = i32
         L.or_render_edited.argtypes = [P, i32, P, P, i32, P, P, i32, i32, i32, P, i32, i32, i32, P, P, P, i32]
         L.or_render_edited.restype = i32
+        L.or_bind_texture.argtypes = [u64, P, i32, i32, i32, i32, i32]
+        L.or_bind_texture.restype = None
+        L.or_clear_textures.argtypes = []
+        L.or_clear_textures.restype = None
         L.or_set_walk.argtypes = [i32]
         L.or_set_walk.restype = None
         _lib = L
@@ -138,7 +142,7 @@ def render(objs, cam, env, rows, spp, max_depth, rng, accum=None, want_aux=False
     objs = np.ascontiguousarray(objs)
     cam = np.ascontiguousarray(cam)
     rows = np.ascontiguousarray(rows, dtype=np.int32)
-    W = int(cam["width"])
+    W = int(np.asarray(cam["width"]).reshape(-1)[0])
     npix = rows.size * W
     assert rng.dtype == np.uint32 and rng.shape == (6, npix) and rng.flags.c_contiguous
     if accum is None:
@@ -157,6 +161,16 @@ def render(objs, cam, env, rows, spp, max_depth, rng, accum=None, want_aux=False
     return accum, st, normal, depth
 
 
+def bind_texture(handle, tex, address_mode=2, filter_mode=1):
+    """Bind texels (texture_io.EnvTexture) to a material texture handle (process-wide)."""
+    rgba = np.ascontiguousarray(tex.rgba, dtype=np.uint8)
+    lib().or_bind_texture(handle, _ptr(rgba), tex.width, tex.height, tex.valid_cols, address_mode, filter_mode)
+
+
+def clear_textures():
+    lib().or_clear_textures()
+
+
 def set_walk(ordered: bool):
     """DIAGNOSTIC: make render() walk the BVH the way CPT_TRAVERSAL_ORDERED does (near child
     first, reference-rank tie rule) instead of the reference's right-first DFS.  Process-wide."""
@@ -171,7 +185,7 @@ def render_edited(objs, edits, cam, env, rows, spp, max_depth, rng, threads=1):
     rows = np.ascontiguousarray(rows, dtype=np.int32)
     idx = np.ascontiguousarray([i for i, _ in edits], dtype=np.int32)
     new = np.ascontiguousarray(np.array([o for _, o in edits], dtype=objs.dtype))
-    npix = rows.size * int(cam["width"])
+    npix = rows.size * int(np.asarray(cam["width"]).reshape(-1)[0])
     assert rng.dtype == np.uint32 and rng.shape == (6, npix) and rng.flags.c_contiguous
     accum = np.zeros((npix, 4), dtype=np.float32)
     stats = np.zeros(5, dtype=np.uint64)

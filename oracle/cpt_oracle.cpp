@@ -418,9 +418,14 @@ Xorwow curand_init(uint64_t seed, uint64_t subsequence) {
 // Bilinear weights are quantised to 1/256 with round-to-nearest (CUDA guide: 9-bit fixed
 // point, 8 fractional bits; rounding mode UNPINNED).
 // ---------------------------------------------------------------------------------------
+// Address modes (cudaTextureAddressMode values) and filter modes (cudaTextureFilterMode).
+enum { ADDR_WRAP = 0, ADDR_CLAMP = 1, ADDR_MIRROR = 2, ADDR_BORDER = 3 };
+enum { FILTER_POINT = 0, FILTER_LINEAR = 1 };
+
 struct Env {
     const uint8_t* rgba;   // valid_cols x h, row pitch valid_cols*4
     int w, h, valid_cols;
+    int addr = ADDR_MIRROR, filter = FILTER_LINEAR;   // the sky's: AddTexByFile defaults (textures.h:9-11)
 };
 
 inline int mirror_index(int i, int n) {
@@ -431,9 +436,19 @@ inline int mirror_index(int i, int n) {
     return m;
 }
 
+// Texel index after addressing; -1 = outside (border colour 0).
+inline int address(int i, int n, int mode) {
+    switch (mode) {
+        case ADDR_WRAP: { int m = i % n; return m < 0 ? m + n : m; }
+        case ADDR_CLAMP: return i < 0 ? 0 : (i >= n ? n - 1 : i);
+        case ADDR_BORDER: return (i < 0 || i >= n) ? -1 : i;
+        default: return mirror_index(i, n);
+    }
+}
+
 inline void texel(const Env& e, int i, int j, float out[3]) {
-    int x = mirror_index(i, e.w), y = mirror_index(j, e.h);
-    if (x >= e.valid_cols || e.rgba == nullptr) { out[0] = out[1] = out[2] = 0.0f; return; }
+    int x = address(i, e.w, e.addr), y = address(j, e.h, e.addr);
+    if (x < 0 || y < 0 || x >= e.valid_cols || e.rgba == nullptr) { out[0] = out[1] = out[2] = 0.0f; return; }
     const uint8_t* p = e.rgba + ((size_t)y * e.valid_cols + x) * 4;
     out[0] = (float)p[0] / 255.0f;
     out[1] = (float)p[1] / 255.0f;
@@ -441,6 +456,13 @@ inline void texel(const Env& e, int i, int j, float out[3]) {
 }
 
 f3 tex2d(const Env& e, float u, float v) {
+    if (e.filter == FILTER_POINT) {
+        float x = u * (float)e.w, y = v * (float)e.h;
+        if (!(x > -1e7f && x < 1e7f && y > -1e7f && y < 1e7f)) return mk1(0.0f);
+        float t[3];
+        texel(e, (int)floorf(x), (int)floorf(y), t);
+        return mk(t[0], t[1], t[2]);
+    }
     float x = u * (float)e.w - 0.5f;
     float y = v * (float)e.h - 0.5f;
     if (!(x > -1e7f && x < 1e7f && y > -1e7f && y < 1e7f)) return mk1(0.0f);  // NaN/huge guard
@@ -457,6 +479,21 @@ f3 tex2d(const Env& e, float u, float v) {
     float r[3];
     for (int c = 0; c < 3; ++c) r[c] = ((w00 * t00[c] + w10 * t10[c]) + w01 * t01[c]) + w11 * t11[c];
     return mk(r[0], r[1], r[2]);
+}
+
+// Material textures (§8(f) rank 4): handle -> texels, bound by or_bind_texture the way the
+// app would keep the cudaTextureObject_t returned by AddTexByFile.
+struct TexRec {
+    std::vector<uint8_t> rgba;
+    Env env;
+};
+std::mutex g_tex_mu;
+std::vector<std::pair<uint64_t, TexRec*>> g_textures;
+
+const TexRec* find_texture(uint64_t handle) {
+    std::lock_guard<std::mutex> g(g_tex_mu);
+    for (auto& t : g_textures) if (t.first == handle) return t.second;
+    return nullptr;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -882,13 +919,22 @@ inline f3 lobe(float x_1, float x_2, double inv_alpha) {
     return mk(r * dm_cosf(phi), r * dm_sinf(phi), z);
 }
 
+// Material::GetKd (material.cu:11-18), always called with (x, y) = (0, 0): the texture's
+// sample at normalized (0, 0) for a textured material (an unbound handle reads 0), else kd_.
+// Emission keeps reading kd_, which aliases tex_ in a textured material (material.cu:36).
+f3 get_kd(const Material& m) {
+    if (!m.have_tex) return m.u.kd;
+    const TexRec* t = find_texture(m.u.tex);
+    return t ? tex2d(t->env, 0.0f, 0.0f) : mk1(0.0f);
+}
+
 void diffuse_shader(const Material& m, Payload& p, f3 position, f3 normal, f3 in_ray_dir, Xorwow& rng) {  // :20-38
     (void)in_ray_dir;
     float x_1 = uniform(rng), x_2 = uniform(rng);
     f3 localRay = lobe(x_1, x_2, 1.0 / 2);
     p.bounce_dir = to_world(localRay, normal);
     float cosalpha = dot(normal, p.bounce_dir);
-    p.attenuation = cosalpha > 0.0f ? m.u.kd : mk(0.0f, 0.0f, 0.0f);
+    p.attenuation = cosalpha > 0.0f ? get_kd(m) : mk(0.0f, 0.0f, 0.0f);
     p.radiance = mul(m.emit_intensity, m.u.kd);
     p.hit_pos = position;
 }
@@ -901,7 +947,7 @@ void mirror_shader(const Material& m, Payload& p, f3 position, f3 normal, f3 in_
     f3 reflect_dir = reflect(in_ray_dir, normal);
     f3 wo = to_world(localRay, reflect_dir);
     float cosalpha = dot(normal, wo);
-    p.attenuation = cosalpha > 0.0f ? m.u.kd : mk(0.0f, 0.0f, 0.0f);
+    p.attenuation = cosalpha > 0.0f ? get_kd(m) : mk(0.0f, 0.0f, 0.0f);
     p.bounce_dir = wo;
     p.radiance = mul(m.emit_intensity, m.u.kd);
     p.hit_pos = position;
@@ -919,7 +965,7 @@ void metal_shader(const Material& m, Payload& p, f3 position, f3 normal, f3 in_r
         f3 localRay = lobe(x_1, x_2, 1.0 / 2.0);
         p.bounce_dir = to_world(localRay, normal);
     }
-    p.attenuation = dot(p.bounce_dir, normal) < 0 ? mk(0.0f, 0.0f, 0.0f) : m.u.kd;
+    p.attenuation = dot(p.bounce_dir, normal) < 0 ? mk(0.0f, 0.0f, 0.0f) : get_kd(m);
     p.radiance = mul(m.emit_intensity, m.u.kd);
     p.hit_pos = position;
 }
@@ -945,7 +991,7 @@ void glass_shader(const Material& m, Payload& p, f3 position, f3 normal, f3 in_r
     else reflect_prob = 1.0f;
     if (uniform(rng) < reflect_prob) p.bounce_dir = to_world(localRay, reflect(in_ray_dir, normal));
     else p.bounce_dir = to_world(localRay, refracted);
-    p.attenuation = m.u.kd;
+    p.attenuation = get_kd(m);
     p.radiance = mul(m.emit_intensity, m.u.kd);
     p.hit_pos = position;
 }
@@ -1086,6 +1132,24 @@ void render_rows(const RenderJob& J, int thread, int nthreads, Stats& st) {
 extern "C" {
 
 int or_abi_version(void) { return 1; }
+
+// Binds texels to a material texture handle (replaces an earlier binding of the handle).
+void or_bind_texture(uint64_t handle, const uint8_t* rgba, int w, int h, int valid_cols, int addr, int filter) {
+    TexRec* t = new TexRec;
+    t->rgba.assign(rgba, rgba + (size_t)valid_cols * h * 4);
+    t->env = Env{nullptr, w, h, valid_cols, addr, filter};
+    t->env.rgba = t->rgba.empty() ? nullptr : t->rgba.data();
+    std::lock_guard<std::mutex> g(g_tex_mu);
+    for (auto& e : g_textures)
+        if (e.first == handle) { delete e.second; e.second = t; return; }
+    g_textures.emplace_back(handle, t);
+}
+
+void or_clear_textures(void) {
+    std::lock_guard<std::mutex> g(g_tex_mu);
+    for (auto& e : g_textures) delete e.second;
+    g_textures.clear();
+}
 
 void or_set_walk(int ordered) { g_walk_ordered = ordered ? 1 : 0; }   // diagnostic, see trace_ray_ordered
 
