@@ -5,9 +5,11 @@
 One step = one full render of the configured workload (all `spp` SamplePixel passes for
 every pixel of the image; each pass continues the pixel's XORWOW stream, exactly like the
 reference's progressive passes) with inputs already resident in HBM, plus — for N > 1 — the
-RCCL gather of the fp32 framebuffer tiles into rank 0.  Multi-GPU: one process per GPU
-(torchrun), the image rows are dealt in interleaved 16-row blocks (row tiling, strong
-scaling: the total image is fixed).
+RCCL gather of the fp32 framebuffer tiles.  Multi-GPU: one process per GPU (torchrun), the
+image rows are dealt in interleaved 8-row blocks (row tiling).  Scaling (DESIGN.md
+§Multi-GPU): "weak" (default) keeps the pixels per GPU fixed — at N GPUs the image is the
+configuration's resolution scaled by sqrt(N) per axis (same aspect and framing; N = 4 is
+3840x2160) — and "strong" renders the configuration's image at every N.
 
 Rank 0 prints one JSON line with `roofline` (algorithmic bytes of SURVEY.md §8(d) ÷ the
 kernel's HIP-event time) and `cpu_baseline` (the scalar oracle on a bounded sample of the
@@ -78,6 +80,8 @@ def main():
     ap.add_argument("--walk", default="ordered", choices=["reference", "ordered"],
                     help="BVH node order: the reference's right-first DFS, or near-first per ray octant "
                          "(CPT_TRAVERSAL_ORDERED, same closest hits; DESIGN.md §Ordered walk)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: pixels per GPU fixed (image grows by sqrt(N) per axis); strong: fixed image")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=None,
@@ -92,9 +96,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # CPT_BENCH_BACKEND=gloo: rehearsal of the N-rank path on a box with fewer GPUs (ranks share
+    # devices round-robin, collectives go through host copies).  Never used for reported runs.
+    backend = os.environ.get("CPT_BENCH_BACKEND", "nccl")
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        local_dev = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local_dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -108,11 +119,21 @@ def main():
     if args.height:
         cfg["height"] = args.height
     cfg["seed"] = args.seed
+    if args.scaling == "weak" and world > 1 and not (args.width or args.height):
+        cfg["width"], cfg["height"] = tiling.weak_scaled_size(cfg["width"], cfg["height"], world)
     W, H, spp, depth = cfg["width"], cfg["height"], cfg["spp"], cfg["depth"]
     objs = scenes.SCENES[cfg["scene"]]()
     sky = texture_io.load_cptex()
     cam = camera_get_copy(scenes.camera_for(W, H))
     rows = tiling.partition_rows(H, world, rank)
+
+    def _all_reduce(x, op=dist.ReduceOp.SUM):
+        if backend == "nccl":
+            dist.all_reduce(x, op=op)
+            return x
+        h = x.cpu()
+        dist.all_reduce(h, op=op)
+        return h.to(x.device)
 
     r = Renderer(torch.cuda.current_device())
     # One non-default HIP stream for everything: the render kernels (via cpt_set_stream), the
@@ -150,7 +171,12 @@ def main():
             # RCCL all-gather of the fp32 tiles over xGMI, then the on-device stitch into the
             # full framebuffer (rank 0 keeps it; every rank holds a copy after all-gather)
             r.copy_accum_device(send.data_ptr(), npix_local * 16)
-            dist.all_gather_into_tensor(gathered, send)
+            if backend == "nccl":
+                dist.all_gather_into_tensor(gathered, send)
+            else:
+                g_host = gathered.cpu()
+                dist.all_gather_into_tensor(g_host, send.cpu())
+                gathered.copy_(g_host)
             fb = gathered.view(world * max_rows, W, 4).index_select(0, stitch_idx)
             return fb
         return None
@@ -168,7 +194,7 @@ def main():
         loc = r.stats()
         v = torch.tensor([loc[k] for k in KEYS], dtype=torch.float64, device=dev)
         if world > 1:
-            dist.all_reduce(v)
+            v = _all_reduce(v)
         return dict(zip(KEYS, (int(x) for x in v.tolist())))
 
     st = count_pass(False)
@@ -184,7 +210,7 @@ def main():
         torch.cuda.synchronize()
         nd = (fb_ref.view(torch.int32) != fb_ord.view(torch.int32)).any(dim=1).sum().to(torch.float64)
         if world > 1:
-            dist.all_reduce(nd)
+            nd = _all_reduce(nd)
         walk_diff = int(nd.item())
         del fb_ref, fb_ord
     r.init_rng(cfg["seed"])
@@ -210,7 +236,7 @@ def main():
 
     t = torch.tensor([elapsed, avg_kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = _all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, avg_kernel_ms_max = t.tolist()
 
     if rank == 0:
@@ -244,7 +270,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (deterministic procedural scene, sky.png fixture)",
@@ -252,7 +278,8 @@ def main():
                 "workload": f"{args.config}: {cfg['scene']} {W}x{H} {spp}spp depth {depth}",
                 "width": W, "height": H, "spp": spp, "max_depth": depth, "seed": cfg["seed"],
                 "rows_rendered": H, "path": args.path, "walk": args.walk,
-                "parallelism": f"row-tiled x{world} (interleaved 16-row blocks)" + (", RCCL all-gather" if world > 1 else ""),
+                "parallelism": f"row-tiled x{world} (interleaved {tiling.BLOCK_ROWS}-row blocks)" + (
+                    ", RCCL all-gather" if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",

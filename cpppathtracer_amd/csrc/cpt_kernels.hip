@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "cpt_path.hpp"
 
@@ -503,6 +504,11 @@ static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_megakernel<S, A, L>, block, shmem);
         if (e != hipSuccess) return e;
         if (blocks_per_cu < 1) blocks_per_cu = 1;
+        // tuning knob (experiments only): cap the resident 256-lane blocks per CU
+        if (const char* v = getenv("CPT_MK_BLOCKS_PER_CU")) {
+            const int cap = atoi(v);
+            if (cap >= 1 && cap < blocks_per_cu) blocks_per_cu = cap;
+        }
     }
     // persistent grid: every resident slot once; lanes pull pixels from p.work
     const long long tiles = (long long)((p.width + 7) / 8) * ((p.n_rows + 7) / 8);

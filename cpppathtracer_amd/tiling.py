@@ -1,6 +1,6 @@
 """Row tiling of the image across GPUs.
 
-Each rank renders the global rows of its interleaved 16-row blocks (block b -> rank
+Each rank renders the global rows of its interleaved 8-row blocks (block b -> rank
 b % world): the sky-heavy top rows and the object-heavy bottom rows are dealt evenly, so the
 ranks' work is balanced without a pilot pass.  A pixel's XORWOW stream depends only on
 (seed, x, y) (path_tracer.cu:36-42), so any row partition gives results bit-identical to a
@@ -9,7 +9,16 @@ framebuffer with a single all-gather (RCCL over xGMI on MI355X; gloo in the CPU 
 """
 import numpy as np
 
-BLOCK_ROWS = 16
+BLOCK_ROWS = 8   # one row of the megakernel's 8x8 pixel tiles
+
+
+def weak_scaled_size(width: int, height: int, world: int) -> tuple:
+    """Weak scaling (bench.py --scaling weak): N times the pixels at the same aspect, i.e. each
+    axis scaled by sqrt(N) and rounded to whole 8x8 tiles (N = 4: 1920x1080 -> 3840x2160)."""
+    if world <= 1:
+        return width, height
+    f = world ** 0.5
+    return int(round(width * f / 8)) * 8, int(round(height * f / 8)) * 8
 
 
 def partition_rows(height: int, world: int, rank: int, block: int = BLOCK_ROWS) -> np.ndarray:

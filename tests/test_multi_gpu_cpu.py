@@ -1,5 +1,5 @@
 """Row-tiled multi-rank rendering on CPU (gloo, world_size 2): the host logic bench.py runs
-on N GPUs over RCCL.  Each rank renders its interleaved 16-row blocks (the oracle stands in
+on N GPUs over RCCL.  Each rank renders its interleaved 8-row blocks (the oracle stands in
 for the GPU in this CPU-only test), the fp32 tiles are all-gathered and stitched, and the
 result must equal a monolithic render bit for bit (per-pixel streams depend only on
 (seed, x, y), path_tracer.cu:36-42)."""
@@ -78,3 +78,16 @@ def test_partition_covers_rows_once(H, world):
     assert np.array_equal(np.sort(allr), np.arange(H))
     sizes = [tiling.partition_rows(H, world, r).size for r in range(world)]
     assert max(sizes) - min(sizes) <= tiling.BLOCK_ROWS
+
+
+def test_weak_scaled_sizes():
+    """bench.py --scaling weak: N x the pixels of 1920x1080 at the same aspect."""
+    assert tiling.weak_scaled_size(1920, 1080, 1) == (1920, 1080)
+    assert tiling.weak_scaled_size(1920, 1080, 4) == (3840, 2160)
+    for n in (2, 4, 8):
+        w, h = tiling.weak_scaled_size(1920, 1080, n)
+        assert w % 8 == 0 and h % 8 == 0
+        assert abs(w * h / (1920 * 1080 * n) - 1) < 0.01
+        assert abs(w / h - 16 / 9) < 0.01
+        rows = [tiling.partition_rows(h, n, r).size for r in range(n)]
+        assert sum(rows) == h and max(rows) - min(rows) <= tiling.BLOCK_ROWS
