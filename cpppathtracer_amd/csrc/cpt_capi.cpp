@@ -420,44 +420,106 @@ int material_slot(cpt_ctx* c, const cpt_material& m) {
     return (int)c->mats_h.size() - 1;
 }
 
-// Walk tree of the ordered walk (CPT_TRAVERSAL_ORDERED): the reference tree with every
-// platform leaf spliced out (its sibling takes the parent's place, the ancestors' boxes are
-// refit with MIN/MAX of their children).  A platform's box spans +-5e30 in x and z, so in the
-// reference tree every ancestor of the floor passes its slab test; without it those nodes
-// cull.  All other boxes stay the reference's.  The spliced leaves (by reference rank) are
-// returned in `unbounded`; the ordered walk tests them first.
-int build_walk_tree(const HostBvh& b, const std::vector<cpt_object>& objs, const std::vector<int>& ref_pos,
-                    HostBvh& w, std::vector<int>& unbounded) {
-    w = b;
-    unbounded.clear();
-    if (w.nodes.empty()) return -1;
-    int root = 0;
-    std::vector<int> order(w.nodes.size());
-    for (size_t i = 0; i < order.size(); ++i) order[ref_pos[i]] = (int)i;
-    for (int i : order) {
-        BNode& n = w.nodes[i];
-        if (!n.is_object || objs[n.obj].type != CPT_PRIM_PLATFORM) continue;
-        unbounded.push_back(i);
-        int p = n.parent;
-        if (p < 0) { root = -1; continue; }
-        int sib = w.nodes[p].left == i ? w.nodes[p].right : w.nodes[p].left;
-        int gp = w.nodes[p].parent;
-        w.nodes[sib].parent = gp;
-        if (gp < 0) root = sib;
-        else if (w.nodes[gp].left == p) w.nodes[gp].left = sib;
-        else w.nodes[gp].right = sib;
-        for (int a = gp; a >= 0; a = w.nodes[a].parent) {
-            BNode& A = w.nodes[a];
-            const BNode &L = w.nodes[A.left], &R = w.nodes[A.right];
-            A.bmin = F3{MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z)};
-            A.bmax = F3{MAX_(L.bmax.x, R.bmax.x), MAX_(L.bmax.y, R.bmax.y), MAX_(L.bmax.z, R.bmax.z)};
-        }
-    }
-    return root;
+// Walk tree of the ordered walk (CPT_TRAVERSAL_ORDERED, DESIGN.md §Ordered walk): a binned
+// SAH tree over the bounded primitives, one primitive per leaf.  Platforms (+-5e30 boxes) stay
+// out of it: the walk tests them first.  The tree only decides which primitives a ray tests;
+// the closest hit is the reference's (rank tie rule, conservative slab test, winner
+// certificate in cpt_path.hpp).
+namespace sah {
+constexpr int NB = 16;
+inline float comp(const F3& v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+inline F3 fmin3(const F3& a, const F3& b) { return F3{MIN_(a.x, b.x), MIN_(a.y, b.y), MIN_(a.z, b.z)}; }
+inline F3 fmax3(const F3& a, const F3& b) { return F3{MAX_(a.x, b.x), MAX_(a.y, b.y), MAX_(a.z, b.z)}; }
+inline float area(const F3& lo, const F3& hi) {
+    const float dx = hi.x - lo.x, dy = hi.y - lo.y, dz = hi.z - lo.z;
+    return 2.f * (dx * dy + dy * dz + dz * dx);
+}
+inline int bin_of(float c, float e0, float e1) { return std::min(NB - 1, (int)((c - e0) / (e1 - e0) * NB)); }
+
+int leaf(HostBvh& t, const std::vector<cpt_object>& O, int o) {
+    BNode n{};
+    n.bmin = aabb_min(O[o]);
+    n.bmax = aabb_max(O[o]);
+    n.is_object = true;
+    n.left = n.right = -1;
+    n.obj = o;
+    n.parent = -1;
+    t.nodes.push_back(n);
+    return (int)t.nodes.size() - 1;
 }
 
+int build(HostBvh& t, const std::vector<cpt_object>& O, std::vector<int>& idx, int l, int r) {
+    if (r - l == 1) return leaf(t, O, idx[l]);
+    F3 lo = aabb_min(O[idx[l]]), hi = aabb_max(O[idx[l]]);
+    F3 clo{1e30f, 1e30f, 1e30f}, chi{-1e30f, -1e30f, -1e30f};
+    std::vector<float> cen(3 * (r - l));
+    for (int i = l; i < r; ++i) {
+        const F3 a = aabb_min(O[idx[i]]), b = aabb_max(O[idx[i]]);
+        lo = fmin3(lo, a);
+        hi = fmax3(hi, b);
+        const F3 c{(a.x + b.x) * .5f, (a.y + b.y) * .5f, (a.z + b.z) * .5f};
+        cen[3 * (i - l)] = c.x; cen[3 * (i - l) + 1] = c.y; cen[3 * (i - l) + 2] = c.z;
+        clo = fmin3(clo, c);
+        chi = fmax3(chi, c);
+    }
+    float best = 3.0e38f;
+    int best_axis = -1, best_bin = -1;
+    for (int axis = 0; axis < 3; ++axis) {
+        const float e0 = comp(clo, axis), e1 = comp(chi, axis);
+        if (!(e1 > e0)) continue;
+        int cnt[NB] = {0};
+        F3 blo[NB], bhi[NB];
+        for (int b = 0; b < NB; ++b) { blo[b] = F3{1e30f, 1e30f, 1e30f}; bhi[b] = F3{-1e30f, -1e30f, -1e30f}; }
+        for (int i = l; i < r; ++i) {
+            const int b = bin_of(cen[3 * (i - l) + axis], e0, e1);
+            cnt[b]++;
+            blo[b] = fmin3(blo[b], aabb_min(O[idx[i]]));
+            bhi[b] = fmax3(bhi[b], aabb_max(O[idx[i]]));
+        }
+        for (int sp = 1; sp < NB; ++sp) {
+            int nl = 0, nr = 0;
+            F3 llo{1e30f, 1e30f, 1e30f}, lhi{-1e30f, -1e30f, -1e30f}, rlo = llo, rhi = lhi;
+            for (int b = 0; b < sp; ++b) if (cnt[b]) { nl += cnt[b]; llo = fmin3(llo, blo[b]); lhi = fmax3(lhi, bhi[b]); }
+            for (int b = sp; b < NB; ++b) if (cnt[b]) { nr += cnt[b]; rlo = fmin3(rlo, blo[b]); rhi = fmax3(rhi, bhi[b]); }
+            if (!nl || !nr) continue;
+            const float cost = area(llo, lhi) * nl + area(rlo, rhi) * nr;
+            if (cost < best) { best = cost; best_axis = axis; best_bin = sp; }
+        }
+    }
+    int axis, mid;
+    if (best_axis < 0) {
+        // all centroids coincide: split the list in half (stable order)
+        axis = 0;
+        mid = (l + r) / 2;
+    } else {
+        axis = best_axis;
+        const float e0 = comp(clo, axis), e1 = comp(chi, axis);
+        std::vector<int> lhs, rhs;
+        for (int i = l; i < r; ++i)
+            (bin_of(cen[3 * (i - l) + axis], e0, e1) < best_bin ? lhs : rhs).push_back(idx[i]);
+        std::copy(lhs.begin(), lhs.end(), idx.begin() + l);
+        std::copy(rhs.begin(), rhs.end(), idx.begin() + l + (int)lhs.size());
+        mid = l + (int)lhs.size();
+    }
+    const int me = (int)t.nodes.size();
+    t.nodes.push_back(BNode{});
+    const int L = build(t, O, idx, l, mid), R = build(t, O, idx, mid, r);
+    BNode& n = t.nodes[me];
+    n.bmin = lo; n.bmax = hi;
+    n.is_object = false;
+    n.left = L; n.right = R; n.obj = -1; n.parent = -1; n.axis = axis;
+    t.nodes[L].parent = me;
+    t.nodes[R].parent = me;
+    return me;
+}
+}  // namespace sah
+
+// Returns the walk tree's root (-1: no bounded primitive); `unbounded` = its platform leaves
+// by reference rank; `rank` = the reference rank of every walk-tree leaf.
+int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, std::vector<int>& rank);
+
 // The reference order followed by the eight octant orders of the walk tree (one array,
-// n_bvh nodes each: the unbounded leaves, then the tree).
+// n_walk nodes each: the unbounded leaves, then the tree).
 void linearise_all(cpt_ctx* c) {
     c->lin.clear();
     c->n_walk = 0;
@@ -466,11 +528,31 @@ void linearise_all(cpt_ctx* c) {
     c->n_bvh = (int)c->lin.size();
     if (c->n_bvh == 0) return;
     HostBvh w;
-    std::vector<int> unbounded, pos;
-    const int root = build_walk_tree(c->bvh, c->objs, c->pos_of_node, w, unbounded);
-    for (int o = 0; o < 8; ++o)
-        linearise(w, c->objs, c->mat_of_obj, c->lin, pos, o, &c->pos_of_node, root, unbounded);
+    std::vector<int> unbounded, rank, pos;
+    const int root = build_walk_tree(c, w, unbounded, rank);
+    for (int o = 0; o < 8; ++o) linearise(w, c->objs, c->mat_of_obj, c->lin, pos, o, &rank, root, unbounded);
     c->n_walk = (int)(c->lin.size() - c->n_bvh) / 8;
+}
+
+int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, std::vector<int>& rank) {
+    const std::vector<cpt_object>& O = c->objs;
+    w.nodes.clear();
+    w.leaf_of_object.assign(O.size(), -1);
+    unbounded.clear();
+    std::vector<int> idx;
+    std::vector<std::pair<int, int>> flat;   // (reference rank, object) of the platforms
+    for (size_t o = 0; o < O.size(); ++o) {
+        const int ref_rank = c->pos_of_node[c->bvh.leaf_of_object[o]];
+        if (O[o].type == CPT_PRIM_PLATFORM) flat.emplace_back(ref_rank, (int)o);
+        else idx.push_back((int)o);
+    }
+    std::sort(flat.begin(), flat.end());
+    for (const auto& f : flat) unbounded.push_back(sah::leaf(w, O, f.second));
+    const int root = idx.empty() ? -1 : sah::build(w, O, idx, 0, (int)idx.size());
+    rank.assign(w.nodes.size(), -1);
+    for (size_t i = 0; i < w.nodes.size(); ++i)
+        if (w.nodes[i].is_object) rank[i] = c->pos_of_node[c->bvh.leaf_of_object[w.nodes[i].obj]];
+    return root;
 }
 
 int upload_scene(cpt_ctx* c) {

@@ -142,11 +142,9 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             const bool finite_ray = !(ray.o.x != ray.o.x || ray.o.y != ray.o.y || ray.o.z != ray.o.z ||
                                       ray.d.x != ray.d.x || ray.d.y != ray.d.y || ray.d.z != ray.d.z);
             bool hit;
-            int n_order;
-            const Node* order = LDS ? nodes : walk_order(p, rk.d, n_order);
-            if (LDS) n_order = p.n_nodes;
-            if (__builtin_expect(finite_ray, 1)) hit = trace<STATS, true>(order, n_order, rk, h, code, cnt);
-            else hit = trace<STATS, false>(order, n_order, rk, h, code, cnt);
+            if (LDS) hit = finite_ray ? trace<STATS, true>(nodes, p.n_nodes, rk, h, code, cnt) > 0
+                                      : trace<STATS, false>(nodes, p.n_nodes, rk, h, code, cnt) > 0;
+            else hit = trace_segment<STATS>(p, rk, finite_ray, h, code, cnt);
             t2 = stamp();
             Shade sh;
             v3 attr_normal;
@@ -234,6 +232,8 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             atomicAdd((unsigned long long*)&p.stats[3], (unsigned long long)d);
             atomicAdd((unsigned long long*)&p.stats[4], (unsigned long long)e);
         }
+        const uint64_t f = wave_sum(cnt.fallbacks);   // ordered walk: certificate fallbacks
+        if (!CPT_STAMPS && lane == 0 && f) atomicAdd((unsigned long long*)&p.stats[5], (unsigned long long)f);
     }
 }
 

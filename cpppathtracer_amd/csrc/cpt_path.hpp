@@ -278,7 +278,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 }
 
 struct Counters {
-    uint32_t segments, nodes, prims, hits, misses;
+    uint32_t segments, nodes, prims, hits, misses, fallbacks;
 #if CPT_STAMPS == 2
     unsigned long long st_leaf, st_slab, st_iter;
 #endif
@@ -290,7 +290,12 @@ struct Counters {
 // (finite box coordinate minus finite origin, times a finite reciprocal), so the ternary
 // MIN/MAX of the reference equal v_min/v_max_f32 up to the sign of a zero, which none of
 // the three comparisons can see.  Rays carrying a NaN take the exact ternary form.
-template <bool FAST>
+// CONS (the ordered walk's tree): the same interval, widened by a relative margin before the
+// three comparisons, so that a primitive whose computed hit lies slightly outside its box by
+// rounding is still tested (DESIGN.md §Ordered walk).
+constexpr float WALK_MARGIN_REL = 1e-3f, WALK_MARGIN_ABS = 1e-4f;
+
+template <bool FAST, bool CONS = false>
 __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, float tmax) {
     float t0x = qdiv_raw(nd.a0 - ray.o.x, ray.yx), t1x = qdiv_raw(nd.b0 - ray.o.x, ray.yx);
     float t0y = qdiv_raw(nd.a1 - ray.o.y, ray.yy), t1y = qdiv_raw(nd.b1 - ray.o.y, ray.yy);
@@ -337,6 +342,10 @@ __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, flo
     }
     lo = ray.d.z != 0.f ? lz : lo;
     hi = ray.d.z != 0.f ? hz : hi;
+    if (CONS) {
+        lo = lo - (WALK_MARGIN_REL * __builtin_fabsf(lo) + WALK_MARGIN_ABS);
+        hi = hi + (WALK_MARGIN_REL * __builtin_fabsf(hi) + WALK_MARGIN_ABS);
+    }
     return lo > hi || lo > tmax || hi < ray.tmin;
 }
 
@@ -368,9 +377,30 @@ __device__ __forceinline__ bool ranked_leaf_test(const Node& nd, const RayK& ray
     return true;
 }
 
-template <bool STATS, bool FAST>
-__device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_nodes, const RayK& ray, Hit& h,
-                                      int& code_out, Counters& cnt) {
+// Object::GetAABBMin/Max (object.cu:134-170) of a leaf's primitive, as the host computes it.
+__device__ __forceinline__ void leaf_aabb(const Node& nd, Node& box) {
+    const float tol = 2e-5f * 5.f;
+    const int type = nd.code & 3;
+    const float r = nd.b0 >= 0 ? nd.b0 : -nd.b0;
+    if (type == 0) {
+        box.a0 = nd.a0 - r; box.a1 = nd.a1 - r; box.a2 = nd.a2 - r;
+        box.b0 = nd.a0 + r; box.b1 = nd.a1 + r; box.b2 = nd.a2 + r;
+    } else if (type == 1) {
+        box.a0 = -1e30f * 5; box.a1 = nd.b1 - tol; box.a2 = -1e30f * 5;
+        box.b0 = 1e30f * 5; box.b1 = nd.b1 + tol; box.b2 = 1e30f * 5;
+    } else if (type == 2) {
+        box.a0 = nd.a0 - r; box.a1 = nd.a1 - nd.b2 / 2 - tol; box.a2 = nd.a2 - r;
+        box.b0 = nd.a0 + r; box.b1 = nd.a1 + nd.b2 / 2 + tol; box.b2 = nd.a2 + r;
+    } else {
+        box.a0 = box.a1 = box.a2 = box.b0 = box.b1 = box.b2 = 0.f;
+    }
+}
+
+// Returns 1 on a hit, 0 on a miss, and -1 (CONS only) when the winner's certificate fails:
+// the caller then walks the reference order instead.
+template <bool STATS, bool FAST, bool CONS = false>
+__device__ __forceinline__ int trace(const Node* __restrict__ nodes, int n_nodes, const RayK& ray, Hit& h,
+                                     int& code_out, Counters& cnt) {
     float tmax = DEFAULT_RAY_TMAX;
     int best = -1, kind = 0;
     int best_rank = 0x7fffffff;   // reference-order position of the current closest primitive
@@ -404,7 +434,7 @@ __device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_node
             const Node pa = nodes[na < last ? na : last];
             const Node pb = nodes[nb < last ? nb : last];
             if (STATS) cnt.nodes++;
-            const bool take_a = !slab_reject<FAST>(nd, ray, tmax);
+            const bool take_a = !slab_reject<FAST, CONS>(nd, ray, tmax);
             ni = take_a ? na : nb;
             nd = take_a ? pa : pb;
         }
@@ -431,7 +461,7 @@ __device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_node
 #if CPT_STAMPS == 2
         const unsigned long long t1 = stamp();
 #endif
-        if (!leaf) take_a = !slab_reject<FAST>(nd, ray, tmax);
+        if (!leaf) take_a = !slab_reject<FAST, CONS>(nd, ray, tmax);
 #if CPT_STAMPS == 2
         const unsigned long long t2 = stamp();
         cnt.st_leaf += t1 - t0;
@@ -444,11 +474,36 @@ __device__ __forceinline__ bool trace(const Node* __restrict__ nodes, int n_node
 #endif
     }
 #endif
-    if (best < 0) return false;
+    if (best < 0) return 0;
     const Node w = nodes[best];
+    if (CONS) {
+        // Certificate: the winner's own box passes the exact slab test at tmax = t_win.  Its
+        // reference ancestors contain that box, so (slab distances are monotone in the box
+        // planes) they pass at any tmax >= t_win: the reference walk reaches the winner, and
+        // with every primitive it tests also tested here, it keeps the same one.
+        Node box;
+        leaf_aabb(w, box);
+        if (slab_reject<FAST>(box, ray, tmax)) return -1;
+    }
     h = hit_attributes(w, ray, tmax, kind);
     code_out = w.code;
-    return true;
+    return 1;
+}
+
+// TraceRay for one segment: the reference order, or the ordered walk with its certificate
+// and the reference-order fallback (CPT_TRAVERSAL_ORDERED).
+template <bool STATS>
+__device__ __forceinline__ bool trace_segment(const KParams& p, const RayK& rk, bool finite, Hit& h, int& code,
+                                              Counters& cnt) {
+    if (p.ordered && __builtin_expect(finite, 1)) {
+        int n;
+        const Node* order = walk_order(p, rk.d, n);
+        const int r = trace<STATS, true, true>(order, n, rk, h, code, cnt);
+        if (__builtin_expect(r >= 0, 1)) return r > 0;
+        if (STATS) cnt.fallbacks++;
+    }
+    if (__builtin_expect(finite, 1)) return trace<STATS, true>(p.nodes, p.n_nodes, rk, h, code, cnt) > 0;
+    return trace<STATS, false>(p.nodes, p.n_nodes, rk, h, code, cnt) > 0;
 }
 
 // ======================================================================================

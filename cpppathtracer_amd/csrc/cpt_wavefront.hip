@@ -110,10 +110,7 @@ __global__ void __launch_bounds__(256) k_wf_extend(const KParams p, WfState w, c
         int code = -1;
         if (STATS) cnt.segments++;
         bool hit;
-        int n_order;
-        const Node* order = walk_order(p, rk.d, n_order);
-        if (__builtin_expect(finite, 1)) hit = trace<STATS, true>(order, n_order, rk, h, code, cnt);
-        else hit = trace<STATS, false>(order, n_order, rk, h, code, cnt);
+        hit = trace_segment<STATS>(p, rk, finite, h, code, cnt);
         w.hit_p[pix] = make_float4(h.pos.x, h.pos.y, h.pos.z, __int_as_float(hit ? code : -1));
         if (hit) w.hit_n[pix] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.f);
     }
@@ -124,6 +121,8 @@ __global__ void __launch_bounds__(256) k_wf_extend(const KParams p, WfState w, c
             atomicAdd((unsigned long long*)&p.stats[1], (unsigned long long)b);
             atomicAdd((unsigned long long*)&p.stats[2], (unsigned long long)c);
         }
+        const uint64_t f = wave_sum(cnt.fallbacks);   // ordered walk: certificate fallbacks
+        if ((threadIdx.x & 63) == 0 && f) atomicAdd((unsigned long long*)&p.stats[5], (unsigned long long)f);
     }
 }
 

@@ -209,8 +209,9 @@ int cpt_read_aux(cpt_ctx* ctx, float* normal3, float* depth); /* either may be N
 int cpt_copy_accum_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
 int cpt_get_stats(cpt_ctx* ctx, cpt_stats* out);
 int cpt_reset_stats(cpt_ctx* ctx);
-/* All 8 raw device counters (0-4 = cpt_stats; 5-7 = per-phase cycle sums of a CPT_STAMPS
- * diagnostic build: refill, traversal, shading). */
+/* All 8 raw device counters (0-4 = cpt_stats; 5 = ordered-walk segments that failed the
+ * winner certificate and took the reference walk (CPT_RENDER_STATS | CPT_TRAVERSAL_ORDERED);
+ * 5-7 in a CPT_STAMPS diagnostic build: refill, traversal, shading cycle sums). */
 int cpt_get_raw_counters(cpt_ctx* ctx, uint64_t* out8);
 /* Device time of the last cpt_render (HIP events on the launch stream); waits for it. */
 int cpt_last_render_ms(cpt_ctx* ctx, float* ms);

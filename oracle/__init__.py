@@ -73,6 +73,8 @@ def lib():
         L.or_bind_texture.restype = None
         L.or_clear_textures.argtypes = []
         L.or_clear_textures.restype = None
+        L.or_last_fallbacks.argtypes = []
+        L.or_last_fallbacks.restype = u64
         L.or_set_walk.argtypes = [i32]
         L.or_set_walk.restype = None
         _lib = L
@@ -169,6 +171,11 @@ def bind_texture(handle, tex, address_mode=2, filter_mode=1):
 
 def clear_textures():
     lib().or_clear_textures()
+
+
+def last_fallbacks() -> int:
+    """DIAGNOSTIC: certificate fallbacks of the last render() in the ordered walk."""
+    return int(lib().or_last_fallbacks())
 
 
 def set_walk(ordered: bool):

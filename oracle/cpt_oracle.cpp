@@ -534,9 +534,11 @@ struct Bvh {
     // diagnostic ordered walk only (trace_ray_ordered):
     std::vector<int> axis;       // split axis per internal node
     std::vector<int> rank;       // right-first preorder position
-    std::vector<Node> walk;      // the tree with the unbounded (platform) leaves spliced out
+    struct WNode { f3 bmin, bmax; int left, right, obj, axis; };
+    std::vector<WNode> walk;     // binned-SAH tree over the bounded primitives
     int walk_root = -1;
-    std::vector<int> unbounded;  // spliced-out leaves, by rank
+    std::vector<int> unbounded;  // platform leaves of `walk`, by rank
+    std::vector<int> rank_of_obj;
 };
 
 // std::sort in the reference (bvh.cu:67-80) is unstable; ties between equal centroids are
@@ -608,37 +610,110 @@ void build_bvh(Bvh& bvh, const Object* objs, int n) {
     build_walk_tree(bvh);
 }
 
-// Walk tree of the diagnostic ordered walk: each platform leaf is removed, its sibling takes
-// its parent's place and the ancestors' boxes are refit (MIN/MAX of the children).
-void build_walk_tree(Bvh& bvh) {
-    const Object* objs = bvh.objs;
-    const int n = (int)bvh.nodes.size();
-    bvh.walk = bvh.nodes;
-    bvh.walk_root = n > 0 ? 0 : -1;
-    bvh.unbounded.clear();
-    std::vector<int> parent(bvh.walk.size(), -1);
-    for (size_t i = 0; i < bvh.walk.size(); ++i)
-        if (!bvh.walk[i].is_object) { parent[bvh.walk[i].left] = (int)i; parent[bvh.walk[i].right] = (int)i; }
-    std::vector<int> order(bvh.walk.size());
-    for (size_t i = 0; i < order.size(); ++i) order[bvh.rank[i]] = (int)i;
-    for (int i : order) {
-        if (!bvh.walk[i].is_object || objs[bvh.walk[i].obj].type != PRIM_PLATFORM) continue;
-        bvh.unbounded.push_back(i);
-        int p = parent[i];
-        if (p < 0) { bvh.walk_root = -1; continue; }
-        int sib = bvh.walk[p].left == i ? bvh.walk[p].right : bvh.walk[p].left;
-        int gp = parent[p];
-        parent[sib] = gp;
-        if (gp < 0) bvh.walk_root = sib;
-        else if (bvh.walk[gp].left == p) bvh.walk[gp].left = sib;
-        else bvh.walk[gp].right = sib;
-        for (int a = gp; a >= 0; a = parent[a]) {
-            Node& A = bvh.walk[a];
-            const Node &L = bvh.walk[A.left], &R = bvh.walk[A.right];
-            A.bmin = mk(MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z));
-            A.bmax = mk(MAX_(L.bmax.x, R.bmax.x), MAX_(L.bmax.y, R.bmax.y), MAX_(L.bmax.z, R.bmax.z));
+// Walk tree of the diagnostic ordered walk: platforms (unbounded) are tested first; the other
+// primitives get a binned-SAH tree (16 bins per axis, one primitive per leaf), built with the
+// same float operations as libcpt's host builder (cpt_capi.cpp, namespace sah).
+namespace walk_sah {
+constexpr int NB = 16;
+inline float comp(f3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+inline f3 fmin3(f3 a, f3 b) { return mk(MIN_(a.x, b.x), MIN_(a.y, b.y), MIN_(a.z, b.z)); }
+inline f3 fmax3(f3 a, f3 b) { return mk(MAX_(a.x, b.x), MAX_(a.y, b.y), MAX_(a.z, b.z)); }
+inline float area(f3 lo, f3 hi) {
+    float dx = hi.x - lo.x, dy = hi.y - lo.y, dz = hi.z - lo.z;
+    return 2.f * (dx * dy + dy * dz + dz * dx);
+}
+inline int bin_of(float c, float e0, float e1) { return std::min(NB - 1, (int)((c - e0) / (e1 - e0) * NB)); }
+
+int leaf(Bvh& b, int o) {
+    Bvh::WNode n;
+    n.bmin = aabb_min(b.objs[o]);
+    n.bmax = aabb_max(b.objs[o]);
+    n.left = n.right = -1;
+    n.obj = o;
+    n.axis = 0;
+    b.walk.push_back(n);
+    return (int)b.walk.size() - 1;
+}
+
+int build(Bvh& b, std::vector<int>& idx, int l, int r) {
+    const Object* O = b.objs;
+    if (r - l == 1) return leaf(b, idx[l]);
+    f3 lo = aabb_min(O[idx[l]]), hi = aabb_max(O[idx[l]]);
+    f3 clo = mk(1e30f, 1e30f, 1e30f), chi = mk(-1e30f, -1e30f, -1e30f);
+    std::vector<float> cen(3 * (r - l));
+    for (int i = l; i < r; ++i) {
+        f3 a = aabb_min(O[idx[i]]), c2 = aabb_max(O[idx[i]]);
+        lo = fmin3(lo, a);
+        hi = fmax3(hi, c2);
+        f3 c = mk((a.x + c2.x) * .5f, (a.y + c2.y) * .5f, (a.z + c2.z) * .5f);
+        cen[3 * (i - l)] = c.x; cen[3 * (i - l) + 1] = c.y; cen[3 * (i - l) + 2] = c.z;
+        clo = fmin3(clo, c);
+        chi = fmax3(chi, c);
+    }
+    float best = 3.0e38f;
+    int best_axis = -1, best_bin = -1;
+    for (int axis = 0; axis < 3; ++axis) {
+        float e0 = comp(clo, axis), e1 = comp(chi, axis);
+        if (!(e1 > e0)) continue;
+        int cnt[NB] = {0};
+        f3 blo[NB], bhi[NB];
+        for (int k = 0; k < NB; ++k) { blo[k] = mk(1e30f, 1e30f, 1e30f); bhi[k] = mk(-1e30f, -1e30f, -1e30f); }
+        for (int i = l; i < r; ++i) {
+            int k = bin_of(cen[3 * (i - l) + axis], e0, e1);
+            cnt[k]++;
+            blo[k] = fmin3(blo[k], aabb_min(O[idx[i]]));
+            bhi[k] = fmax3(bhi[k], aabb_max(O[idx[i]]));
+        }
+        for (int sp = 1; sp < NB; ++sp) {
+            int nl = 0, nr = 0;
+            f3 llo = mk(1e30f, 1e30f, 1e30f), lhi = mk(-1e30f, -1e30f, -1e30f), rlo = llo, rhi = lhi;
+            for (int k = 0; k < sp; ++k) if (cnt[k]) { nl += cnt[k]; llo = fmin3(llo, blo[k]); lhi = fmax3(lhi, bhi[k]); }
+            for (int k = sp; k < NB; ++k) if (cnt[k]) { nr += cnt[k]; rlo = fmin3(rlo, blo[k]); rhi = fmax3(rhi, bhi[k]); }
+            if (!nl || !nr) continue;
+            float cost = area(llo, lhi) * nl + area(rlo, rhi) * nr;
+            if (cost < best) { best = cost; best_axis = axis; best_bin = sp; }
         }
     }
+    int axis, mid;
+    if (best_axis < 0) {
+        axis = 0;
+        mid = (l + r) / 2;
+    } else {
+        axis = best_axis;
+        float e0 = comp(clo, axis), e1 = comp(chi, axis);
+        std::vector<int> lhs, rhs;
+        for (int i = l; i < r; ++i) (bin_of(cen[3 * (i - l) + axis], e0, e1) < best_bin ? lhs : rhs).push_back(idx[i]);
+        std::copy(lhs.begin(), lhs.end(), idx.begin() + l);
+        std::copy(rhs.begin(), rhs.end(), idx.begin() + l + (int)lhs.size());
+        mid = l + (int)lhs.size();
+    }
+    int me = (int)b.walk.size();
+    b.walk.push_back(Bvh::WNode{});
+    int L = build(b, idx, l, mid), R = build(b, idx, mid, r);
+    Bvh::WNode& n = b.walk[me];
+    n.bmin = lo; n.bmax = hi;
+    n.left = L; n.right = R; n.obj = -1; n.axis = axis;
+    return me;
+}
+}  // namespace walk_sah
+
+void build_walk_tree(Bvh& bvh) {
+    const int n_obj = (int)(bvh.nodes.empty() ? 0 : (bvh.nodes.size() + 1) / 2);
+    bvh.walk.clear();
+    bvh.unbounded.clear();
+    bvh.walk_root = -1;
+    bvh.rank_of_obj.assign(n_obj, 0);
+    for (size_t i = 0; i < bvh.nodes.size(); ++i)
+        if (bvh.nodes[i].is_object) bvh.rank_of_obj[bvh.nodes[i].obj] = bvh.rank[i];
+    std::vector<std::pair<int, int>> flat;
+    std::vector<int> idx;
+    for (int o = 0; o < n_obj; ++o) {
+        if (bvh.objs[o].type == PRIM_PLATFORM) flat.emplace_back(bvh.rank_of_obj[o], o);
+        else idx.push_back(o);
+    }
+    std::sort(flat.begin(), flat.end());
+    for (auto& f : flat) bvh.unbounded.push_back(walk_sah::leaf(bvh, f.second));
+    if (!idx.empty()) bvh.walk_root = walk_sah::build(bvh, idx, 0, (int)idx.size());
 }
 
 // ---------------------------------------------------------------------------------------
@@ -746,13 +821,14 @@ bool intersection_test(const Object& o, Ray& ray, Attr& attr) {  // object.cu:11
     }
 }
 
-struct Stats { uint64_t segments, nodes, prims, hits, misses; };
+struct Stats { uint64_t segments, nodes, prims, hits, misses, fallbacks; };
 
 // SceneBVH::TraceRay (bvh.cu:167-205): DFS, explicit stack, leaf test before slab test,
 // left pushed before right (right popped first), ray taken BY VALUE.
 bool slab_pass(const Node& n, const Ray& ray);
 bool trace_ray_ordered(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st);
 static int g_walk_ordered = 0;
+static std::atomic<uint64_t> g_last_fallbacks{0};   // diagnostic walk: certificate fallbacks of the last render
 // Diagnostic hook for walk experiments compiled against this file (never set by the library).
 static bool (*g_trace_hook)(const Bvh&, Ray, Attr&, int&, Stats&) = nullptr;
 
@@ -828,42 +904,71 @@ bool slab_pass(const Node& n, const Ray& ray) {                 // bvh.cu:181-20
     return !(local_tmin > local_tmax || local_tmin > ray.tmax || local_tmax < ray.tmin);
 }
 
+bool slab_pass_conservative(const Bvh::WNode& n, const Ray& ray) {
+    float lo = -DEFAULT_RAY_TMAX * 2, hi = DEFAULT_RAY_TMAX * 2;
+    const float o[3] = {ray.origin.x, ray.origin.y, ray.origin.z}, d[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
+    const float a[3] = {n.bmin.x, n.bmin.y, n.bmin.z}, b[3] = {n.bmax.x, n.bmax.y, n.bmax.z};
+    for (int k = 0; k < 3; ++k) {
+        if (d[k] == 0.f) continue;
+        float t0 = (a[k] - o[k]) / d[k], t1 = (b[k] - o[k]) / d[k];
+        lo = MAX_(lo, MIN_(t0, t1));
+        hi = MIN_(hi, MAX_(t0, t1));
+    }
+    lo = lo - (1e-3f * fabsf(lo) + 1e-4f);
+    hi = hi + (1e-3f * fabsf(hi) + 1e-4f);
+    return !(lo > hi || lo > ray.tmax || hi < ray.tmin);
+}
+
 bool trace_ray_ordered(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st) {
+    const Ray ray0 = ray;   // TraceRay's by-value ray, for the fallback
     bool ret = false;
-    int best_rank = 0x7fffffff;
-    auto leaf = [&](int ni) {
+    int best_rank = 0x7fffffff, win = -1;
+    auto leaf = [&](int wi) {
+        const int o = bvh.walk[wi].obj;
         st.nodes++;
         st.prims++;
         Ray r2 = ray;
-        if (bvh.rank[ni] < best_rank) {
+        if (bvh.rank_of_obj[o] < best_rank) {
             uint32_t u;
             std::memcpy(&u, &r2.tmax, 4);
             u += 1;
             std::memcpy(&r2.tmax, &u, 4);
         }
-        if (intersection_test(bvh.objs[bvh.walk[ni].obj], r2, attr)) {
+        if (intersection_test(bvh.objs[o], r2, attr)) {
             ray.tmax = r2.tmax;
-            hit_obj = bvh.walk[ni].obj;
-            best_rank = bvh.rank[ni];
+            hit_obj = o;
+            win = o;
+            best_rank = bvh.rank_of_obj[o];
             ret = true;
         }
     };
-    for (int ni : bvh.unbounded) leaf(ni);
-    if (bvh.walk_root < 0) return ret;
-    int stack[512];
-    int top = 0;
-    stack[top++] = bvh.walk_root;
-    const float d[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
-    while (top > 0) {
-        int ni = stack[--top];
-        const Node& n = bvh.walk[ni];
-        if (n.is_object) { leaf(ni); continue; }
-        st.nodes++;
-        if (!slab_pass(n, ray)) continue;
-        if (top + 2 > 512) return ret;
-        const bool right_first = d[bvh.axis[ni]] < 0.f;
-        stack[top++] = right_first ? n.left : n.right;
-        stack[top++] = right_first ? n.right : n.left;
+    for (int wi : bvh.unbounded) leaf(wi);
+    if (bvh.walk_root >= 0) {
+        int stack[512];
+        int top = 0;
+        stack[top++] = bvh.walk_root;
+        const float d[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
+        while (top > 0) {
+            int wi = stack[--top];
+            const Bvh::WNode& n = bvh.walk[wi];
+            if (n.obj >= 0) { leaf(wi); continue; }
+            st.nodes++;
+            if (!slab_pass_conservative(n, ray)) continue;
+            if (top + 2 > 512) break;
+            const bool right_first = d[n.axis] < 0.f;
+            stack[top++] = right_first ? n.left : n.right;
+            stack[top++] = right_first ? n.right : n.left;
+        }
+    }
+    if (win >= 0) {
+        // certificate: the winner's own box passes the exact slab test at tmax = t_win
+        Node box;
+        box.bmin = aabb_min(bvh.objs[win]);
+        box.bmax = aabb_max(bvh.objs[win]);
+        if (!slab_pass(box, ray)) {
+            st.fallbacks++;
+            return trace_ray_ref(bvh, ray0, attr, hit_obj, st);
+        }
     }
     return ret;
 }
@@ -1151,6 +1256,8 @@ void or_clear_textures(void) {
     g_textures.clear();
 }
 
+uint64_t or_last_fallbacks(void) { return g_last_fallbacks; }
+
 void or_set_walk(int ordered) { g_walk_ordered = ordered ? 1 : 0; }   // diagnostic, see trace_ray_ordered
 
 int or_sizeof(int which) {
@@ -1309,16 +1416,19 @@ static int render_with(Bvh& bvh, const void* camera, const uint8_t* env_rgba, in
     J.rng = rng_planar; J.accum = accum; J.normal = normal_out; J.depthbuf = depth_out;
     J.accumulate = accumulate;
     if (nthreads < 1) nthreads = 1;
-    std::vector<Stats> st(nthreads, Stats{0, 0, 0, 0, 0});
+    std::vector<Stats> st(nthreads, Stats{0, 0, 0, 0, 0, 0});
     std::vector<std::thread> th;
     for (int t = 1; t < nthreads; ++t) th.emplace_back([&, t] { render_rows(J, t, nthreads, st[t]); });
     render_rows(J, 0, nthreads, st[0]);
     for (auto& x : th) x.join();
     if (stats5) {
-        Stats s{0, 0, 0, 0, 0};
+        Stats s{0, 0, 0, 0, 0, 0};
         for (auto& x : st) { s.segments += x.segments; s.nodes += x.nodes; s.prims += x.prims; s.hits += x.hits; s.misses += x.misses; }
         stats5[0] = s.segments; stats5[1] = s.nodes; stats5[2] = s.prims; stats5[3] = s.hits; stats5[4] = s.misses;
     }
+    uint64_t fb = 0;
+    for (auto& x : st) fb += x.fallbacks;
+    g_last_fallbacks = fb;
     return 0;
 }
 

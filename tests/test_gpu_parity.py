@@ -87,6 +87,8 @@ def _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, rows=None, seed=1234
     gpu.reset_stats()
     gpu.render(cam, spp, depth, aux=aux, stats=True, sync=True, **_kw(path))
     g_acc, g_rng, g_st = gpu.read_accum(), gpu.read_rng(), gpu.stats()
+    if _kw(path)["ordered"]:
+        g_st["fallbacks"] = gpu.raw_counters()[5]
     g_aux = gpu.read_aux() if aux else None
     rng = oracle_mod.init_rng(seed, W, rows, threads=8)
     o_acc, o_st, o_n, o_d = oracle_mod.render(objs, cam, sky if env else None, rows, spp, depth, rng,
@@ -98,6 +100,7 @@ def _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, rows=None, seed=1234
         oracle_mod.set_walk(True)
         try:
             w_acc, w_st, _, _ = oracle_mod.render(objs, cam, sky if env else None, rows, spp, depth, rng2, threads=8)
+            w_st["fallbacks"] = oracle_mod.last_fallbacks()
         finally:
             oracle_mod.set_walk(False)
         np.testing.assert_array_equal(w_acc.view(np.uint32), o_acc.view(np.uint32))
@@ -123,7 +126,8 @@ CASES = [
 
 # "<path>:ordered" = the near-first octant walk (CPT_TRAVERSAL_ORDERED): same closest hits,
 # so the same images, RNG end states and segment/hit/miss counts; its node/prim counts are its
-# own and equal the oracle's diagnostic restatement of the ordered walk (oracle.set_walk).
+# own and equal the oracle's diagnostic restatement of the ordered walk (oracle.set_walk),
+# including the number of segments whose winner certificate failed (reference-walk fallback).
 PATHS = ["megakernel", "wavefront", "megakernel:ordered", "wavefront:ordered"]
 
 
@@ -291,6 +295,8 @@ def test_update_object_refit(gpu, oracle_mod, sky, path):
     gpu.reset_stats()
     gpu.render(cam, spp, depth, stats=True, sync=True, **_kw(path))
     ga, gs = gpu.read_accum(), gpu.stats()
+    if _kw(path)["ordered"]:
+        gs["fallbacks"] = gpu.raw_counters()[5]
     rows = np.arange(H, dtype=np.int32)
     rng = oracle_mod.init_rng(11, W, rows, threads=8)
     oa, os_ = oracle_mod.render_edited(objs, edits, cam, sky, rows, spp, depth, rng, threads=8)
@@ -299,6 +305,7 @@ def test_update_object_refit(gpu, oracle_mod, sky, path):
         try:
             _, w_st = oracle_mod.render_edited(objs, edits, cam, sky, rows, spp, depth,
                                                oracle_mod.init_rng(11, W, rows, threads=8), threads=8)
+            w_st["fallbacks"] = oracle_mod.last_fallbacks()
         finally:
             oracle_mod.set_walk(False)
         os_ = dict(os_, walk=w_st)

@@ -12,6 +12,10 @@
 //   3  as 2 on a binned-SAH tree over the bounded primitives (1 primitive per leaf)
 //   4  the reference tree with the unbounded leaves spliced out (sibling promoted, the
 //      ancestors' boxes refit); every other node keeps the reference's box
+//   5  as 3 (SAH), with a conservative slab test (relative margin LAB_MARGIN) and a winner
+//      certificate: the winner's own AABB must pass the exact slab test at t = t_win, else
+//      the segment falls back to the reference walk (counted)
+//   6  as 4, with the margin and the certificate of mode 5
 #include "../oracle/cpt_oracle.cpp"
 
 namespace lab {
@@ -29,6 +33,8 @@ struct Tree {
 };
 
 int g_mode = 0;
+float g_margin = 1e-3f;
+std::atomic<uint64_t> g_fallback{0};
 Tree g_tree;
 std::atomic<uint64_t> g_nodes{0}, g_prims{0}, g_segments{0}, g_diff{0}, g_diff_obj{0};
 std::mutex g_mu;
@@ -137,7 +143,7 @@ void prepare(const Bvh& bvh) {
     for (const Node& n : bvh.nodes) if (n.is_object) n_obj = std::max(n_obj, n.obj + 1);
     t.rank_of_obj.assign(n_obj, 0);
     for (size_t i = 0; i < bvh.nodes.size(); ++i) if (bvh.nodes[i].is_object) t.rank_of_obj[bvh.nodes[i].obj] = bvh.rank[i];
-    if (g_mode == 1 || g_mode == 4) {
+    if (g_mode == 1 || g_mode == 4 || g_mode == 6) {
         for (const Node& n : bvh.nodes) {
             ANode a;
             a.bmin = n.bmin; a.bmax = n.bmax; a.left = n.left; a.right = n.right;
@@ -146,7 +152,7 @@ void prepare(const Bvh& bvh) {
         }
         for (size_t i = 0; i < bvh.nodes.size(); ++i) t.nodes[i].axis = bvh.axis[i];
         t.root = 0;
-        if (g_mode == 4) {
+        if (g_mode == 4 || g_mode == 6) {
             std::vector<int> parent(t.nodes.size(), -1);
             for (size_t i = 0; i < t.nodes.size(); ++i)
                 if (t.nodes[i].obj < 0) { parent[t.nodes[i].left] = (int)i; parent[t.nodes[i].right] = (int)i; }
@@ -186,7 +192,19 @@ void prepare(const Bvh& bvh) {
 bool slab_ok(const ANode& n, const Ray& ray) {
     Node m;
     m.bmin = n.bmin; m.bmax = n.bmax;
-    return slab_pass(m, ray);
+    if (g_mode < 5) return slab_pass(m, ray);
+    // conservative: the reference's slab interval widened by a relative margin
+    float lo = -DEFAULT_RAY_TMAX * 2, hi = DEFAULT_RAY_TMAX * 2;
+    const float o[3] = {ray.origin.x, ray.origin.y, ray.origin.z}, d[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
+    const float a[3] = {n.bmin.x, n.bmin.y, n.bmin.z}, b[3] = {n.bmax.x, n.bmax.y, n.bmax.z};
+    for (int k = 0; k < 3; ++k) {
+        if (d[k] == 0.f) continue;
+        float t0 = (a[k] - o[k]) / d[k], t1 = (b[k] - o[k]) / d[k];
+        lo = MAX_(lo, MIN_(t0, t1));
+        hi = MIN_(hi, MAX_(t0, t1));
+    }
+    const float ml = g_margin * fabsf(lo) + 1e-4f, mh = g_margin * fabsf(hi) + 1e-4f;
+    return !(lo - ml > hi + mh || lo - ml > ray.tmax || hi + mh < ray.tmin);
 }
 
 bool alt_trace(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, uint64_t& nodes, uint64_t& prims) {
@@ -232,7 +250,26 @@ bool hook(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st) {
     int h2 = -1;
     uint64_t nodes = 0, prims = 0;
     bool r2 = alt_trace(bvh, ray, a2, h2, nodes, prims);
+    const Attr a_in = attr;
     bool r = trace_ray_ref(bvh, ray, attr, hit_obj, st);
+    if (g_mode >= 5 && r2) {
+        // certificate: the winner's own AABB passes the exact slab test at tmax = t_win
+        Node m;
+        m.bmin = aabb_min(bvh.objs[h2]);
+        m.bmax = aabb_max(bvh.objs[h2]);
+        Ray rc = ray;
+        // t_win from the hit position is not exact; recompute by re-testing the winner alone
+        Attr tmp = a_in;
+        rc.tmax = DEFAULT_RAY_TMAX;
+        Ray rw = ray;
+        rw.tmax = DEFAULT_RAY_TMAX;
+        intersection_test(bvh.objs[h2], rw, tmp);
+        rc.tmax = rw.tmax;
+        if (!slab_pass(m, rc)) {
+            g_fallback++;
+            r2 = r; h2 = hit_obj; a2 = attr;   // fallback: the reference walk's result
+        }
+    }
     g_nodes += nodes;
     g_prims += prims;
     g_segments++;
@@ -252,13 +289,15 @@ bool hook(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st) {
 }  // namespace lab
 
 extern "C" {
+void lab_set_margin(float m) { lab::g_margin = m; }
 void lab_set_mode(int m) {
     lab::g_mode = m;
     lab::g_src = nullptr;
     g_trace_hook = m ? lab::hook : nullptr;
 }
-void lab_counts(uint64_t out[5]) {
+void lab_counts(uint64_t out[6]) {
     out[0] = lab::g_segments; out[1] = lab::g_nodes; out[2] = lab::g_prims; out[3] = lab::g_diff; out[4] = lab::g_diff_obj;
-    lab::g_segments = lab::g_nodes = lab::g_prims = lab::g_diff = lab::g_diff_obj = 0;
+    out[5] = lab::g_fallback;
+    lab::g_segments = lab::g_nodes = lab::g_prims = lab::g_diff = lab::g_diff_obj = lab::g_fallback = 0;
 }
 }

@@ -24,6 +24,8 @@ def main():
     L = oracle.lib()
     L.lab_set_mode.argtypes = [ctypes.c_int]
     L.lab_counts.argtypes = [ctypes.c_void_p]
+    L.lab_set_margin.argtypes = [ctypes.c_float]
+    L.lab_set_margin(float(os.environ.get("LAB_MARGIN", "1e-3")))
     from cpppathtracer_amd import camera_get_copy, scenes, texture_io
     sky = texture_io.load_cptex()
     objs = scenes.scene_s1000()
@@ -34,14 +36,14 @@ def main():
         rng = oracle.init_rng(1234, W, rows, threads=8)
         t = time.time()
         _, st, _, _ = oracle.render(objs, cam, sky, rows, spp, 16, rng, threads=8)
-        c = np.zeros(5, np.uint64)
+        c = np.zeros(6, np.uint64)
         L.lab_counts(c.ctypes.data)
         if mode == 0:
             print(f"reference: {st['segments']} segments, {st['nodes'] / st['segments']:.2f} nodes/seg, "
                   f"{st['prims'] / st['segments']:.2f} prims/seg")
         else:
             print(f"mode {mode}: {c[1] / c[0]:.2f} nodes/seg, {c[2] / c[0]:.2f} prims/seg, "
-                  f"diff {int(c[3])} (obj {int(c[4])}) of {int(c[0])} [{time.time() - t:.1f}s]")
+                  f"diff {int(c[3])} (obj {int(c[4])}) fallback {int(c[5])} of {int(c[0])} [{time.time() - t:.1f}s]")
     L.lab_set_mode(0)
 
 
