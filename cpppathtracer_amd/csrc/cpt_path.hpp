@@ -104,6 +104,8 @@ struct RayK {
     double yx, yy, yz;   // 1/d.x, 1/d.y, 1/d.z   (slab planes; d.y also for caps / platform)
     double ya;           // 1/dot(d,d)            (sphere roots, object.cu:15-20)
     double yc;           // 1/(dx*dx + dz*dz)     (cylinder side roots, object.cu:69-79)
+    float ix, iy, iz;    // f32 1/d per axis for the ordered walk's conservative slabs; 0 = the
+                         // axis is skipped (|d| < 1e-30: no constraint, which only widens)
 };
 
 __device__ __forceinline__ RayK make_rayk(const Ray& r) {
@@ -116,6 +118,9 @@ __device__ __forceinline__ RayK make_rayk(const Ray& r) {
     k.yz = rcp_d(r.d.z);
     k.ya = rcp_d(dot(r.d, r.d));
     k.yc = rcp_d(r.d.x * r.d.x + r.d.z * r.d.z);
+    k.ix = __builtin_fabsf(r.d.x) >= 1e-30f ? 1.0f / r.d.x : 0.0f;
+    k.iy = __builtin_fabsf(r.d.y) >= 1e-30f ? 1.0f / r.d.y : 0.0f;
+    k.iz = __builtin_fabsf(r.d.z) >= 1e-30f ? 1.0f / r.d.z : 0.0f;
     return k;
 }
 
@@ -290,13 +295,33 @@ struct Counters {
 // (finite box coordinate minus finite origin, times a finite reciprocal), so the ternary
 // MIN/MAX of the reference equal v_min/v_max_f32 up to the sign of a zero, which none of
 // the three comparisons can see.  Rays carrying a NaN take the exact ternary form.
-// CONS (the ordered walk's tree): the same interval, widened by a relative margin before the
-// three comparisons, so that a primitive whose computed hit lies slightly outside its box by
-// rounding is still tested (DESIGN.md §Ordered walk).
+// CONS (the ordered walk's tree): the interval from f32 reciprocals (no exactness needed),
+// widened by a relative margin before the three comparisons, so that a primitive whose
+// computed hit lies slightly outside its box by rounding is still tested (DESIGN.md
+// §Ordered walk).  The margin dwarfs the reciprocal's few-ulp error.
 constexpr float WALK_MARGIN_REL = 1e-3f, WALK_MARGIN_ABS = 1e-4f;
 
 template <bool FAST, bool CONS = false>
 __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, float tmax) {
+    if (CONS) {
+        // (b - o) * (1/d): a few ulps from the exact quotient, far inside the margin; axes
+        // with ix == 0 impose nothing.  All operands finite (FAST rays only), no NaN.
+        const float BIG = DEFAULT_RAY_TMAX * 2;
+        const float t0x = (nd.a0 - ray.o.x) * ray.ix, t1x = (nd.b0 - ray.o.x) * ray.ix;
+        const float t0y = (nd.a1 - ray.o.y) * ray.iy, t1y = (nd.b1 - ray.o.y) * ray.iy;
+        const float t0z = (nd.a2 - ray.o.z) * ray.iz, t1z = (nd.b2 - ray.o.z) * ray.iz;
+        const float lx = ray.ix != 0.f ? __builtin_fminf(t0x, t1x) : -BIG;
+        const float hx = ray.ix != 0.f ? __builtin_fmaxf(t0x, t1x) : BIG;
+        const float ly = ray.iy != 0.f ? __builtin_fminf(t0y, t1y) : -BIG;
+        const float hy = ray.iy != 0.f ? __builtin_fmaxf(t0y, t1y) : BIG;
+        const float lz = ray.iz != 0.f ? __builtin_fminf(t0z, t1z) : -BIG;
+        const float hz = ray.iz != 0.f ? __builtin_fmaxf(t0z, t1z) : BIG;
+        float lo = __builtin_fmaxf(__builtin_fmaxf(lx, ly), lz);
+        float hi = __builtin_fminf(__builtin_fminf(hx, hy), hz);
+        lo = lo - (WALK_MARGIN_REL * __builtin_fabsf(lo) + WALK_MARGIN_ABS);
+        hi = hi + (WALK_MARGIN_REL * __builtin_fabsf(hi) + WALK_MARGIN_ABS);
+        return lo > hi || lo > tmax || hi < ray.tmin;
+    }
     float t0x = qdiv_raw(nd.a0 - ray.o.x, ray.yx), t1x = qdiv_raw(nd.b0 - ray.o.x, ray.yx);
     float t0y = qdiv_raw(nd.a1 - ray.o.y, ray.yy), t1y = qdiv_raw(nd.b1 - ray.o.y, ray.yy);
     float t0z = qdiv_raw(nd.a2 - ray.o.z, ray.yz), t1z = qdiv_raw(nd.b2 - ray.o.z, ray.yz);
@@ -342,10 +367,6 @@ __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, flo
     }
     lo = ray.d.z != 0.f ? lz : lo;
     hi = ray.d.z != 0.f ? hz : hi;
-    if (CONS) {
-        lo = lo - (WALK_MARGIN_REL * __builtin_fabsf(lo) + WALK_MARGIN_ABS);
-        hi = hi + (WALK_MARGIN_REL * __builtin_fabsf(hi) + WALK_MARGIN_ABS);
-    }
     return lo > hi || lo > tmax || hi < ray.tmin;
 }
 

@@ -904,16 +904,21 @@ bool slab_pass(const Node& n, const Ray& ray) {                 // bvh.cu:181-20
     return !(local_tmin > local_tmax || local_tmin > ray.tmax || local_tmax < ray.tmin);
 }
 
+// The product's conservative slab (cpt_path.hpp slab_reject<FAST, true>): f32 reciprocals,
+// skipped axes for |d| < 1e-30, interval widened by 1e-3*|t| + 1e-4.
 bool slab_pass_conservative(const Bvh::WNode& n, const Ray& ray) {
-    float lo = -DEFAULT_RAY_TMAX * 2, hi = DEFAULT_RAY_TMAX * 2;
+    const float BIG = DEFAULT_RAY_TMAX * 2;
     const float o[3] = {ray.origin.x, ray.origin.y, ray.origin.z}, d[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
     const float a[3] = {n.bmin.x, n.bmin.y, n.bmin.z}, b[3] = {n.bmax.x, n.bmax.y, n.bmax.z};
+    float l[3], h[3];
     for (int k = 0; k < 3; ++k) {
-        if (d[k] == 0.f) continue;
-        float t0 = (a[k] - o[k]) / d[k], t1 = (b[k] - o[k]) / d[k];
-        lo = MAX_(lo, MIN_(t0, t1));
-        hi = MIN_(hi, MAX_(t0, t1));
+        const float inv = fabsf(d[k]) >= 1e-30f ? 1.0f / d[k] : 0.0f;
+        const float t0 = (a[k] - o[k]) * inv, t1 = (b[k] - o[k]) * inv;
+        l[k] = inv != 0.f ? fminf(t0, t1) : -BIG;
+        h[k] = inv != 0.f ? fmaxf(t0, t1) : BIG;
     }
+    float lo = fmaxf(fmaxf(l[0], l[1]), l[2]);
+    float hi = fminf(fminf(h[0], h[1]), h[2]);
     lo = lo - (1e-3f * fabsf(lo) + 1e-4f);
     hi = hi + (1e-3f * fabsf(hi) + 1e-4f);
     return !(lo > hi || lo > ray.tmax || hi < ray.tmin);
