@@ -245,12 +245,14 @@ def main():
         # algorithmic bytes of one launch on rank 0's pixels: scale whole-image counts by the
         # pixel share (interleaved blocks keep the shares statistically equal)
         share = npix_local / float(W * H)
-        bytes_launch = byte_model(st, paths_total) * share
+        # Algorithmic bytes of one launch (SURVEY.md 8(d) per-unit model x the units the launch
+        # processes): the executed walk's own segment/node/primitive counts.  The same model on
+        # the reference algorithm's counts (its right-first DFS over its median tree, which
+        # visits more nodes for the same closest hits) is reported beside it.
+        bytes_ref = byte_model(st, paths_total) * share
+        bytes_launch = byte_model(walk_counts, paths_total) * share if walk_counts else bytes_ref
         achieved = bytes_launch / (avg_kernel_ms / 1e3) / 1e9
-        # the same per-unit byte model on the executed walk's own node/prim counts (the ordered
-        # walk visits fewer nodes than the reference algorithm for the same closest hits)
-        achieved_walk = (byte_model(walk_counts, paths_total) * share / (avg_kernel_ms / 1e3) / 1e9
-                         if walk_counts else achieved)
+        achieved_ref_model = bytes_ref / (avg_kernel_ms / 1e3) / 1e9
         # HBM traffic per launch from rocprofv3 PMC passes of this same workload (committed under
         # profiles/, made by tools/profile.sh + tools/pmc_traffic.py); null when none matches.
         traffic = None
@@ -288,13 +290,13 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "achieved_walk": round(achieved_walk, 2),
+                "achieved_reference_model": round(achieved_ref_model, 2),
                 "kernel": "k_megakernel" if args.path == "megakernel" else "wavefront (k_wf_extend+k_wf_shade per bounce)",
                 "kernel_avg_ms": round(avg_kernel_ms, 3),
                 "bytes_per_launch": int(bytes_launch),
-                "byte_model": "SURVEY.md 8(d): 76 S + 32 nodes + 32 prims + 40 hits + 16 misses + 16 P",
-                "counts": st,
+                "byte_model": "SURVEY.md 8(d): 76 S + 32 nodes + 32 prims + 40 hits + 16 misses + 16 P, on walk_counts",
                 "walk_counts": walk_counts,
+                "reference_counts": st,
                 "walk_vs_reference_pixels_differing": walk_diff,
             },
             "rng_init_ms": round(t_init * 1e3, 2),

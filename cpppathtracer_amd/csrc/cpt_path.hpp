@@ -390,14 +390,6 @@ __device__ __forceinline__ const Node* walk_order(const KParams& p, v3 d, int& n
 // tie, so it is tested against next_up(tmax): "temp < next_up(tmax)" == "temp <= tmax".  Its
 // first accepted case sets tmax = temp, so its later cases compare strictly, as in the
 // reference.  tmax > 0 always (hits need temp > tmin >= 0), so next_up is the bit pattern + 1.
-__device__ __forceinline__ bool ranked_leaf_test(const Node& nd, const RayK& ray, float& tmax, int& kind, int& best_rank) {
-    float tm = nd.miss < best_rank ? __int_as_float(__float_as_int(tmax) + 1) : tmax;
-    if (!leaf_test(nd, ray, tm, kind)) return false;
-    tmax = tm;
-    best_rank = nd.miss;
-    return true;
-}
-
 // Object::GetAABBMin/Max (object.cu:134-170) of a leaf's primitive, as the host computes it.
 __device__ __forceinline__ void leaf_aabb(const Node& nd, Node& box) {
     const float tol = 2e-5f * 5.f;
@@ -415,6 +407,28 @@ __device__ __forceinline__ void leaf_aabb(const Node& nd, Node& box) {
     } else {
         box.a0 = box.a1 = box.a2 = box.b0 = box.b1 = box.b2 = 0.f;
     }
+}
+
+#ifndef CPT_LEAF_PRETEST
+#define CPT_LEAF_PRETEST 2   // ordered walk: conservative slab test of a leaf's own box before
+                             // its exact test (1 = cylinders, 2 = spheres and cylinders)
+#endif
+
+template <bool FAST, bool CONS>
+__device__ __forceinline__ bool ranked_leaf_test(const Node& nd, const RayK& ray, float& tmax, int& kind, int& best_rank) {
+    float tm = nd.miss < best_rank ? __int_as_float(__float_as_int(tmax) + 1) : tmax;
+    if (CONS && CPT_LEAF_PRETEST) {
+        const int type = nd.code & 3;
+        if (type == 2 || (CPT_LEAF_PRETEST == 2 && type == 0)) {
+            Node box;
+            leaf_aabb(nd, box);
+            if (slab_reject<FAST, true>(box, ray, tm)) return false;
+        }
+    }
+    if (!leaf_test(nd, ray, tm, kind)) return false;
+    tmax = tm;
+    best_rank = nd.miss;
+    return true;
 }
 
 // Returns 1 on a hit, 0 on a miss, and -1 (CONS only) when the winner's certificate fails:
@@ -446,7 +460,7 @@ __device__ __forceinline__ int trace(const Node* __restrict__ nodes, int n_nodes
                 const Node nx = nodes[ni + 1 < last ? ni + 1 : last];
                 if (STATS) { cnt.nodes++; cnt.prims++; }
                 int k;
-                if (ranked_leaf_test(nd, ray, tmax, k, best_rank)) { best = ni; kind = k; }
+                if (ranked_leaf_test<FAST, CONS>(nd, ray, tmax, k, best_rank)) { best = ni; kind = k; }
                 ni = ni + 1;
                 nd = nx;
             }
@@ -477,7 +491,7 @@ __device__ __forceinline__ int trace(const Node* __restrict__ nodes, int n_nodes
             // IntersectionTest first (bvh.cu:175-180); the leaf's own box test is moot
             if (STATS) cnt.prims++;
             int k;
-            if (ranked_leaf_test(nd, ray, tmax, k, best_rank)) { best = ni; kind = k; }
+            if (ranked_leaf_test<FAST, CONS>(nd, ray, tmax, k, best_rank)) { best = ni; kind = k; }
         }
 #if CPT_STAMPS == 2
         const unsigned long long t1 = stamp();

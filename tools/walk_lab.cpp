@@ -34,7 +34,7 @@ struct Tree {
 
 int g_mode = 0;
 float g_margin = 1e-3f;
-std::atomic<uint64_t> g_fallback{0};
+std::atomic<uint64_t> g_fallback{0}, g_pretest_miss{0};
 Tree g_tree;
 std::atomic<uint64_t> g_nodes{0}, g_prims{0}, g_segments{0}, g_diff{0}, g_diff_obj{0};
 std::mutex g_mu;
@@ -193,18 +193,22 @@ bool slab_ok(const ANode& n, const Ray& ray) {
     Node m;
     m.bmin = n.bmin; m.bmax = n.bmax;
     if (g_mode < 5) return slab_pass(m, ray);
-    // conservative: the reference's slab interval widened by a relative margin
-    float lo = -DEFAULT_RAY_TMAX * 2, hi = DEFAULT_RAY_TMAX * 2;
+    // conservative: the product's slab (f32 reciprocals, cpt_path.hpp slab_reject<FAST, true>)
+    const float BIG = DEFAULT_RAY_TMAX * 2;
     const float o[3] = {ray.origin.x, ray.origin.y, ray.origin.z}, d[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
     const float a[3] = {n.bmin.x, n.bmin.y, n.bmin.z}, b[3] = {n.bmax.x, n.bmax.y, n.bmax.z};
+    float l[3], h[3];
     for (int k = 0; k < 3; ++k) {
-        if (d[k] == 0.f) continue;
-        float t0 = (a[k] - o[k]) / d[k], t1 = (b[k] - o[k]) / d[k];
-        lo = MAX_(lo, MIN_(t0, t1));
-        hi = MIN_(hi, MAX_(t0, t1));
+        const float inv = fabsf(d[k]) >= 1e-30f ? 1.0f / d[k] : 0.0f;
+        const float t0 = (a[k] - o[k]) * inv, t1 = (b[k] - o[k]) * inv;
+        l[k] = inv != 0.f ? fminf(t0, t1) : -BIG;
+        h[k] = inv != 0.f ? fmaxf(t0, t1) : BIG;
     }
-    const float ml = g_margin * fabsf(lo) + 1e-4f, mh = g_margin * fabsf(hi) + 1e-4f;
-    return !(lo - ml > hi + mh || lo - ml > ray.tmax || hi + mh < ray.tmin);
+    float lo = fmaxf(fmaxf(l[0], l[1]), l[2]);
+    float hi = fminf(fminf(h[0], h[1]), h[2]);
+    lo = lo - (g_margin * fabsf(lo) + 1e-4f);
+    hi = hi + (g_margin * fabsf(hi) + 1e-4f);
+    return !(lo > hi || lo > ray.tmax || hi < ray.tmin);
 }
 
 bool alt_trace(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, uint64_t& nodes, uint64_t& prims) {
@@ -219,6 +223,25 @@ bool alt_trace(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, uint64_t& node
             std::memcpy(&u, &r2.tmax, 4);
             u += 1;
             std::memcpy(&r2.tmax, &u, 4);
+        }
+        if (g_mode >= 5 && bvh.objs[o].type != PRIM_PLATFORM) {
+            ANode box;
+            box.bmin = aabb_min(bvh.objs[o]);
+            box.bmax = aabb_max(bvh.objs[o]);
+            if (!slab_ok(box, r2)) {
+                Ray r3 = r2;
+                Attr a3 = attr;
+                if (intersection_test(bvh.objs[o], r3, a3)) {
+                    g_pretest_miss++;
+                    std::lock_guard<std::mutex> g(g_mu);
+                    if (g_pretest_miss <= 5)
+                        fprintf(stderr, "pretest-miss: type=%d o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) tmin=%g t=%.9g tmax=%.9g c=(%.9g %.9g %.9g) r=%.9g h=%.9g\n",
+                                bvh.objs[o].type, ray.origin.x, ray.origin.y, ray.origin.z, ray.dir.x, ray.dir.y, ray.dir.z,
+                                ray.tmin, r3.tmax, r2.tmax, bvh.objs[o].center.x, bvh.objs[o].center.y, bvh.objs[o].center.z,
+                                bvh.objs[o].radius, bvh.objs[o].height);
+                }
+                return;
+            }
         }
         if (intersection_test(bvh.objs[o], r2, attr)) {
             ray.tmax = r2.tmax;
@@ -298,6 +321,8 @@ void lab_set_mode(int m) {
 void lab_counts(uint64_t out[6]) {
     out[0] = lab::g_segments; out[1] = lab::g_nodes; out[2] = lab::g_prims; out[3] = lab::g_diff; out[4] = lab::g_diff_obj;
     out[5] = lab::g_fallback;
+    fprintf(stderr, "pretest misses: %llu\n", (unsigned long long)lab::g_pretest_miss.load());
+    lab::g_pretest_miss = 0;
     lab::g_segments = lab::g_nodes = lab::g_prims = lab::g_diff = lab::g_diff_obj = lab::g_fallback = 0;
 }
 }
