@@ -17,7 +17,7 @@ r.set_frame(cfg["width"], cfg["height"])
 r.init_rng(1234)
 cam = camera_get_copy(scenes.camera_for(cfg["width"], cfg["height"]))
 r.reset_stats()
-r.render(cam, spp, cfg["depth"], stats=True, sync=True)
+r.render(cam, spp, cfg["depth"], stats=True, sync=True, ordered=os.environ.get("CPT_WALK", "ordered") == "ordered")
 c = r.raw_counters()
 print("counts", dict(zip(["segments", "nodes", "prims", "hits", "misses"], c[:5])))
 if mode == 1:
