@@ -556,6 +556,9 @@ int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, s
 }
 
 int upload_scene(cpt_ctx* c) {
+    if (c->lin.size() * sizeof(Node) > (size_t)INT32_MAX)   // the walk's buffer descriptor range
+        return fail(c, CPT_ERR_UNSUPPORTED, "scene too large: %zu BVH nodes in all orders (max %zu)", c->lin.size(),
+                    (size_t)INT32_MAX / sizeof(Node));
     HIP_TRY(c, hipSetDevice(c->device));
     int rc;
     if ((rc = ensure(c, &c->d_nodes, &c->cap_nodes, std::max<size_t>(1, c->lin.size()))) != CPT_OK) return rc;

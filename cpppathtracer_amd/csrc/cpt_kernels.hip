@@ -142,8 +142,8 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             const bool finite_ray = !(ray.o.x != ray.o.x || ray.o.y != ray.o.y || ray.o.z != ray.o.z ||
                                       ray.d.x != ray.d.x || ray.d.y != ray.d.y || ray.d.z != ray.d.z);
             bool hit;
-            if (LDS) hit = finite_ray ? trace<STATS, true>(nodes, p.n_nodes, rk, h, code, cnt) > 0
-                                      : trace<STATS, false>(nodes, p.n_nodes, rk, h, code, cnt) > 0;
+            if (LDS) hit = finite_ray ? trace<STATS, true>(PtrSrc{nodes}, p.n_nodes, rk, h, code, cnt) > 0
+                                      : trace<STATS, false>(PtrSrc{nodes}, p.n_nodes, rk, h, code, cnt) > 0;
             else hit = trace_segment<STATS>(p, rk, finite_ray, h, code, cnt);
             t2 = stamp();
             Shade sh;

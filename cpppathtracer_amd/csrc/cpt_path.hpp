@@ -374,14 +374,44 @@ __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, flo
 #define CPT_LEAF_BATCH 0   // K > 0: leaf tests run in wave-uniform leaf phases (see trace)
 #endif
 
+// Node fetch.  BufSrc reads through a buffer descriptor over the whole node array (built from
+// kernel arguments, so it is wave-uniform and lives in SGPRs): a 32-bit per-lane byte offset
+// instead of 64-bit address arithmetic, and out-of-range offsets read 0 instead of needing a
+// clamp (the walk never uses a node past its order's end).  PtrSrc is the plain pointer form
+// (LDS-staged variant).
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+
+struct BufSrc {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t base;   // byte offset of the order's node 0
+    __device__ __forceinline__ Node operator()(uint32_t i) const {
+        const uint32_t off = base + (i << 5);
+        const v4u32 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+        const v4u32 b = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16, 0, 0);
+        Node n;
+        n.a0 = __uint_as_float(a.x); n.a1 = __uint_as_float(a.y); n.a2 = __uint_as_float(a.z); n.miss = (int32_t)a.w;
+        n.b0 = __uint_as_float(b.x); n.b1 = __uint_as_float(b.y); n.b2 = __uint_as_float(b.z); n.code = (int32_t)b.w;
+        return n;
+    }
+};
+
+struct PtrSrc {
+    const Node* __restrict__ p;
+    __device__ __forceinline__ Node operator()(uint32_t i) const { return p[i]; }
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(const KParams& p) {
+    const uint32_t bytes = (uint32_t)(p.n_nodes + 8 * p.n_walk) * (uint32_t)sizeof(Node);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p.nodes, (short)0, (int)bytes, 0x00020000);
+}
+
 // The node order a ray walks: the reference order, or with CPT_TRAVERSAL_ORDERED the walk
 // tree's order for its direction octant (near child of every split first, DESIGN.md
 // §Ordered walk).  Returns the first node and sets the order's length.
-__device__ __forceinline__ const Node* walk_order(const KParams& p, v3 d, int& n) {
-    if (!p.ordered) { n = p.n_nodes; return p.nodes; }
+__device__ __forceinline__ uint32_t walk_order(const KParams& p, v3 d, int& n) {
     const int oct = (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
     n = p.n_walk;
-    return p.nodes + p.n_nodes + (size_t)oct * p.n_walk;
+    return (uint32_t)(p.n_nodes + oct * p.n_walk);   // first node of the octant's order
 }
 
 // Leaf test with the reference's first-found rule for equal distances.  `rank` is the leaf's
@@ -433,16 +463,16 @@ __device__ __forceinline__ bool ranked_leaf_test(const Node& nd, const RayK& ray
 
 // Returns 1 on a hit, 0 on a miss, and -1 (CONS only) when the winner's certificate fails:
 // the caller then walks the reference order instead.
-template <bool STATS, bool FAST, bool CONS = false>
-__device__ __forceinline__ int trace(const Node* __restrict__ nodes, int n_nodes, const RayK& ray, Hit& h,
-                                     int& code_out, Counters& cnt) {
+template <bool STATS, bool FAST, bool CONS = false, typename SRC>
+__device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& ray, Hit& h, int& code_out,
+                                     Counters& cnt) {
     float tmax = DEFAULT_RAY_TMAX;
     int best = -1, kind = 0;
     int best_rank = 0x7fffffff;   // reference-order position of the current closest primitive
     int ni = 0;
-    Node nd;
-    if (n_nodes > 0) nd = nodes[0];
-    const int last = n_nodes - 1;
+    Node nd{};
+    if (n_nodes > 0) nd = nodes(0);
+    [[maybe_unused]] const int last = n_nodes - 1;
 #if CPT_LEAF_BATCH > 0
     // Leaf batching: a lane that reaches a leaf parks there; leaf tests run in a wave-uniform
     // leaf phase once >= 1/K of the walking lanes are parked (or nobody can slab-test).  A
@@ -457,7 +487,7 @@ __device__ __forceinline__ int trace(const Node* __restrict__ nodes, int n_nodes
             (lm == wm || __popcll(lm) * CPT_LEAF_BATCH >= __popcll(wm)) ? 1 : 0);
         if (leaf_phase) {
             if (at_leaf) {
-                const Node nx = nodes[ni + 1 < last ? ni + 1 : last];
+                const Node nx = nodes(ni + 1 < last ? ni + 1 : last);
                 if (STATS) { cnt.nodes++; cnt.prims++; }
                 int k;
                 if (ranked_leaf_test<FAST, CONS>(nd, ray, tmax, k, best_rank)) { best = ni; kind = k; }
@@ -466,8 +496,8 @@ __device__ __forceinline__ int trace(const Node* __restrict__ nodes, int n_nodes
             }
         } else if (walking && !at_leaf) {
             const int na = ni + 1, nb = nd.miss;
-            const Node pa = nodes[na < last ? na : last];
-            const Node pb = nodes[nb < last ? nb : last];
+            const Node pa = nodes(na < last ? na : last);
+            const Node pb = nodes(nb < last ? nb : last);
             if (STATS) cnt.nodes++;
             const bool take_a = !slab_reject<FAST, CONS>(nd, ray, tmax);
             ni = take_a ? na : nb;
@@ -483,8 +513,8 @@ __device__ __forceinline__ int trace(const Node* __restrict__ nodes, int n_nodes
 #endif
         const bool leaf = nd.code >= 0;
         const int na = ni + 1, nb = leaf ? na : nd.miss;
-        const Node pa = nodes[na < last ? na : last];
-        const Node pb = nodes[nb < last ? nb : last];
+        const Node pa = nodes(na);   // past the order's end: never used (the loop ends)
+        const Node pb = nodes(nb);
         if (STATS) cnt.nodes++;
         bool take_a = false;
         if (leaf) {
@@ -510,7 +540,7 @@ __device__ __forceinline__ int trace(const Node* __restrict__ nodes, int n_nodes
     }
 #endif
     if (best < 0) return 0;
-    const Node w = nodes[best];
+    const Node w = nodes(best);
     if (CONS) {
         // Certificate: the winner's own box passes the exact slab test at tmax = t_win.  Its
         // reference ancestors contain that box, so (slab distances are monotone in the box
@@ -530,15 +560,17 @@ __device__ __forceinline__ int trace(const Node* __restrict__ nodes, int n_nodes
 template <bool STATS>
 __device__ __forceinline__ bool trace_segment(const KParams& p, const RayK& rk, bool finite, Hit& h, int& code,
                                               Counters& cnt) {
+    const __amdgpu_buffer_rsrc_t rsrc = node_rsrc(p);
     if (p.ordered && __builtin_expect(finite, 1)) {
         int n;
-        const Node* order = walk_order(p, rk.d, n);
+        const BufSrc order{rsrc, walk_order(p, rk.d, n) * (uint32_t)sizeof(Node)};
         const int r = trace<STATS, true, true>(order, n, rk, h, code, cnt);
         if (__builtin_expect(r >= 0, 1)) return r > 0;
         if (STATS) cnt.fallbacks++;
     }
-    if (__builtin_expect(finite, 1)) return trace<STATS, true>(p.nodes, p.n_nodes, rk, h, code, cnt) > 0;
-    return trace<STATS, false>(p.nodes, p.n_nodes, rk, h, code, cnt) > 0;
+    const BufSrc ref{rsrc, 0u};
+    if (__builtin_expect(finite, 1)) return trace<STATS, true>(ref, p.n_nodes, rk, h, code, cnt) > 0;
+    return trace<STATS, false>(ref, p.n_nodes, rk, h, code, cnt) > 0;
 }
 
 // ======================================================================================
