@@ -439,6 +439,10 @@ __device__ __forceinline__ void leaf_aabb(const Node& nd, Node& box) {
     }
 }
 
+#ifndef CPT_UNIFIED_SLAB
+#define CPT_UNIFIED_SLAB 0   // ordered walk: leaf pretest and internal slab test as one test
+#endif
+
 #ifndef CPT_LEAF_PRETEST
 #define CPT_LEAF_PRETEST 2   // ordered walk: conservative slab test of a leaf's own box before
                              // its exact test (1 = cylinders, 2 = spheres and cylinders)
@@ -517,6 +521,26 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
         const Node pb = nodes(nb);
         if (STATS) cnt.nodes++;
         bool take_a = false;
+        if (CONS && CPT_UNIFIED_SLAB) {
+            // One conservative slab test for every lane: an internal node's box, or a leaf
+            // primitive's own box (the leaf pretest); only leaves that pass run their exact
+            // test.  The wave then runs the slab code once per iteration instead of once for
+            // the internal lanes and again for the leaf lanes.
+            Node box = nd;
+            if (leaf) leaf_aabb(nd, box);
+            const float tcmp = (leaf && nd.miss < best_rank) ? __int_as_float(__float_as_int(tmax) + 1) : tmax;
+            const bool pass = !slab_reject<FAST, true>(box, ray, tcmp);
+            if (leaf) {
+                if (STATS) cnt.prims++;
+                int k;
+                if (pass && ranked_leaf_test<FAST, false>(nd, ray, tmax, k, best_rank)) { best = ni; kind = k; }
+            } else {
+                take_a = pass;
+            }
+            ni = take_a ? na : nb;
+            nd = take_a ? pa : pb;
+            continue;
+        }
         if (leaf) {
             // IntersectionTest first (bvh.cu:175-180); the leaf's own box test is moot
             if (STATS) cnt.prims++;
@@ -622,34 +646,33 @@ __device__ __forceinline__ bool refract(v3 v, v3 n, float ni_over_nt, v3& refrac
 }
 
 // Material::EvalAttenuationAndCreateRay (material.cu:145-163) with the Metal/Mirror swap.
+// The four shaders share their expensive tail: every one draws x_1, x_2, builds a lobe
+// direction (pow + sincos in double) and rotates it onto an axis with to_world.  Only the
+// lobe exponent, the axis and the extra draws differ, so those are selected per lane first
+// and lobe()/to_world() run once for the whole wave instead of once per material type
+// present in it.  Per lane, the operations and the RNG draw order are exactly the shaders':
+//   Diffuse (material.cu:20-38):  x1 x2;      lobe(1/2) about N
+//   Metal -> MirrorHitShader (:40-64):  x1 x2;  lobe(1/alpha) about reflect(dir, N)
+//   Mirror -> MetalHitShader (:66-99):  x1 x2 u;  u < reflectivity ? lobe(1/alpha) about
+//                                       reflect(dir, N) : lobe(1/2) about N
+//   Glass (:101-143):  x1 x2; refract/schlick; u;  lobe(1/alpha) about reflect(in, N) or
+//                      the refracted direction
 __device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow& rng, Shade& out) {
     const v3 kd = mk(m.att_x, m.att_y, m.att_z);   // GetKd(0, 0)
     const v3 zero = mk(0.0f, 0.0f, 0.0f);
-    if (m.type == 1) {
-        // MaterialType::Metal -> MirrorHitShader (material.cu:40-64)
-        float x_1 = uniform(rng), x_2 = uniform(rng);
-        v3 local = lobe(x_1, x_2, m.inv_alpha);
-        v3 wo = to_world(local, reflect(in_dir, normal));
-        out.attenuation = dot(normal, wo) > 0.0f ? kd : zero;
-        out.bounce = wo;
-    } else if (m.type == 2) {
-        // MaterialType::Mirror -> MetalHitShader (material.cu:66-99)
-        float x_1 = uniform(rng), x_2 = uniform(rng);
-        if (uniform(rng) < m.reflectivity) {
-            v3 local = lobe(x_1, x_2, m.inv_alpha);
-            out.bounce = to_world(local, reflect(in_dir, normal));
-        } else {
-            v3 local = lobe(x_1, x_2, 1.0 / 2.0);
-            out.bounce = to_world(local, normal);
-        }
-        out.attenuation = dot(out.bounce, normal) < 0 ? zero : kd;
-    } else if (m.type == 3) {
-        // GlassHitShader (material.cu:101-143)
-        float x_1 = uniform(rng), x_2 = uniform(rng);
-        v3 local = lobe(x_1, x_2, m.inv_alpha);
+    const int type = (m.type >= 1 && m.type <= 3) ? m.type : 0;   // Test / unknown: Diffuse (:161)
+    const float x_1 = uniform(rng), x_2 = uniform(rng);
+    double ia = type == 0 ? 1.0 / 2 : m.inv_alpha;
+    v3 axis = normal;
+    if (type == 1) {
+        axis = reflect(in_dir, normal);
+    } else if (type == 2) {
+        if (uniform(rng) < m.reflectivity) axis = reflect(in_dir, normal);
+        else ia = 1.0 / 2.0;
+    } else if (type == 3) {
         v3 outward, refracted = mk1(0.0f);
         float ni_over_nt, reflect_prob, cosine;
-        v3 in = normalize(in_dir);
+        const v3 in = normalize(in_dir);
         if (dot(in, normal) > 0) {
             outward = -normal;
             ni_over_nt = m.ior;
@@ -662,16 +685,14 @@ __device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow&
         }
         if (refract(in, outward, ni_over_nt, refracted)) reflect_prob = schlick(cosine, m.ior);
         else reflect_prob = 1.0f;
-        if (uniform(rng) < reflect_prob) out.bounce = to_world(local, reflect(in, normal));
-        else out.bounce = to_world(local, refracted);
-        out.attenuation = kd;
-    } else {
-        // Diffuse (and Test / unknown: default branch) -> DiffuseHitShader (material.cu:20-38)
-        float x_1 = uniform(rng), x_2 = uniform(rng);
-        v3 local = lobe(x_1, x_2, 1.0 / 2);
-        out.bounce = to_world(local, normal);
-        out.attenuation = dot(normal, out.bounce) > 0.0f ? kd : zero;
+        axis = uniform(rng) < reflect_prob ? reflect(in, normal) : refracted;
     }
+    const v3 local = lobe(x_1, x_2, ia);
+    out.bounce = to_world(local, axis);
+    const float c = dot(normal, out.bounce);
+    if (type == 3) out.attenuation = kd;
+    else if (type == 2) out.attenuation = c < 0 ? zero : kd;
+    else out.attenuation = c > 0.0f ? kd : zero;
     out.radiance = mk(m.rad_x, m.rad_y, m.rad_z);   // emit_intensity_ * kd_
 }
 
