@@ -106,6 +106,8 @@ struct RayK {
     double yc;           // 1/(dx*dx + dz*dz)     (cylinder side roots, object.cu:69-79)
     float ix, iy, iz;    // f32 1/d per axis for the ordered walk's conservative slabs; 0 = the
                          // axis is skipped (|d| < 1e-30: no constraint, which only widens)
+    float bx, by, bz;    // 2e30 on a skipped axis, else 0: fma(b - o, i, -+bias) = -+2e30 there
+    float t3;            // conservative tmin limit: (tmin - 1e-4) * (1 + 2e-3)
 };
 
 __device__ __forceinline__ RayK make_rayk(const Ray& r) {
@@ -121,6 +123,10 @@ __device__ __forceinline__ RayK make_rayk(const Ray& r) {
     k.ix = __builtin_fabsf(r.d.x) >= 1e-30f ? 1.0f / r.d.x : 0.0f;
     k.iy = __builtin_fabsf(r.d.y) >= 1e-30f ? 1.0f / r.d.y : 0.0f;
     k.iz = __builtin_fabsf(r.d.z) >= 1e-30f ? 1.0f / r.d.z : 0.0f;
+    k.bx = k.ix != 0.0f ? 0.0f : DEFAULT_RAY_TMAX * 2;
+    k.by = k.iy != 0.0f ? 0.0f : DEFAULT_RAY_TMAX * 2;
+    k.bz = k.iz != 0.0f ? 0.0f : DEFAULT_RAY_TMAX * 2;
+    k.t3 = (r.tmin - 1e-4f) * (1.0f + 2e-3f);
     return k;
 }
 
@@ -300,27 +306,30 @@ struct Counters {
 // computed hit lies slightly outside its box by rounding is still tested (DESIGN.md
 // §Ordered walk).  The margin dwarfs the reciprocal's few-ulp error.
 constexpr float WALK_MARGIN_REL = 1e-3f, WALK_MARGIN_ABS = 1e-4f;
+// The conservative walk's tmax limit (slab_reject<*, true>'s `tmax` argument).
+__device__ __forceinline__ float walk_limit(float tmax) {
+    return (tmax + WALK_MARGIN_ABS) * (1.0f + 2.0f * WALK_MARGIN_REL);
+}
 
 template <bool FAST, bool CONS = false>
 __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, float tmax) {
     if (CONS) {
-        // (b - o) * (1/d): a few ulps from the exact quotient, far inside the margin; axes
-        // with ix == 0 impose nothing.  All operands finite (FAST rays only), no NaN.
-        const float BIG = DEFAULT_RAY_TMAX * 2;
-        const float t0x = (nd.a0 - ray.o.x) * ray.ix, t1x = (nd.b0 - ray.o.x) * ray.ix;
-        const float t0y = (nd.a1 - ray.o.y) * ray.iy, t1y = (nd.b1 - ray.o.y) * ray.iy;
-        const float t0z = (nd.a2 - ray.o.z) * ray.iz, t1z = (nd.b2 - ray.o.z) * ray.iz;
-        const float lx = ray.ix != 0.f ? __builtin_fminf(t0x, t1x) : -BIG;
-        const float hx = ray.ix != 0.f ? __builtin_fmaxf(t0x, t1x) : BIG;
-        const float ly = ray.iy != 0.f ? __builtin_fminf(t0y, t1y) : -BIG;
-        const float hy = ray.iy != 0.f ? __builtin_fmaxf(t0y, t1y) : BIG;
-        const float lz = ray.iz != 0.f ? __builtin_fminf(t0z, t1z) : -BIG;
-        const float hz = ray.iz != 0.f ? __builtin_fmaxf(t0z, t1z) : BIG;
-        float lo = __builtin_fmaxf(__builtin_fmaxf(lx, ly), lz);
-        float hi = __builtin_fminf(__builtin_fminf(hx, hy), hz);
-        lo = lo - (WALK_MARGIN_REL * __builtin_fabsf(lo) + WALK_MARGIN_ABS);
-        hi = hi + (WALK_MARGIN_REL * __builtin_fabsf(hi) + WALK_MARGIN_ABS);
-        return lo > hi || lo > tmax || hi < ray.tmin;
+        // (b - o) * (1/d): a few ulps from the exact quotient, far inside the margin.  Skipped
+        // axes (i == 0) get -+2e30 through the fma's addend: no constraint.  `tmax` is the
+        // widened limit walk_limit(tmax).  Reject iff
+        //   lo - m(lo) > hi + m(hi),  i.e. lo - hi > 1e-3 (|lo| + |hi|) + 2e-4  (box missed),
+        //   lo > walk_limit(tmax)                                           (box beyond tmax),
+        //   hi < ray.t3                                                      (box behind tmin),
+        // each implied by the exact test's rejection with a margin to spare.
+        const float t0x = __builtin_fmaf(nd.a0 - ray.o.x, ray.ix, -ray.bx), t1x = __builtin_fmaf(nd.b0 - ray.o.x, ray.ix, ray.bx);
+        const float t0y = __builtin_fmaf(nd.a1 - ray.o.y, ray.iy, -ray.by), t1y = __builtin_fmaf(nd.b1 - ray.o.y, ray.iy, ray.by);
+        const float t0z = __builtin_fmaf(nd.a2 - ray.o.z, ray.iz, -ray.bz), t1z = __builtin_fmaf(nd.b2 - ray.o.z, ray.iz, ray.bz);
+        const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
+                                         __builtin_fminf(t0z, t1z));
+        const float hi = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
+                                         __builtin_fmaxf(t0z, t1z));
+        const float m2 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo) + __builtin_fabsf(hi), 2.0f * WALK_MARGIN_ABS);
+        return lo - hi > m2 || lo > tmax || hi < ray.t3;
     }
     float t0x = qdiv_raw(nd.a0 - ray.o.x, ray.yx), t1x = qdiv_raw(nd.b0 - ray.o.x, ray.yx);
     float t0y = qdiv_raw(nd.a1 - ray.o.y, ray.yy), t1y = qdiv_raw(nd.b1 - ray.o.y, ray.yy);
@@ -456,7 +465,7 @@ __device__ __forceinline__ bool ranked_leaf_test(const Node& nd, const RayK& ray
         if (type == 2 || (CPT_LEAF_PRETEST == 2 && type == 0)) {
             Node box;
             leaf_aabb(nd, box);
-            if (slab_reject<FAST, true>(box, ray, tm)) return false;
+            if (slab_reject<FAST, true>(box, ray, walk_limit(tm))) return false;
         }
     }
     if (!leaf_test(nd, ray, tm, kind)) return false;
@@ -503,7 +512,7 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
             const Node pa = nodes(na < last ? na : last);
             const Node pb = nodes(nb < last ? nb : last);
             if (STATS) cnt.nodes++;
-            const bool take_a = !slab_reject<FAST, CONS>(nd, ray, tmax);
+            const bool take_a = !slab_reject<FAST, CONS>(nd, ray, CONS ? walk_limit(tmax) : tmax);
             ni = take_a ? na : nb;
             nd = take_a ? pa : pb;
         }
@@ -529,7 +538,7 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
             Node box = nd;
             if (leaf) leaf_aabb(nd, box);
             const float tcmp = (leaf && nd.miss < best_rank) ? __int_as_float(__float_as_int(tmax) + 1) : tmax;
-            const bool pass = !slab_reject<FAST, true>(box, ray, tcmp);
+            const bool pass = !slab_reject<FAST, true>(box, ray, walk_limit(tcmp));
             if (leaf) {
                 if (STATS) cnt.prims++;
                 int k;
@@ -550,7 +559,7 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
 #if CPT_STAMPS == 2
         const unsigned long long t1 = stamp();
 #endif
-        if (!leaf) take_a = !slab_reject<FAST, CONS>(nd, ray, tmax);
+        if (!leaf) take_a = !slab_reject<FAST, CONS>(nd, ray, CONS ? walk_limit(tmax) : tmax);
 #if CPT_STAMPS == 2
         const unsigned long long t2 = stamp();
         cnt.st_leaf += t1 - t0;

@@ -905,7 +905,8 @@ bool slab_pass(const Node& n, const Ray& ray) {                 // bvh.cu:181-20
 }
 
 // The product's conservative slab (cpt_path.hpp slab_reject<FAST, true>): f32 reciprocals,
-// skipped axes for |d| < 1e-30, interval widened by 1e-3*|t| + 1e-4.
+// skipped axes for |d| < 1e-30 (a -+2e30 fma addend), reject iff lo - hi > 1e-3 (|lo| + |hi|)
+// + 2e-4, lo > (tmax + 1e-4) * 1.002, or hi < (tmin - 1e-4) * 1.002.
 bool slab_pass_conservative(const Bvh::WNode& n, const Ray& ray) {
     const float BIG = DEFAULT_RAY_TMAX * 2;
     const float o[3] = {ray.origin.x, ray.origin.y, ray.origin.z}, d[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
@@ -913,15 +914,17 @@ bool slab_pass_conservative(const Bvh::WNode& n, const Ray& ray) {
     float l[3], h[3];
     for (int k = 0; k < 3; ++k) {
         const float inv = fabsf(d[k]) >= 1e-30f ? 1.0f / d[k] : 0.0f;
-        const float t0 = (a[k] - o[k]) * inv, t1 = (b[k] - o[k]) * inv;
-        l[k] = inv != 0.f ? fminf(t0, t1) : -BIG;
-        h[k] = inv != 0.f ? fmaxf(t0, t1) : BIG;
+        const float bias = inv != 0.0f ? 0.0f : BIG;
+        const float t0 = fmaf(a[k] - o[k], inv, -bias), t1 = fmaf(b[k] - o[k], inv, bias);
+        l[k] = fminf(t0, t1);
+        h[k] = fmaxf(t0, t1);
     }
-    float lo = fmaxf(fmaxf(l[0], l[1]), l[2]);
-    float hi = fminf(fminf(h[0], h[1]), h[2]);
-    lo = lo - (1e-3f * fabsf(lo) + 1e-4f);
-    hi = hi + (1e-3f * fabsf(hi) + 1e-4f);
-    return !(lo > hi || lo > ray.tmax || hi < ray.tmin);
+    const float lo = fmaxf(fmaxf(l[0], l[1]), l[2]);
+    const float hi = fminf(fminf(h[0], h[1]), h[2]);
+    const float m2 = fmaf(1e-3f, fabsf(lo) + fabsf(hi), 2.0f * 1e-4f);
+    const float tlim = (ray.tmax + 1e-4f) * (1.0f + 2.0f * 1e-3f);
+    const float t3 = (ray.tmin - 1e-4f) * (1.0f + 2e-3f);
+    return !(lo - hi > m2 || lo > tlim || hi < t3);
 }
 
 bool trace_ray_ordered(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st) {
