@@ -699,9 +699,9 @@ __device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow&
     const v3 local = lobe(x_1, x_2, ia);
     out.bounce = to_world(local, axis);
     const float c = dot(normal, out.bounce);
-    if (type == 3) out.attenuation = kd;
-    else if (type == 2) out.attenuation = c < 0 ? zero : kd;
-    else out.attenuation = c > 0.0f ? kd : zero;
+    // per component: a struct-valued select here became an indexed scratch load
+    const bool keep = type == 3 || (type == 2 ? !(c < 0) : c > 0.0f);
+    out.attenuation = mk(keep ? kd.x : zero.x, keep ? kd.y : zero.y, keep ? kd.z : zero.z);
     out.radiance = mk(m.rad_x, m.rad_y, m.rad_z);   // emit_intensity_ * kd_
 }
 
