@@ -448,6 +448,10 @@ __device__ __forceinline__ void leaf_aabb(const Node& nd, Node& box) {
     }
 }
 
+#ifndef CPT_PREFETCH
+#define CPT_PREFETCH 0   // load both successors before the node's test (else the chosen one after)
+#endif
+
 #ifndef CPT_UNIFIED_SLAB
 #define CPT_UNIFIED_SLAB 0   // ordered walk: leaf pretest and internal slab test as one test
 #endif
@@ -526,8 +530,10 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
 #endif
         const bool leaf = nd.code >= 0;
         const int na = ni + 1, nb = leaf ? na : nd.miss;
+#if CPT_PREFETCH
         const Node pa = nodes(na);   // past the order's end: never used (the loop ends)
         const Node pb = nodes(nb);
+#endif
         if (STATS) cnt.nodes++;
         bool take_a = false;
         if (CONS && CPT_UNIFIED_SLAB) {
@@ -547,7 +553,11 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
                 take_a = pass;
             }
             ni = take_a ? na : nb;
+#if CPT_PREFETCH
             nd = take_a ? pa : pb;
+#else
+            nd = nodes(ni);
+#endif
             continue;
         }
         if (leaf) {
@@ -566,7 +576,11 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
         cnt.st_slab += t2 - t1;
 #endif
         ni = take_a ? na : nb;
+#if CPT_PREFETCH
         nd = take_a ? pa : pb;
+#else
+        nd = nodes(ni);
+#endif
 #if CPT_STAMPS == 2
         cnt.st_iter += stamp() - t0;
 #endif
