@@ -379,9 +379,6 @@ __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, flo
     return lo > hi || lo > tmax || hi < ray.tmin;
 }
 
-#ifndef CPT_LEAF_BATCH
-#define CPT_LEAF_BATCH 0   // K > 0: leaf tests run in wave-uniform leaf phases (see trace)
-#endif
 
 // Node fetch.  BufSrc reads through a buffer descriptor over the whole node array (built from
 // kernel arguments, so it is wave-uniform and lives in SGPRs): a 32-bit per-lane byte offset
@@ -452,9 +449,6 @@ __device__ __forceinline__ void leaf_aabb(const Node& nd, Node& box) {
 #define CPT_PREFETCH 0   // load both successors before the node's test (else the chosen one after)
 #endif
 
-#ifndef CPT_UNIFIED_SLAB
-#define CPT_UNIFIED_SLAB 0   // ordered walk: leaf pretest and internal slab test as one test
-#endif
 
 #ifndef CPT_LEAF_PRETEST
 #define CPT_LEAF_PRETEST 2   // ordered walk: conservative slab test of a leaf's own box before
@@ -489,41 +483,9 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
     int ni = 0;
     Node nd{};
     if (n_nodes > 0) nd = nodes(0);
-    [[maybe_unused]] const int last = n_nodes - 1;
-#if CPT_LEAF_BATCH > 0
-    // Leaf batching: a lane that reaches a leaf parks there; leaf tests run in a wave-uniform
-    // leaf phase once >= 1/K of the walking lanes are parked (or nobody can slab-test).  A
-    // lane's own visit sequence — and so its tmax history, pruning and first-found tie rule —
-    // is unchanged; only the interleaving of lanes changes.
-    for (;;) {
-        const bool walking = ni < n_nodes;
-        const bool at_leaf = walking && nd.code >= 0;
-        const uint64_t lm = __ballot(at_leaf), wm = __ballot(walking);
-        if (wm == 0) break;
-        const int leaf_phase = __builtin_amdgcn_readfirstlane(
-            (lm == wm || __popcll(lm) * CPT_LEAF_BATCH >= __popcll(wm)) ? 1 : 0);
-        if (leaf_phase) {
-            if (at_leaf) {
-                const Node nx = nodes(ni + 1 < last ? ni + 1 : last);
-                if (STATS) { cnt.nodes++; cnt.prims++; }
-                int k;
-                if (ranked_leaf_test<FAST, CONS>(nd, ray, tmax, k, best_rank)) { best = ni; kind = k; }
-                ni = ni + 1;
-                nd = nx;
-            }
-        } else if (walking && !at_leaf) {
-            const int na = ni + 1, nb = nd.miss;
-            const Node pa = nodes(na < last ? na : last);
-            const Node pb = nodes(nb < last ? nb : last);
-            if (STATS) cnt.nodes++;
-            const bool take_a = !slab_reject<FAST, CONS>(nd, ray, CONS ? walk_limit(tmax) : tmax);
-            ni = take_a ? na : nb;
-            nd = take_a ? pa : pb;
-        }
-    }
-#else
     // The successor of node ni is ni + 1 (box hit: its first child; after a leaf) or nd.miss
-    // (box miss); both loads are issued before the node's test so their latency hides under it.
+    // (box miss).  With CPT_PREFETCH both are loaded before the node's test; by default the
+    // chosen one is loaded after it (the other waves of the SIMD hide the latency).
     while (ni < n_nodes) {
 #if CPT_STAMPS == 2
         const unsigned long long t0 = stamp();
@@ -536,30 +498,6 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
 #endif
         if (STATS) cnt.nodes++;
         bool take_a = false;
-        if (CONS && CPT_UNIFIED_SLAB) {
-            // One conservative slab test for every lane: an internal node's box, or a leaf
-            // primitive's own box (the leaf pretest); only leaves that pass run their exact
-            // test.  The wave then runs the slab code once per iteration instead of once for
-            // the internal lanes and again for the leaf lanes.
-            Node box = nd;
-            if (leaf) leaf_aabb(nd, box);
-            const float tcmp = (leaf && nd.miss < best_rank) ? __int_as_float(__float_as_int(tmax) + 1) : tmax;
-            const bool pass = !slab_reject<FAST, true>(box, ray, walk_limit(tcmp));
-            if (leaf) {
-                if (STATS) cnt.prims++;
-                int k;
-                if (pass && ranked_leaf_test<FAST, false>(nd, ray, tmax, k, best_rank)) { best = ni; kind = k; }
-            } else {
-                take_a = pass;
-            }
-            ni = take_a ? na : nb;
-#if CPT_PREFETCH
-            nd = take_a ? pa : pb;
-#else
-            nd = nodes(ni);
-#endif
-            continue;
-        }
         if (leaf) {
             // IntersectionTest first (bvh.cu:175-180); the leaf's own box test is moot
             if (STATS) cnt.prims++;
@@ -585,7 +523,6 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
         cnt.st_iter += stamp() - t0;
 #endif
     }
-#endif
     if (best < 0) return 0;
     const Node w = nodes(best);
     if (CONS) {
