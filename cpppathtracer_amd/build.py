@@ -65,7 +65,10 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, out: str = None, defines=()) -> str:
-    """Build libcpt.so; `out`/`defines` produce A/B variants (e.g. defines=["CPT_LDS=0"])."""
+    """Build libcpt.so; `out`/`defines` produce A/B variants: defines is a list of "NAME=VALUE"
+    strings or a {NAME: VALUE} dict."""
+    if isinstance(defines, dict):
+        defines = [f"{k}={v}" for k, v in defines.items()]
     target = out or LIB_PATH
     if not force and out is None and not defines and not needs_build():
         return LIB_PATH

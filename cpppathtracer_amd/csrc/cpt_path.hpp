@@ -451,7 +451,7 @@ __device__ __forceinline__ void leaf_aabb(const Node& nd, Node& box) {
 
 
 #ifndef CPT_LEAF_PRETEST
-#define CPT_LEAF_PRETEST 2   // ordered walk: conservative slab test of a leaf's own box before
+#define CPT_LEAF_PRETEST 1   // ordered walk: conservative slab test of a leaf's own box before
                              // its exact test (1 = cylinders, 2 = spheres and cylinders)
 #endif
 
