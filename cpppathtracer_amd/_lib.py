@@ -59,6 +59,7 @@ CPT_RENDER_SYNC = 0x8
 CPT_PATH_MEGAKERNEL = 0x000
 CPT_PATH_WAVEFRONT = 0x100
 CPT_TRAVERSAL_ORDERED = 0x200
+CPT_TRAVERSAL_PLAIN_LEAVES = 0x400
 
 
 class CptError(RuntimeError):

@@ -945,7 +945,7 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     p.mats = c->d_mats;
     p.n_nodes = c->n_bvh;
     p.n_walk = c->n_walk;
-    p.ordered = (flags & CPT_TRAVERSAL_ORDERED) ? 1 : 0;
+    p.ordered = (flags & CPT_TRAVERSAL_ORDERED) ? ((flags & CPT_TRAVERSAL_PLAIN_LEAVES) ? 2 : 1) : 0;
     p.env = c->d_env;
     p.env_w = c->env_w;
     p.env_h = c->env_h;

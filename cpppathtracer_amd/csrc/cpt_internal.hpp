@@ -25,7 +25,7 @@ struct KParams {
                             // the walk tree's eight octant orders (n_walk each)
     const Mat* mats;        // deduplicated materials, indexed by Node::code >> 2
     int n_nodes, n_walk;
-    int ordered;            // CPT_TRAVERSAL_ORDERED: walk the ray's octant order
+    int ordered;            // CPT_TRAVERSAL_ORDERED: walk the ray's octant order (2: plain leaves)
     const uint32_t* env;    // packed RGBA8, env_cols x env_h
     int env_w, env_h, env_cols;
     CamK cam;

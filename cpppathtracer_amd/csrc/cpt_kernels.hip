@@ -138,6 +138,9 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             Hit h;
             int code = -1;
             if (STATS) cnt.segments++;
+#if CPT_STAMPS == 3
+            if (lowest_active_lane()) cnt.st_seg++;
+#endif
             const RayK rk = make_rayk(ray);
             const bool finite_ray = !(ray.o.x != ray.o.x || ray.o.y != ray.o.y || ray.o.z != ray.o.z ||
                                       ray.d.x != ray.d.x || ray.d.y != ray.d.y || ray.d.z != ray.d.z);
@@ -216,6 +219,16 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
     st_refill = cnt.st_leaf;
     st_trace = cnt.st_slab;
     st_shade = cnt.st_iter;
+#elif CPT_STAMPS == 3
+    // wave-level counts: iterations with any lane at a leaf / at an inner node, all walk
+    // iterations, and segment rounds (stats[4] is replaced by the last, misses are not needed)
+    st_refill = wave_sum((uint32_t)cnt.st_leaf);
+    st_trace = wave_sum((uint32_t)cnt.st_slab);
+    st_shade = wave_sum((uint32_t)cnt.st_iter);
+    {
+        const uint64_t ws = wave_sum((uint32_t)cnt.st_seg);
+        if (lane == 0) atomicAdd(&p.stats[4], (unsigned long long)ws);
+    }
 #endif
     if (CPT_STAMPS && lane == 0) {
         atomicAdd(&p.stats[5], st_refill);

@@ -290,10 +290,17 @@ __device__ __forceinline__ unsigned long long stamp() {
 
 struct Counters {
     uint32_t segments, nodes, prims, hits, misses, fallbacks;
-#if CPT_STAMPS == 2
-    unsigned long long st_leaf, st_slab, st_iter;
+#if CPT_STAMPS >= 2
+    unsigned long long st_leaf, st_slab, st_iter, st_seg;
 #endif
 };
+
+// CPT_STAMPS == 3 (diagnostic): count wave-level events in the lowest active lane, so that a
+// wave_sum over the lanes gives the wave's count.
+__device__ __forceinline__ bool lowest_active_lane() {
+    const uint64_t m = __ballot(1);
+    return (int)(__lane_id()) == __ffsll((unsigned long long)m) - 1;
+}
 
 // Slab test of one internal node (bvh.cu:181-200).  The six plane distances use the exact
 // quotient; if any of them is zero/subnormal the node is redone with the IEEE divide.
@@ -497,6 +504,12 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
         const Node pb = nodes(nb);
 #endif
         if (STATS) cnt.nodes++;
+#if CPT_STAMPS == 3
+        {
+            const bool any_leaf = __ballot(leaf) != 0, any_inner = __ballot(!leaf) != 0;
+            if (lowest_active_lane()) { cnt.st_iter++; cnt.st_leaf += any_leaf; cnt.st_slab += any_inner; }
+        }
+#endif
         bool take_a = false;
         if (leaf) {
             // IntersectionTest first (bvh.cu:175-180); the leaf's own box test is moot
@@ -539,6 +552,68 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
     return 1;
 }
 
+#ifndef CPT_SPEC_LEAF
+#define CPT_SPEC_LEAF 32  // ordered walk: postpone leaf tests and run them wave-wide (0 = off;
+                          // else the share of working lanes, in 64ths, that must be waiting
+                          // on a leaf before the wave runs its leaf round)
+#endif
+
+#ifndef CPT_SPEC_ONLY_STOPPED
+#define CPT_SPEC_ONLY_STOPPED 0
+#endif
+
+// The ordered walk with postponed leaves (Aila & Laine's speculative traversal, on the skip
+// links).  A lane that meets a leaf parks its index and walks on through inner nodes; it
+// stops when it meets a second leaf or the order's end.  Leaf tests then run for every parked
+// lane at once when enough working lanes are stopped, instead of in every iteration where
+// one lane is at a leaf.  Inner nodes are culled with the tmax of the leaves tested so far,
+// which is never below the final one: a superset of the plain walk's tests, so the same
+// closest hit under the rank rule, and the same certificate.
+template <bool STATS, bool FAST, typename SRC>
+__device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const RayK& ray, Hit& h, int& code_out,
+                                          Counters& cnt) {
+    float tmax = DEFAULT_RAY_TMAX;
+    int best = -1, kind = 0;
+    int best_rank = 0x7fffffff;
+    int ni = 0, parked = -1;
+    Node nd{};
+    if (n_nodes > 0) nd = nodes(0);
+    for (;;) {
+        const bool leaf = nd.code >= 0;
+        if (ni < n_nodes && !(leaf && parked >= 0)) {
+            if (STATS) cnt.nodes++;
+            if (leaf) {
+                parked = ni;
+                ni = ni + 1;
+            } else {
+                ni = slab_reject<FAST, true>(nd, ray, walk_limit(tmax)) ? nd.miss : ni + 1;
+            }
+            nd = nodes(ni);
+        }
+        const bool working = parked >= 0 || ni < n_nodes;
+        const bool stopped = parked >= 0 && (ni >= n_nodes || nd.code >= 0);
+        const uint64_t w = __ballot(working);
+        if (!w) break;
+        if (__popcll(__ballot(stopped)) * 64 >= CPT_SPEC_LEAF * __popcll(w)) {
+            if (CPT_SPEC_ONLY_STOPPED ? stopped : parked >= 0) {
+                if (STATS) cnt.prims++;
+                const Node lf = nodes(parked);
+                int k;
+                if (ranked_leaf_test<FAST, true>(lf, ray, tmax, k, best_rank)) { best = parked; kind = k; }
+                parked = -1;
+            }
+        }
+    }
+    if (best < 0) return 0;
+    const Node w = nodes(best);
+    Node box;
+    leaf_aabb(w, box);
+    if (slab_reject<FAST>(box, ray, tmax)) return -1;
+    h = hit_attributes(w, ray, tmax, kind);
+    code_out = w.code;
+    return 1;
+}
+
 // TraceRay for one segment: the reference order, or the ordered walk with its certificate
 // and the reference-order fallback (CPT_TRAVERSAL_ORDERED).
 template <bool STATS>
@@ -548,7 +623,8 @@ __device__ __forceinline__ bool trace_segment(const KParams& p, const RayK& rk, 
     if (p.ordered && __builtin_expect(finite, 1)) {
         int n;
         const BufSrc order{rsrc, walk_order(p, rk.d, n) * (uint32_t)sizeof(Node)};
-        const int r = trace<STATS, true, true>(order, n, rk, h, code, cnt);
+        const int r = CPT_SPEC_LEAF && p.ordered == 1 ? trace_spec<STATS, true>(order, n, rk, h, code, cnt)
+                                                      : trace<STATS, true, true>(order, n, rk, h, code, cnt);
         if (__builtin_expect(r >= 0, 1)) return r > 0;
         if (STATS) cnt.fallbacks++;
     }

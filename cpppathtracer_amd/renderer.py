@@ -9,7 +9,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import (CPT_PATH_WAVEFRONT, CPT_TRAVERSAL_ORDERED, CPT_RENDER_ACCUMULATE, CPT_RENDER_AUX, CPT_RENDER_STATS, CPT_RENDER_SYNC,
+from ._lib import (CPT_PATH_WAVEFRONT, CPT_TRAVERSAL_ORDERED, CPT_TRAVERSAL_PLAIN_LEAVES, CPT_RENDER_ACCUMULATE, CPT_RENDER_AUX, CPT_RENDER_STATS, CPT_RENDER_SYNC,
                    CptError, check)
 
 PATHS = ("megakernel", "wavefront")
@@ -123,12 +123,15 @@ class Renderer:
         """path: "megakernel" (per-lane regeneration, state in VGPRs) or "wavefront" (SoA state in
         HBM, extend/shade kernels with ballot compaction).  Both give identical results.
         ordered: near-first BVH walk per direction octant (CPT_TRAVERSAL_ORDERED); same closest
-        hits as the reference order up to box/primitive rounding (DESIGN.md §Ordered walk)."""
+        hits as the reference order up to box/primitive rounding (DESIGN.md §Ordered walk).
+        ordered="plain": the same walk testing each leaf where it meets it (per-ray node/prim
+        counts, CPT_TRAVERSAL_PLAIN_LEAVES) instead of parking leaves for wave-wide rounds."""
         if path not in PATHS:
             raise ValueError(f"path must be one of {PATHS}")
         c = np.ascontiguousarray(np.array(cam, dtype=CAMERA_DTYPE))
         f = flags | (CPT_PATH_WAVEFRONT if path == "wavefront" else 0)
         f |= CPT_TRAVERSAL_ORDERED if ordered else 0
+        f |= CPT_TRAVERSAL_PLAIN_LEAVES if ordered == "plain" else 0
         f |= CPT_RENDER_ACCUMULATE if accumulate else 0
         f |= CPT_RENDER_AUX if aux else 0
         f |= CPT_RENDER_STATS if stats else 0

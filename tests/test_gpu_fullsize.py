@@ -31,6 +31,9 @@ def test_fullsize_walks_agree_and_rows_match_oracle(gpu, oracle_mod, sky, W, H):
     ord_acc, ord_rng = _render(gpu, cam, 1, 16, ordered=True)
     np.testing.assert_array_equal(ord_acc.view(np.uint32), ref_acc.view(np.uint32))
     np.testing.assert_array_equal(ord_rng, ref_rng)
+    gpu.init_rng(1234)
+    plain_acc, _ = _render(gpu, cam, 1, 16, ordered="plain")
+    np.testing.assert_array_equal(plain_acc.view(np.uint32), ref_acc.view(np.uint32))
     rows = np.linspace(0, H - 1, 6).astype(np.int32)
     rng = oracle_mod.init_rng(1234, W, rows, threads=16)
     o_acc, _, _, _ = oracle_mod.render(objs, cam, sky, rows, 1, 16, rng, threads=16)

@@ -112,7 +112,7 @@ def _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, rows=None, seed=1234
 
 def _kw(path):
     base, _, mode = path.partition(":")
-    return dict(path=base, ordered=(mode == "ordered"))
+    return dict(path=base, ordered={"": False, "ordered": True, "plain": "plain"}[mode])
 
 
 CASES = [
@@ -126,17 +126,27 @@ CASES = [
 
 
 # "<path>:ordered" = the near-first octant walk (CPT_TRAVERSAL_ORDERED): same closest hits,
-# so the same images, RNG end states and segment/hit/miss counts; its node/prim counts are its
-# own and equal the oracle's diagnostic restatement of the ordered walk (oracle.set_walk),
-# including the number of segments whose winner certificate failed (reference-walk fallback).
-PATHS = ["megakernel", "wavefront", "megakernel:ordered", "wavefront:ordered"]
+# so the same images, RNG end states and segment/hit/miss counts.  "<path>:plain" tests each
+# leaf where the walk meets it (CPT_TRAVERSAL_PLAIN_LEAVES): its node/prim counts equal the
+# oracle's diagnostic restatement of the ordered walk (oracle.set_walk), including the number
+# of segments whose winner certificate failed (reference-walk fallback).  The default
+# ordered walk parks leaves for wave-wide rounds: counts at least the plain walk's.
+PATHS = ["megakernel", "wavefront", "megakernel:ordered", "wavefront:ordered", "megakernel:plain",
+         "wavefront:plain"]
 
 
 def _check_stats(gs, os_, path):
-    if path.endswith(":ordered"):
+    if path.endswith(":plain"):
         for k in ("segments", "hits", "misses"):
             assert gs[k] == os_[k], k
         assert gs == os_["walk"]
+    elif path.endswith(":ordered"):
+        # postponed leaves: the same closest hits (so segments/hits/misses and the winner
+        # certificates match); each ray walks a superset of the plain walk's nodes and leaves
+        for k in ("segments", "hits", "misses"):
+            assert gs[k] == os_[k], k
+        assert gs["fallbacks"] == os_["walk"]["fallbacks"]
+        assert gs["nodes"] >= os_["walk"]["nodes"] and gs["prims"] >= os_["walk"]["prims"]
     else:
         assert gs == os_
 
@@ -217,7 +227,7 @@ def test_empty_scene_and_no_env(gpu, oracle_mod, sky, path):
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
 
 
-@pytest.mark.parametrize("path", ["megakernel", "megakernel:ordered"])
+@pytest.mark.parametrize("path", ["megakernel", "megakernel:ordered", "megakernel:plain"])
 def test_single_object_and_cylinders(gpu, oracle_mod, sky, path):
     objs = scenes.scene_s1000(n=3)
     for sl in (slice(0, 1), slice(1, 2), slice(0, 4)):
@@ -264,7 +274,7 @@ def test_invalid_arguments(gpu):
         gpu.set_frame(16, 16, [16])
 
 
-@pytest.mark.parametrize("path", ["megakernel", "wavefront", "megakernel:ordered"])
+@pytest.mark.parametrize("path", ["megakernel", "wavefront", "megakernel:ordered", "megakernel:plain"])
 def test_update_object_refit(gpu, oracle_mod, sky, path):
     """SceneBVH::UpdateObject (bvh.cu:122-157): the leaf takes the new object, its ancestors'
     boxes are refit and the topology is kept.  Moves a sphere far out (boxes grow), shrinks a
@@ -315,7 +325,7 @@ def test_update_object_refit(gpu, oracle_mod, sky, path):
     _check_stats(gs, os_, path)
 
 
-@pytest.mark.parametrize("path", ["megakernel:ordered", "wavefront:ordered"])
+@pytest.mark.parametrize("path", ["megakernel:ordered", "wavefront:ordered", "megakernel:plain"])
 def test_ordered_walk_platform_only_and_multiple_platforms(gpu, oracle_mod, sky, path):
     """Walk-tree edge cases: a scene that is only a platform (no tree left after splicing),
     and several platforms (floor, a ceiling plane, a duplicate floor) mixed with primitives."""
