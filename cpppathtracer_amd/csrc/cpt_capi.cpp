@@ -194,6 +194,15 @@ void linearise(const HostBvh& b, const std::vector<cpt_object>& objs, const std:
                 st.pop_back();
                 continue;
             }
+            if (octant >= 0) {
+                // octant form (cpt_path.hpp slab_reject_octant): a = the planes a ray of this
+                // octant enters through, b = the ones it leaves through (bmax first on an
+                // axis the ray runs down)
+                Node& q = out.back();
+                if (octant & 1) std::swap(q.a0, q.b0);
+                if (octant & 2) std::swap(q.a1, q.b1);
+                if (octant & 4) std::swap(q.a2, q.b2);
+            }
             f.stage = 1;
             // the reference pops the right child first; a ray moving +axis meets the left
             // (lower-centroid) child first

@@ -386,6 +386,27 @@ __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, flo
     return lo > hi || lo > tmax || hi < ray.tmin;
 }
 
+// slab_reject<FAST, true> on a walk-tree inner node stored in octant form (cpt_capi.cpp
+// linearise): a.xyz are the planes a ray of the node's octant enters through, b.xyz the ones
+// it leaves through.  For an axis with i != 0 the sign of i is the octant's, so the entry
+// plane's distance is the min of the pair and the exit plane's the max (the subtraction, the
+// product and the fma are monotone); a skipped axis gives -2e30 / +2e30 in that order.  So
+// lo and hi are bit for bit those of the min/max form and the decision is the same.  x and y
+// go through packed f32 ops (v_pk_add/v_pk_fma_f32: two lanes of IEEE f32 per instruction).
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ bool slab_reject_octant(const Node& nd, const RayK& ray, float limit) {
+    const f2v oxy = {ray.o.x, ray.o.y}, ixy = {ray.ix, ray.iy}, bxy = {ray.bx, ray.by};
+    const f2v nxy = {nd.a0, nd.a1}, fxy = {nd.b0, nd.b1};
+    const f2v tn = __builtin_elementwise_fma(nxy - oxy, ixy, -bxy);
+    const f2v tf = __builtin_elementwise_fma(fxy - oxy, ixy, bxy);
+    const float tnz = __builtin_fmaf(nd.a2 - ray.o.z, ray.iz, -ray.bz);
+    const float tfz = __builtin_fmaf(nd.b2 - ray.o.z, ray.iz, ray.bz);
+    const float lo = __builtin_fmaxf(__builtin_fmaxf(tn.x, tn.y), tnz);
+    const float hi = __builtin_fminf(__builtin_fminf(tf.x, tf.y), tfz);
+    const float m2 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo) + __builtin_fabsf(hi), 2.0f * WALK_MARGIN_ABS);
+    return lo - hi > m2 || lo > limit || hi < ray.t3;
+}
 
 // Node fetch.  BufSrc reads through a buffer descriptor over the whole node array (built from
 // kernel arguments, so it is wave-uniform and lives in SGPRs): a 32-bit per-lane byte offset
@@ -520,7 +541,7 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
 #if CPT_STAMPS == 2
         const unsigned long long t1 = stamp();
 #endif
-        if (!leaf) take_a = !slab_reject<FAST, CONS>(nd, ray, CONS ? walk_limit(tmax) : tmax);
+        if (!leaf) take_a = CONS ? !slab_reject_octant(nd, ray, walk_limit(tmax)) : !slab_reject<FAST>(nd, ray, tmax);
 #if CPT_STAMPS == 2
         const unsigned long long t2 = stamp();
         cnt.st_leaf += t1 - t0;
@@ -576,6 +597,7 @@ __device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const R
     int best = -1, kind = 0;
     int best_rank = 0x7fffffff;
     int ni = 0, parked = -1;
+    float limit = walk_limit(tmax);   // changes only in leaf rounds
     Node nd{};
     if (n_nodes > 0) nd = nodes(0);
     for (;;) {
@@ -586,7 +608,7 @@ __device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const R
                 parked = ni;
                 ni = ni + 1;
             } else {
-                ni = slab_reject<FAST, true>(nd, ray, walk_limit(tmax)) ? nd.miss : ni + 1;
+                ni = slab_reject_octant(nd, ray, limit) ? nd.miss : ni + 1;
             }
             nd = nodes(ni);
         }
@@ -599,7 +621,11 @@ __device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const R
                 if (STATS) cnt.prims++;
                 const Node lf = nodes(parked);
                 int k;
-                if (ranked_leaf_test<FAST, true>(lf, ray, tmax, k, best_rank)) { best = parked; kind = k; }
+                if (ranked_leaf_test<FAST, true>(lf, ray, tmax, k, best_rank)) {
+                    best = parked;
+                    kind = k;
+                    limit = walk_limit(tmax);
+                }
                 parked = -1;
             }
         }
