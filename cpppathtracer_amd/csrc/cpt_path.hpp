@@ -483,6 +483,55 @@ __device__ __forceinline__ void leaf_aabb(const Node& nd, Node& box) {
                              // its exact test (1 = cylinders, 2 = spheres and cylinders)
 #endif
 
+#ifndef CPT_UNIFIED_LEAF
+#define CPT_UNIFIED_LEAF 1   // ordered walk's leaf rounds: spheres and cylinder sides share one
+                             // quadratic (a wave with both kinds runs the root code once)
+#endif
+
+// Sphere (object.cu:10-35) and cylinder (object.cu:50-112) in one code path for a wave that
+// holds both.  Each lane computes exactly its own type's expressions in the reference's
+// operation order: dot(A_C, d) = (x + y) + z for a sphere, cx*dx + cz*dz for a cylinder side
+// (the y term is selected in or out, never multiplied by 0), likewise for a and c; the root
+// quotients use that type's own reciprocal (ya or yc).  The cylinder's caps run first (only on
+// cylinder lanes), then the shared roots with the cylinder's y-range check.
+__device__ __forceinline__ bool sphere_cyl_test(const Node& nd, const RayK& ray, float& tmax, int& kind) {
+    const bool sph = (nd.code & 3) == 0;
+    const float r = nd.b0;
+    bool ret = false;
+    float lower = 0.f, upper = 0.f;
+    if (!sph) {
+        upper = nd.a1 + nd.b2 / 2;
+        if (cap_test(nd.a0, nd.a2, r, ray, tmax, kind, upper)) ret = true;
+        lower = nd.a1 - nd.b2 / 2;
+        if (cap_test(nd.a0, nd.a2, r, ray, tmax, kind, lower)) ret = true;
+    }
+    const float cx = ray.o.x - nd.a0, cy = ray.o.y - nd.a1, cz = ray.o.z - nd.a2;
+    const float dx = ray.d.x, dy = ray.d.y, dz = ray.d.z;
+    const float bx = cx * dx, ax = dx * dx, qx = cx * cx;
+    const float b = (sph ? bx + cy * dy : bx) + cz * dz;
+    const float a = (sph ? ax + dy * dy : ax) + dz * dz;
+    const float c = ((sph ? qx + cy * cy : qx) + cz * cz) - r * r;
+    const float disc = b * b - a * c;
+    if (!(disc > 0.f)) return ret;
+    const double y = sph ? ray.ya : ray.yc;
+    const float sq = __builtin_sqrtf(disc);
+    float temp = qdiv(-b - sq, a, y);
+    float hy = ray.o.y + temp * dy;
+    if (temp < tmax && temp > ray.tmin && (sph || (hy > lower && hy < upper))) {
+        tmax = temp;
+        kind = sph ? HK_SPHERE_ROOT1 : HK_CYL_SIDE;
+        return true;
+    }
+    temp = qdiv(-b + sq, a, y);
+    hy = ray.o.y + temp * dy;
+    if (temp < tmax && temp > ray.tmin && (sph || (hy > lower && hy < upper))) {
+        tmax = temp;
+        kind = sph ? HK_SPHERE_ROOT2 : HK_CYL_SIDE;
+        return true;
+    }
+    return ret;
+}
+
 template <bool FAST, bool CONS>
 __device__ __forceinline__ bool ranked_leaf_test(const Node& nd, const RayK& ray, float& tmax, int& kind, int& best_rank) {
     float tm = nd.miss < best_rank ? __int_as_float(__float_as_int(tmax) + 1) : tmax;
@@ -494,7 +543,11 @@ __device__ __forceinline__ bool ranked_leaf_test(const Node& nd, const RayK& ray
             if (slab_reject<FAST, true>(box, ray, walk_limit(tm))) return false;
         }
     }
-    if (!leaf_test(nd, ray, tm, kind)) return false;
+    if (CONS && CPT_UNIFIED_LEAF && ((nd.code & 1) == 0)) {   // sphere (0) or cylinder (2)
+        if (!sphere_cyl_test(nd, ray, tm, kind)) return false;
+    } else if (!leaf_test(nd, ray, tm, kind)) {
+        return false;
+    }
     tmax = tm;
     best_rank = nd.miss;
     return true;
@@ -601,6 +654,9 @@ __device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const R
     Node nd{};
     if (n_nodes > 0) nd = nodes(0);
     for (;;) {
+#if CPT_STAMPS == 2
+        const unsigned long long t0 = stamp();
+#endif
         const bool leaf = nd.code >= 0;
         if (ni < n_nodes && !(leaf && parked >= 0)) {
             if (STATS) cnt.nodes++;
@@ -616,7 +672,23 @@ __device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const R
         const bool stopped = parked >= 0 && (ni >= n_nodes || nd.code >= 0);
         const uint64_t w = __ballot(working);
         if (!w) break;
-        if (__popcll(__ballot(stopped)) * 64 >= CPT_SPEC_LEAF * __popcll(w)) {
+        const bool round = __popcll(__ballot(stopped)) * 64 >= CPT_SPEC_LEAF * __popcll(w);
+#if CPT_STAMPS == 2
+        const unsigned long long t1 = stamp();
+        cnt.st_slab += t1 - t0;   // stepping (and the ballots)
+#endif
+#if CPT_STAMPS == 3
+        // wave-level: walk iterations, leaf rounds, iterations with a lane stepping an inner node
+        if (lowest_active_lane()) {
+            cnt.st_iter++;
+            cnt.st_leaf += round;
+        }
+        {
+            const bool stepping = ni < n_nodes && parked < 0;
+            if (__ballot(stepping) != 0 && lowest_active_lane()) cnt.st_slab++;
+        }
+#endif
+        if (round) {
             if (CPT_SPEC_ONLY_STOPPED ? stopped : parked >= 0) {
                 if (STATS) cnt.prims++;
                 const Node lf = nodes(parked);
@@ -629,6 +701,11 @@ __device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const R
                 parked = -1;
             }
         }
+#if CPT_STAMPS == 2
+        const unsigned long long t2 = stamp();
+        cnt.st_leaf += t2 - t1;   // leaf round
+        cnt.st_iter += t2 - t0;
+#endif
     }
     if (best < 0) return 0;
     const Node w = nodes(best);
