@@ -30,10 +30,11 @@ METRIC = "Mpaths/sec (pixels×spp/s) at 1920×1080; achieved HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 
 
-def byte_model(st, paths):
-    """B_read = sum_segments[76 + 32 n_node + 32 n_prim + (hit ? 40 : 16)] + 16 P."""
-    return (76 * st["segments"] + 32 * st["nodes"] + 32 * st["prims"] + 40 * st["hits"] + 16 * st["misses"]
-            + 16 * paths)
+def byte_model(st, paths, node_bytes=32):
+    """B_read = sum_segments[76 + 32 n_node + 32 n_prim + (hit ? 40 : 16)] + 16 P.
+    node_bytes = 128 for the ordered walk's 4-wide nodes (four child boxes + refs per visit)."""
+    return (76 * st["segments"] + node_bytes * st["nodes"] + 32 * st["prims"] + 40 * st["hits"]
+            + 16 * st["misses"] + 16 * paths)
 
 
 def cpu_baseline(cfg, objs, sky, cam, seconds_hint=15.0, threads=None):
@@ -197,6 +198,8 @@ def main():
             v = _all_reduce(v)
         return dict(zip(KEYS, (int(x) for x in v.tolist())))
 
+    walk_info = r.walk_info()
+    walk_node_bytes = 128 if ordered and walk_info["n_wide"] > 0 else 32   # 4-wide walk nodes
     st = count_pass(False)
     walk_counts, walk_diff = None, None
     if ordered:
@@ -250,7 +253,7 @@ def main():
         # the reference algorithm's counts (its right-first DFS over its median tree, which
         # visits more nodes for the same closest hits) is reported beside it.
         bytes_ref = byte_model(st, paths_total) * share
-        bytes_launch = byte_model(walk_counts, paths_total) * share if walk_counts else bytes_ref
+        bytes_launch = byte_model(walk_counts, paths_total, walk_node_bytes) * share if walk_counts else bytes_ref
         achieved = bytes_launch / (avg_kernel_ms / 1e3) / 1e9
         achieved_ref_model = bytes_ref / (avg_kernel_ms / 1e3) / 1e9
         # HBM traffic per launch from rocprofv3 PMC passes of this same workload (committed under
@@ -294,7 +297,10 @@ def main():
                 "kernel": "k_megakernel" if args.path == "megakernel" else "wavefront (k_wf_extend+k_wf_shade per bounce)",
                 "kernel_avg_ms": round(avg_kernel_ms, 3),
                 "bytes_per_launch": int(bytes_launch),
-                "byte_model": "SURVEY.md 8(d): 76 S + 32 nodes + 32 prims + 40 hits + 16 misses + 16 P, on walk_counts",
+                "byte_model": f"SURVEY.md 8(d): 76 S + {walk_node_bytes if walk_counts else 32} nodes + 32 prims + 40 hits "
+                              f"+ 16 misses + 16 P, on walk_counts ({walk_node_bytes}-B nodes: "
+                              f"{'4-wide' if walk_node_bytes == 128 else 'binary'} walk tree)",
+                "walk_info": walk_info,
                 "walk_counts": walk_counts,
                 "reference_counts": st,
                 "walk_vs_reference_pixels_differing": walk_diff,

@@ -44,6 +44,7 @@ PROTOTYPES = {
     "cpt_get_stats": (_I, [_P, _P]),
     "cpt_reset_stats": (_I, [_P]),
     "cpt_get_raw_counters": (_I, [_P, _P]),
+    "cpt_get_walk_info": (_I, [_P, _P]),
     "cpt_last_render_ms": (_I, [_P, _P]),
     "cpt_last_kernel_stats": (_I, [_P, _P, _P]),
     "cpt_denoise_mix": (_I, [_P, _U32, _P]),

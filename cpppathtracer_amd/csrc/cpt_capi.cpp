@@ -13,6 +13,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/cpt.h"
@@ -300,6 +301,8 @@ struct cpt_ctx {
     std::vector<int> pos_of_node;      // BNode -> position in the reference order
     int n_bvh = 0;                     // nodes of the reference order
     int n_walk = 0;                    // nodes of each octant order (walk tree + unbounded leaves)
+    int n_wide = 0;                    // 4-wide walk-tree nodes per octant (0: none, binary walk)
+    int n_unb = 0;                     // unbounded (platform) leaves at the head of each octant order
     std::vector<Mat> mats_h;           // deduplicated materials (host-staged, see Mat)
     std::vector<int> mat_have_tex;     // per material slot: textured?
     std::vector<uint64_t> mat_tex;     // per material slot: texture handle (textured slots)
@@ -523,6 +526,102 @@ int build(HostBvh& t, const std::vector<cpt_object>& O, std::vector<int>& idx, i
 }
 }  // namespace sah
 
+// ------------------------------------------------------------------------------------
+// 4-wide walk tree (DESIGN.md §Wide walk).  The binary SAH walk tree is collapsed into
+// nodes of up to four children: starting from a node's two children, the internal child
+// with the largest box is replaced by its own two children until there are four (or only
+// leaves).  Every octant gets its own copy: the children in the near-first order of the
+// binary splits between the node and them (the binary octant order's rule), each child's
+// box in octant form (entry planes, exit planes).  Layout of one 128-B node, 32 dwords:
+//   [0..3] entry x of children 0..3, [4..7] entry y, [8..11] entry z,
+//   [12..15] exit x, [16..19] exit y, [20..23] exit z,
+//   [24..27] child refs: >= 0 a wide node of the same octant, <= -2 a leaf as ~(absolute
+//            Node index of the leaf in the octant-0 binary order), empty slots -1 with an
+//            inverted box that every ray rejects,
+//   [28..31] 0.
+// Nodes are numbered in preorder (root 0); octant o's node k starts at Node slot
+// n_bvh + 8 n_walk + 4 (o n_wide + k).  Returns n_wide, or 0 when the device walk's stack
+// (WIDE_STACK entries per lane, cpt_path.hpp) could overflow on this tree.
+// ------------------------------------------------------------------------------------
+constexpr int WIDE_STACK = CPT_WSTACK;
+
+int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int n_bvh, int n_unb,
+                   std::vector<Node>& out) {
+    std::vector<int> wbin;                      // binary node of each wide node
+    std::vector<std::vector<int>> kids;         // its children (binary node ids)
+    std::vector<int> wide_of(w.nodes.size(), -1);
+    auto area = [&](int b) {
+        const BNode& n = w.nodes[b];
+        const float dx = n.bmax.x - n.bmin.x, dy = n.bmax.y - n.bmin.y, dz = n.bmax.z - n.bmin.z;
+        return dx * dy + dy * dz + dz * dx;
+    };
+    int max_push = 0;
+    std::function<void(int, int)> make = [&](int b, int pushed) {
+        const int id = (int)wbin.size();
+        wbin.push_back(b);
+        wide_of[b] = id;
+        std::vector<int> ch = {w.nodes[b].left, w.nodes[b].right};
+        while (ch.size() < 4) {
+            int best = -1;
+            float ba = -1.f;
+            for (size_t k = 0; k < ch.size(); ++k)
+                if (!w.nodes[ch[k]].is_object && area(ch[k]) > ba) { ba = area(ch[k]); best = (int)k; }
+            if (best < 0) break;
+            const int x = ch[best];
+            ch.erase(ch.begin() + best);
+            ch.insert(ch.begin() + best, {w.nodes[x].left, w.nodes[x].right});
+        }
+        kids.push_back(ch);
+        // a lane entering this node keeps one hit child and pushes the others
+        pushed += (int)ch.size() - 1;
+        max_push = std::max(max_push, pushed);
+        for (int x : ch)
+            if (!w.nodes[x].is_object) make(x, pushed);
+    };
+    make(root, n_unb);   // the walk starts with the root and the platforms on the stack
+    if (max_push + 1 > WIDE_STACK) return 0;
+    const int n_wide = (int)wbin.size();
+    const size_t base = out.size();
+    out.resize(base + (size_t)8 * n_wide * 4);
+    for (int o = 0; o < 8; ++o) {
+        for (int id = 0; id < n_wide; ++id) {
+            const std::vector<int>& ch = kids[id];
+            std::vector<int> ord;
+            std::function<void(int)> rec = [&](int x) {
+                if (std::find(ch.begin(), ch.end(), x) != ch.end()) { ord.push_back(x); return; }
+                const BNode& n = w.nodes[x];
+                const bool right_first = (o >> n.axis) & 1;
+                rec(right_first ? n.right : n.left);
+                rec(right_first ? n.left : n.right);
+            };
+            rec(wbin[id]);
+            float f[24];
+            int32_t ref[4];
+            for (int k = 0; k < 4; ++k) {
+                F3 lo{1e30f, 1e30f, 1e30f}, hi{-1e30f, -1e30f, -1e30f};
+                ref[k] = -1;
+                if (k < (int)ord.size()) {
+                    const BNode& n = w.nodes[ord[k]];
+                    lo = n.bmin;
+                    hi = n.bmax;
+                    ref[k] = n.is_object ? ~(n_bvh + pos0[ord[k]]) : wide_of[ord[k]];
+                }
+                const float l3[3] = {lo.x, lo.y, lo.z}, h3[3] = {hi.x, hi.y, hi.z};
+                for (int a = 0; a < 3; ++a) {
+                    const bool neg = (o >> a) & 1;
+                    f[a * 4 + k] = neg ? h3[a] : l3[a];         // entry plane
+                    f[12 + a * 4 + k] = neg ? l3[a] : h3[a];    // exit plane
+                }
+            }
+            uint32_t dw[32] = {0};
+            std::memcpy(dw, f, sizeof(f));
+            std::memcpy(dw + 24, ref, sizeof(ref));
+            std::memcpy(&out[base + ((size_t)o * n_wide + id) * 4], dw, sizeof(dw));
+        }
+    }
+    return n_wide;
+}
+
 // Returns the walk tree's root (-1: no bounded primitive); `unbounded` = its platform leaves
 // by reference rank; `rank` = the reference rank of every walk-tree leaf.
 int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, std::vector<int>& rank);
@@ -532,15 +631,22 @@ int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, s
 void linearise_all(cpt_ctx* c) {
     c->lin.clear();
     c->n_walk = 0;
+    c->n_wide = 0;
+    c->n_unb = 0;
     c->lin.reserve(9 * c->bvh.nodes.size());
     linearise(c->bvh, c->objs, c->mat_of_obj, c->lin, c->pos_of_node, -1, nullptr);
     c->n_bvh = (int)c->lin.size();
     if (c->n_bvh == 0) return;
     HostBvh w;
-    std::vector<int> unbounded, rank, pos;
+    std::vector<int> unbounded, rank, pos, pos0;
     const int root = build_walk_tree(c, w, unbounded, rank);
-    for (int o = 0; o < 8; ++o) linearise(w, c->objs, c->mat_of_obj, c->lin, pos, o, &rank, root, unbounded);
+    for (int o = 0; o < 8; ++o) {
+        linearise(w, c->objs, c->mat_of_obj, c->lin, pos, o, &rank, root, unbounded);
+        if (o == 0) pos0 = pos;
+    }
     c->n_walk = (int)(c->lin.size() - c->n_bvh) / 8;
+    c->n_unb = (int)unbounded.size();
+    if (CPT_WIDE && root >= 0 && !w.nodes[root].is_object) c->n_wide = linearise_wide(w, root, pos0, c->n_bvh, c->n_unb, c->lin);
 }
 
 int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, std::vector<int>& rank) {
@@ -954,6 +1060,8 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     p.mats = c->d_mats;
     p.n_nodes = c->n_bvh;
     p.n_walk = c->n_walk;
+    p.n_wide = c->n_wide;
+    p.n_unb = c->n_unb;
     p.ordered = (flags & CPT_TRAVERSAL_ORDERED) ? ((flags & CPT_TRAVERSAL_PLAIN_LEAVES) ? 2 : 1) : 0;
     p.env = c->d_env;
     p.env_w = c->env_w;
@@ -1076,6 +1184,15 @@ int cpt_get_raw_counters(cpt_ctx* c, uint64_t* out8) {
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream()));
     HIP_TRY(c, hipMemcpy(out8, c->d_stats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return CPT_OK;
+}
+
+int cpt_get_walk_info(cpt_ctx* c, int32_t* out4) {
+    if (!c || !out4) return CPT_ERR_INVALID_ARG;
+    out4[0] = c->n_bvh;
+    out4[1] = c->n_walk;
+    out4[2] = c->n_wide;
+    out4[3] = c->n_unb;
     return CPT_OK;
 }
 

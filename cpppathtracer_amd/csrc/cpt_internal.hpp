@@ -6,6 +6,14 @@
 
 #include "cpt_device.hpp"
 
+#ifndef CPT_WIDE
+#define CPT_WIDE 1      // the ordered walk runs on the 4-wide walk tree (0: the binary octant orders)
+#endif
+#ifndef CPT_WSTACK
+#define CPT_WSTACK 32   // per-lane LDS stack entries of the wide walk; the host keeps the binary
+                        // walk for a tree that could need more (cpt_capi.cpp linearise_wide)
+#endif
+
 namespace cpt {
 
 // Camera snapshot as the kernel needs it (the reference passes the whole MotionalCamera by
@@ -25,6 +33,9 @@ struct KParams {
                             // the walk tree's eight octant orders (n_walk each)
     const Mat* mats;        // deduplicated materials, indexed by Node::code >> 2
     int n_nodes, n_walk;
+    int n_wide;             // 4-wide walk-tree nodes per octant, after the eight octant orders
+                            // (0: the ordered walk uses the binary octant orders)
+    int n_unb;              // unbounded leaves at the head of every octant order
     int ordered;            // CPT_TRAVERSAL_ORDERED: walk the ray's octant order (2: plain leaves)
     const uint32_t* env;    // packed RGBA8, env_cols x env_h
     int env_w, env_h, env_cols;

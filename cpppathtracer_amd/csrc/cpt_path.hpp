@@ -435,7 +435,7 @@ struct PtrSrc {
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(const KParams& p) {
-    const uint32_t bytes = (uint32_t)(p.n_nodes + 8 * p.n_walk) * (uint32_t)sizeof(Node);
+    const uint32_t bytes = (uint32_t)(p.n_nodes + 8 * p.n_walk + 32 * p.n_wide) * (uint32_t)sizeof(Node);
     return __builtin_amdgcn_make_buffer_rsrc((void*)p.nodes, (short)0, (int)bytes, 0x00020000);
 }
 
@@ -717,6 +717,128 @@ __device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const R
     return 1;
 }
 
+// ======================================================================================
+// The ordered walk on the 4-wide walk tree (CPT_WIDE, DESIGN.md §Wide walk).  One
+// iteration loads a 128-B node (cpt_capi.cpp linearise_wide) and tests its four children's
+// boxes with the conservative octant-form slab; the nearest hit child is taken next, the
+// other hits go onto a per-lane stack in LDS (far ones first).  Leaves are parked and tested
+// in wave-wide rounds as in trace_spec; a leaf is parked without a node iteration.  The
+// boxes tested are the binary tree's, so the same superset argument holds: every primitive
+// the plain walk tests, whose box passes the conservative test, is tested here too, under a
+// limit that is never below the final tmax; the rank rule and the certificate are unchanged.
+// ======================================================================================
+constexpr int WIDE_LANES = 256;   // block size of every kernel that walks (stack stride)
+
+struct WideNode {
+    f2v e[3][2], x[3][2];   // entry / exit planes per axis, children (0,1) and (2,3)
+    int ref[4];
+};
+
+__device__ __forceinline__ WideNode load_wide(__amdgpu_buffer_rsrc_t rsrc, uint32_t off) {
+    WideNode n;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16 * q, 0, 0);
+        f2v lo = {__uint_as_float(v.x), __uint_as_float(v.y)}, hi = {__uint_as_float(v.z), __uint_as_float(v.w)};
+        if (q < 3) { n.e[q][0] = lo; n.e[q][1] = hi; }
+        else { n.x[q - 3][0] = lo; n.x[q - 3][1] = hi; }
+    }
+    const v4u32 r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 96, 0, 0);
+    n.ref[0] = (int)r.x; n.ref[1] = (int)r.y; n.ref[2] = (int)r.z; n.ref[3] = (int)r.w;
+    return n;
+}
+
+// Hit mask of the four children: slab_reject_octant for each, two children per packed op.
+__device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], const RayK& ray, float limit) {
+    const f2v ox = {ray.o.x, ray.o.x}, oy = {ray.o.y, ray.o.y}, oz = {ray.o.z, ray.o.z};
+    const f2v ix = {ray.ix, ray.ix}, iy = {ray.iy, ray.iy}, iz = {ray.iz, ray.iz};
+    const f2v bx = {ray.bx, ray.bx}, by = {ray.by, ray.by}, bz = {ray.bz, ray.bz};
+    const f2v tnx = __builtin_elementwise_fma(e[0] - ox, ix, -bx), tfx = __builtin_elementwise_fma(x[0] - ox, ix, bx);
+    const f2v tny = __builtin_elementwise_fma(e[1] - oy, iy, -by), tfy = __builtin_elementwise_fma(x[1] - oy, iy, by);
+    const f2v tnz = __builtin_elementwise_fma(e[2] - oz, iz, -bz), tfz = __builtin_elementwise_fma(x[2] - oz, iz, bz);
+    const float lo0 = __builtin_fmaxf(__builtin_fmaxf(tnx.x, tny.x), tnz.x);
+    const float hi0 = __builtin_fminf(__builtin_fminf(tfx.x, tfy.x), tfz.x);
+    const float lo1 = __builtin_fmaxf(__builtin_fmaxf(tnx.y, tny.y), tnz.y);
+    const float hi1 = __builtin_fminf(__builtin_fminf(tfx.y, tfy.y), tfz.y);
+    const float m0 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo0) + __builtin_fabsf(hi0), 2.0f * WALK_MARGIN_ABS);
+    const float m1 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo1) + __builtin_fabsf(hi1), 2.0f * WALK_MARGIN_ABS);
+    const bool rej0 = lo0 - hi0 > m0 || lo0 > limit || hi0 < ray.t3;
+    const bool rej1 = lo1 - hi1 > m1 || lo1 > limit || hi1 < ray.t3;
+    return (rej0 ? 0u : 1u) | (rej1 ? 0u : 2u);
+}
+
+template <bool STATS>
+__device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc_t rsrc, int oct, const RayK& ray,
+                                          Hit& h, int& code_out, Counters& cnt) {
+    __shared__ int wstack[CPT_WSTACK * WIDE_LANES];
+    int* const stk = wstack + threadIdx.x;
+    const BufSrc nodes{rsrc, 0u};   // leaves by absolute Node index
+    constexpr int NONE = -1;        // refs: >= 0 wide node, -1 none, <= -2 leaf ~index
+    float tmax = DEFAULT_RAY_TMAX;
+    int best = -1, kind = 0;
+    int best_rank = 0x7fffffff;
+    float limit = walk_limit(tmax);
+    // start: the platforms (reference-rank order, as at the head of the binary orders), then
+    // the tree's root
+    int sp = 0, cur = 0;
+    if (p.n_unb > 0) {
+        stk[0] = 0;
+        sp = 1;
+        for (int k = p.n_unb - 1; k >= 1; --k) stk[(sp++) * WIDE_LANES] = ~(p.n_nodes + k);
+        cur = ~p.n_nodes;
+    }
+    const uint32_t wbase = (uint32_t)(p.n_nodes + 8 * p.n_walk + 4 * oct * p.n_wide) * (uint32_t)sizeof(Node);
+    int parked = -1;
+    for (;;) {
+        if (cur <= -2 && parked < 0) {
+            parked = ~cur;
+            cur = sp > 0 ? stk[(--sp) * WIDE_LANES] : NONE;
+        }
+        if (cur >= 0) {
+            if (STATS) cnt.nodes++;
+            const WideNode n = load_wide(rsrc, wbase + (uint32_t)cur * 128u);
+            const f2v e01[3] = {n.e[0][0], n.e[1][0], n.e[2][0]}, x01[3] = {n.x[0][0], n.x[1][0], n.x[2][0]};
+            const f2v e23[3] = {n.e[0][1], n.e[1][1], n.e[2][1]}, x23[3] = {n.x[0][1], n.x[1][1], n.x[2][1]};
+            const uint32_t m = wide_pair(e01, x01, ray, limit) | (wide_pair(e23, x23, ray, limit) << 2);
+            int next = NONE;
+#pragma unroll
+            for (int k = 3; k >= 0; --k) {
+                if ((m >> k) & 1u) {
+                    if (next != NONE) stk[(sp++) * WIDE_LANES] = next;
+                    next = n.ref[k];
+                }
+            }
+            if (next == NONE && sp > 0) next = stk[(--sp) * WIDE_LANES];
+            cur = next;
+        }
+        const bool working = parked >= 0 || cur != NONE;
+        const bool stopped = parked >= 0 && cur <= -1;
+        const uint64_t w = __ballot(working);
+        if (!w) break;
+        if (__popcll(__ballot(stopped)) * 64 >= CPT_SPEC_LEAF * __popcll(w)) {
+            if (parked >= 0) {
+                if (STATS) cnt.prims++;
+                const Node lf = nodes(parked);
+                int k;
+                if (ranked_leaf_test<true, true>(lf, ray, tmax, k, best_rank)) {
+                    best = parked;
+                    kind = k;
+                    limit = walk_limit(tmax);
+                }
+                parked = -1;
+            }
+        }
+    }
+    if (best < 0) return 0;
+    const Node wn = nodes(best);
+    Node box;
+    leaf_aabb(wn, box);
+    if (slab_reject<true>(box, ray, tmax)) return -1;
+    h = hit_attributes(wn, ray, tmax, kind);
+    code_out = wn.code;
+    return 1;
+}
+
 // TraceRay for one segment: the reference order, or the ordered walk with its certificate
 // and the reference-order fallback (CPT_TRAVERSAL_ORDERED).
 template <bool STATS>
@@ -724,10 +846,15 @@ __device__ __forceinline__ bool trace_segment(const KParams& p, const RayK& rk, 
                                               Counters& cnt) {
     const __amdgpu_buffer_rsrc_t rsrc = node_rsrc(p);
     if (p.ordered && __builtin_expect(finite, 1)) {
-        int n;
-        const BufSrc order{rsrc, walk_order(p, rk.d, n) * (uint32_t)sizeof(Node)};
-        const int r = CPT_SPEC_LEAF && p.ordered == 1 ? trace_spec<STATS, true>(order, n, rk, h, code, cnt)
-                                                      : trace<STATS, true, true>(order, n, rk, h, code, cnt);
+        int n, r;
+        if (p.ordered == 1 && p.n_wide > 0) {   // n_wide = 0 unless CPT_WIDE
+            const int oct = (rk.d.x < 0.f ? 1 : 0) | (rk.d.y < 0.f ? 2 : 0) | (rk.d.z < 0.f ? 4 : 0);
+            r = trace_wide<STATS>(p, rsrc, oct, rk, h, code, cnt);
+        } else {
+            const BufSrc order{rsrc, walk_order(p, rk.d, n) * (uint32_t)sizeof(Node)};
+            r = CPT_SPEC_LEAF && p.ordered == 1 ? trace_spec<STATS, true>(order, n, rk, h, code, cnt)
+                                                : trace<STATS, true, true>(order, n, rk, h, code, cnt);
+        }
         if (__builtin_expect(r >= 0, 1)) return r > 0;
         if (STATS) cnt.fallbacks++;
     }

@@ -188,6 +188,12 @@ class Renderer:
         self._check(self._L.cpt_get_raw_counters(self._ctx, _p(out)))
         return [int(x) for x in out]
 
+    def walk_info(self):
+        """[reference-order nodes, binary octant-order nodes, 4-wide nodes per octant, platforms]."""
+        out = np.zeros(4, dtype=np.int32)
+        self._check(self._L.cpt_get_walk_info(self._ctx, _p(out)))
+        return dict(zip(("n_bvh", "n_walk", "n_wide", "n_unb"), (int(x) for x in out)))
+
     def reset_stats(self):
         self._check(self._L.cpt_reset_stats(self._ctx))
 

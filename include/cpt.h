@@ -218,6 +218,12 @@ int cpt_reset_stats(cpt_ctx* ctx);
  * winner certificate and took the reference walk (CPT_RENDER_STATS | CPT_TRAVERSAL_ORDERED);
  * 5-7 in a CPT_STAMPS diagnostic build: refill, traversal, shading cycle sums). */
 int cpt_get_raw_counters(cpt_ctx* ctx, uint64_t* out8);
+/* Node counts of the scene's walk structures (host-side, no GPU work): [0] the reference
+ * order (bvh.cu's tree, 32-B nodes), [1] each octant order of the binary walk tree, [2] the
+ * 4-wide walk tree's nodes per octant (128 B each; 0 = the ordered walk uses the binary
+ * orders), [3] the unbounded (platform) leaves tested before the walk tree.  With [2] > 0,
+ * the `nodes` counter of an ordered render counts 4-wide node visits. */
+int cpt_get_walk_info(cpt_ctx* ctx, int32_t* out4);
 /* Device time of the last cpt_render (HIP events on the launch stream); waits for it. */
 int cpt_last_render_ms(cpt_ctx* ctx, float* ms);
 /* Average device time of one kernel launch of the last cpt_render's dominant kernel. */

@@ -130,7 +130,7 @@ CASES = [
 # leaf where the walk meets it (CPT_TRAVERSAL_PLAIN_LEAVES): its node/prim counts equal the
 # oracle's diagnostic restatement of the ordered walk (oracle.set_walk), including the number
 # of segments whose winner certificate failed (reference-walk fallback).  The default
-# ordered walk parks leaves for wave-wide rounds: counts at least the plain walk's.
+# ordered walk runs on 4-wide nodes and parks leaves for wave-wide rounds.
 PATHS = ["megakernel", "wavefront", "megakernel:ordered", "wavefront:ordered", "megakernel:plain",
          "wavefront:plain"]
 
@@ -141,12 +141,14 @@ def _check_stats(gs, os_, path):
             assert gs[k] == os_[k], k
         assert gs == os_["walk"]
     elif path.endswith(":ordered"):
-        # postponed leaves: the same closest hits (so segments/hits/misses and the winner
-        # certificates match); each ray walks a superset of the plain walk's nodes and leaves
+        # the default ordered walk (4-wide nodes, postponed leaves) finds the same closest
+        # hits, so segments/hits/misses and the winner certificates match; its node and
+        # primitive counts are its own (wide nodes; leaves whose box the parent rejected are
+        # never tested)
         for k in ("segments", "hits", "misses"):
             assert gs[k] == os_[k], k
         assert gs["fallbacks"] == os_["walk"]["fallbacks"]
-        assert gs["nodes"] >= os_["walk"]["nodes"] and gs["prims"] >= os_["walk"]["prims"]
+        assert (gs["nodes"] > 0) == (os_["walk"]["nodes"] > 0)
     else:
         assert gs == os_
 

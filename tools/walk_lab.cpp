@@ -17,6 +17,8 @@
 //      the segment falls back to the reference walk (counted)
 //   6  as 4, with the margin and the certificate of mode 5
 #include "../oracle/cpt_oracle.cpp"
+#include <cstdlib>
+#include <functional>
 
 namespace lab {
 
@@ -25,7 +27,15 @@ struct ANode {
     int left = -1, right = -1, obj = -1, axis = 0;
 };
 
+struct WNode {               // mode 7: 4-wide node, children per octant in near-first order
+    int child[8][4];
+    int n = 0;
+};
+
 struct Tree {
+    std::vector<WNode> wide;
+    std::vector<ANode> wbox;   // box of each wide node
+    int wroot = -1;
     std::vector<ANode> nodes;
     std::vector<int> unbounded;      // objects tested before the walk
     std::vector<int> rank_of_obj;    // reference right-first preorder rank of each object's leaf
@@ -90,14 +100,14 @@ int build_sah(Tree& t, const Object* O, std::vector<int>& idx, int l, int r) {
         f3 c = mk((a.x + b.x) * .5f, (a.y + b.y) * .5f, (a.z + b.z) * .5f);
         clo = fmin3(clo, c); chi = fmax3(chi, c);
     }
-    const int NB = 16;
+    static const int NB = std::getenv("LAB_NB") ? std::max(2, std::min(256, std::atoi(std::getenv("LAB_NB")))) : 16;
     float best = 1e38f;
     int best_axis = -1, best_bin = -1;
     for (int axis = 0; axis < 3; ++axis) {
         float e0 = comp(clo, axis), e1 = comp(chi, axis);
         if (!(e1 > e0)) continue;
-        int cnt[NB] = {0};
-        f3 blo[NB], bhi[NB];
+        int cnt[256] = {0};
+        f3 blo[256], bhi[256];
         for (int b = 0; b < NB; ++b) { blo[b] = mk(1e30f, 1e30f, 1e30f); bhi[b] = mk(-1e30f, -1e30f, -1e30f); }
         for (int i = l; i < r; ++i) {
             f3 a = aabb_min(O[idx[i]]), bb = aabb_max(O[idx[i]]);
@@ -184,6 +194,49 @@ void prepare(const Bvh& bvh) {
             t.root = g_mode == 2 ? build_median(t, bvh.objs, idx, 0, (int)idx.size())
                                  : build_sah(t, bvh.objs, idx, 0, (int)idx.size());
     }
+    if (g_mode == 7 && t.root >= 0 && t.nodes[t.root].obj < 0) {
+        // collapse: replace the largest-area internal child by its two children until 4
+        std::function<int(int)> collapse = [&](int b) -> int {
+            std::vector<int> ch = {t.nodes[b].left, t.nodes[b].right};
+            while (ch.size() < 4) {
+                int best = -1; float ba = -1.f;
+                for (size_t k = 0; k < ch.size(); ++k) {
+                    const ANode& c = t.nodes[ch[k]];
+                    if (c.obj >= 0) continue;
+                    const float dx = c.bmax.x - c.bmin.x, dy = c.bmax.y - c.bmin.y, dz = c.bmax.z - c.bmin.z;
+                    const float a = dx * dy + dy * dz + dz * dx;
+                    if (a > ba) { ba = a; best = (int)k; }
+                }
+                if (best < 0) break;
+                const int c = ch[best];
+                ch.erase(ch.begin() + best);
+                ch.insert(ch.begin() + best, {t.nodes[c].left, t.nodes[c].right});
+            }
+            // octant orders: near-first by the binary subtree's split axes, via a recursive
+            // order over the binary nodes between b and its wide children
+            const int me = (int)t.wide.size();
+            t.wide.push_back(WNode{});
+            t.wbox.push_back(t.nodes[b]);
+            std::vector<int> wch(ch.size());
+            for (size_t k = 0; k < ch.size(); ++k) wch[k] = t.nodes[ch[k]].obj >= 0 ? -1 - ch[k] : collapse(ch[k]);
+            WNode& w = t.wide[me];
+            w.n = (int)ch.size();
+            for (int o = 0; o < 8; ++o) {
+                std::vector<int> ord;
+                std::function<void(int)> rec = [&](int x) {
+                    for (size_t k = 0; k < ch.size(); ++k) if (ch[k] == x) { ord.push_back(wch[k]); return; }
+                    const ANode& n = t.nodes[x];
+                    const bool neg = (o >> n.axis) & 1;
+                    rec(neg ? n.right : n.left);
+                    rec(neg ? n.left : n.right);
+                };
+                rec(b);
+                for (int k = 0; k < w.n; ++k) t.wide[me].child[o][k] = ord[k];
+            }
+            return me;
+        };
+        t.wroot = collapse(t.root);
+    }
     g_tree = std::move(t);
     std::atomic_thread_fence(std::memory_order_seq_cst);
     g_src = &bvh;
@@ -210,6 +263,8 @@ bool slab_ok(const ANode& n, const Ray& ray) {
     hi = hi + (g_margin * fabsf(hi) + 1e-4f);
     return !(lo > hi || lo > ray.tmax || hi < ray.tmin);
 }
+
+std::atomic<uint64_t> g_boxes{0};
 
 bool alt_trace(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, uint64_t& nodes, uint64_t& prims) {
     const Tree& t = g_tree;
@@ -252,6 +307,29 @@ bool alt_trace(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, uint64_t& node
     };
     for (int o : t.unbounded) test(o);
     if (t.root < 0) return ret;
+    if (g_mode == 7 && t.wroot >= 0) {
+        const int oct = (ray.dir.x < 0.f ? 1 : 0) | (ray.dir.y < 0.f ? 2 : 0) | (ray.dir.z < 0.f ? 4 : 0);
+        int st[512], tp = 0;
+        st[tp++] = t.wroot;
+        while (tp > 0) {
+            const int x = st[--tp];
+            nodes++;                       // iterations (pops)
+            if (x < 0) { test(t.nodes[-1 - x].obj); continue; }
+            const WNode& w = t.wide[x];
+            int hit[4], nh = 0;
+            for (int k = 0; k < w.n; ++k) {
+                const int c = w.child[oct][k];
+                g_boxes++;
+                const ANode& cn = c < 0 ? t.nodes[-1 - c] : t.nodes[0];
+                ANode box;
+                if (c < 0) box = cn;
+                else { box.bmin = t.wbox[c].bmin; box.bmax = t.wbox[c].bmax; }
+                if (slab_ok(box, ray)) hit[nh++] = c;
+            }
+            for (int k = nh - 1; k >= 0; --k) st[tp++] = hit[k];
+        }
+        return ret;
+    }
     int stack[512], top = 0;
     stack[top++] = t.root;
     const float d[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
@@ -321,7 +399,9 @@ void lab_set_mode(int m) {
 void lab_counts(uint64_t out[6]) {
     out[0] = lab::g_segments; out[1] = lab::g_nodes; out[2] = lab::g_prims; out[3] = lab::g_diff; out[4] = lab::g_diff_obj;
     out[5] = lab::g_fallback;
-    fprintf(stderr, "pretest misses: %llu\n", (unsigned long long)lab::g_pretest_miss.load());
+    fprintf(stderr, "pretest misses: %llu, wide box tests/seg %.2f\n", (unsigned long long)lab::g_pretest_miss.load(),
+            lab::g_segments ? (double)lab::g_boxes.load() / lab::g_segments : 0.0);
+    lab::g_boxes = 0;
     lab::g_pretest_miss = 0;
     lab::g_segments = lab::g_nodes = lab::g_prims = lab::g_diff = lab::g_diff_obj = lab::g_fallback = 0;
 }
