@@ -727,6 +727,12 @@ __device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const R
 // the plain walk tests, whose box passes the conservative test, is tested here too, under a
 // limit that is never below the final tmax; the rank rule and the certificate are unchanged.
 // ======================================================================================
+#ifndef CPT_WIDE_CULL
+#define CPT_WIDE_CULL 0    // keep each stack entry's entry distance; pops beyond the limit are dropped
+#endif
+#ifndef CPT_WIDE_PARK2
+#define CPT_WIDE_PARK2 1   // park the nearest hit leaf in the node's own iteration (+2% A/B)
+#endif
 constexpr int WIDE_LANES = 256;   // block size of every kernel that walks (stack stride)
 
 struct WideNode {
@@ -749,7 +755,7 @@ __device__ __forceinline__ WideNode load_wide(__amdgpu_buffer_rsrc_t rsrc, uint3
 }
 
 // Hit mask of the four children: slab_reject_octant for each, two children per packed op.
-__device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], const RayK& ray, float limit) {
+__device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], const RayK& ray, float limit, f2v& los) {
     const f2v ox = {ray.o.x, ray.o.x}, oy = {ray.o.y, ray.o.y}, oz = {ray.o.z, ray.o.z};
     const f2v ix = {ray.ix, ray.ix}, iy = {ray.iy, ray.iy}, iz = {ray.iz, ray.iz};
     const f2v bx = {ray.bx, ray.bx}, by = {ray.by, ray.by}, bz = {ray.bz, ray.bz};
@@ -764,6 +770,7 @@ __device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], co
     const float m1 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo1) + __builtin_fabsf(hi1), 2.0f * WALK_MARGIN_ABS);
     const bool rej0 = lo0 - hi0 > m0 || lo0 > limit || hi0 < ray.t3;
     const bool rej1 = lo1 - hi1 > m1 || lo1 > limit || hi1 < ray.t3;
+    los = {lo0, lo1};
     return (rej0 ? 0u : 1u) | (rej1 ? 0u : 2u);
 }
 
@@ -772,6 +779,12 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
                                           Hit& h, int& code_out, Counters& cnt) {
     __shared__ int wstack[CPT_WSTACK * WIDE_LANES];
     int* const stk = wstack + threadIdx.x;
+#if CPT_WIDE_CULL
+    __shared__ float wstack_lo[CPT_WSTACK * WIDE_LANES];
+    float* const stk_lo = wstack_lo + threadIdx.x;
+#else
+    float* const stk_lo = nullptr;
+#endif
     const BufSrc nodes{rsrc, 0u};   // leaves by absolute Node index
     constexpr int NONE = -1;        // refs: >= 0 wide node, -1 none, <= -2 leaf ~index
     float tmax = DEFAULT_RAY_TMAX;
@@ -782,40 +795,77 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     // the tree's root
     int sp = 0, cur = 0;
     if (p.n_unb > 0) {
-        stk[0] = 0;
-        sp = 1;
-        for (int k = p.n_unb - 1; k >= 1; --k) stk[(sp++) * WIDE_LANES] = ~(p.n_nodes + k);
+        for (int k = p.n_unb; k >= 1; --k) {   // the root, then platforms n_unb-1 .. 1
+            stk[sp * WIDE_LANES] = k == p.n_unb ? 0 : ~(p.n_nodes + k);
+            if (CPT_WIDE_CULL) stk_lo[sp * WIDE_LANES] = -3.0e38f;
+            sp++;
+        }
         cur = ~p.n_nodes;
     }
     const uint32_t wbase = (uint32_t)(p.n_nodes + 8 * p.n_walk + 4 * oct * p.n_wide) * (uint32_t)sizeof(Node);
     int parked = -1;
+    // next stack entry (NONE when empty); with CPT_WIDE_CULL entries whose box starts beyond the
+    // current limit are dropped (the limit only shrinks, so they can no longer hold a winner)
+    auto pop = [&]() -> int {
+        while (sp > 0) {
+            --sp;
+            const int e = stk[sp * WIDE_LANES];
+            if (!CPT_WIDE_CULL || stk_lo[sp * WIDE_LANES] <= limit) return e;
+        }
+        return NONE;
+    };
     for (;;) {
+#if CPT_STAMPS == 2
+        const unsigned long long t0 = stamp();
+#endif
         if (cur <= -2 && parked < 0) {
             parked = ~cur;
-            cur = sp > 0 ? stk[(--sp) * WIDE_LANES] : NONE;
+            cur = pop();
         }
         if (cur >= 0) {
             if (STATS) cnt.nodes++;
             const WideNode n = load_wide(rsrc, wbase + (uint32_t)cur * 128u);
             const f2v e01[3] = {n.e[0][0], n.e[1][0], n.e[2][0]}, x01[3] = {n.x[0][0], n.x[1][0], n.x[2][0]};
             const f2v e23[3] = {n.e[0][1], n.e[1][1], n.e[2][1]}, x23[3] = {n.x[0][1], n.x[1][1], n.x[2][1]};
-            const uint32_t m = wide_pair(e01, x01, ray, limit) | (wide_pair(e23, x23, ray, limit) << 2);
+            f2v lo01, lo23;
+            const uint32_t m = wide_pair(e01, x01, ray, limit, lo01) | (wide_pair(e23, x23, ray, limit, lo23) << 2);
+            const float lo[4] = {lo01.x, lo01.y, lo23.x, lo23.y};
             int next = NONE;
+            float next_lo = 0.f;
 #pragma unroll
             for (int k = 3; k >= 0; --k) {
                 if ((m >> k) & 1u) {
-                    if (next != NONE) stk[(sp++) * WIDE_LANES] = next;
+                    if (next != NONE) {
+                        stk[sp * WIDE_LANES] = next;
+                        if (CPT_WIDE_CULL) stk_lo[sp * WIDE_LANES] = next_lo;
+                        sp++;
+                    }
                     next = n.ref[k];
+                    next_lo = lo[k];
                 }
             }
-            if (next == NONE && sp > 0) next = stk[(--sp) * WIDE_LANES];
+            if (next == NONE) next = pop();
             cur = next;
+            if (CPT_WIDE_PARK2 && cur <= -2 && parked < 0) {   // park the nearest leaf at once
+                parked = ~cur;
+                cur = pop();
+            }
         }
         const bool working = parked >= 0 || cur != NONE;
         const bool stopped = parked >= 0 && cur <= -1;
         const uint64_t w = __ballot(working);
         if (!w) break;
-        if (__popcll(__ballot(stopped)) * 64 >= CPT_SPEC_LEAF * __popcll(w)) {
+        const bool round = __popcll(__ballot(stopped)) * 64 >= CPT_SPEC_LEAF * __popcll(w);
+#if CPT_STAMPS == 2
+        const unsigned long long t1 = stamp();
+        cnt.st_slab += t1 - t0;
+#elif CPT_STAMPS == 3
+        if (lowest_active_lane()) {
+            cnt.st_iter++;
+            cnt.st_leaf += round;
+        }
+#endif
+        if (round) {
             if (parked >= 0) {
                 if (STATS) cnt.prims++;
                 const Node lf = nodes(parked);
@@ -828,6 +878,11 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
                 parked = -1;
             }
         }
+#if CPT_STAMPS == 2
+        const unsigned long long t2 = stamp();
+        cnt.st_leaf += t2 - t1;
+        cnt.st_iter += t2 - t0;
+#endif
     }
     if (best < 0) return 0;
     const Node wn = nodes(best);

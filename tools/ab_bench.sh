@@ -14,5 +14,5 @@ for lib in cpppathtracer_amd/libcpt.so build/ab/*.so; do
     CPT_LIB_PATH=$PWD/$lib timeout -k 10 300 python bench.py $args > /tmp/ab_out.txt 2>&1
     rc=$?
     [ $rc -eq 0 ] || { echo "bench rc=$rc"; tail -n 5 /tmp/ab_out.txt; exit $rc; }
-    tail -n 1 /tmp/ab_out.txt | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], 'Mpaths/s', d['roofline']['kernel_avg_ms'], 'ms', d['roofline']['frac'])"
+    tail -n 1 /tmp/ab_out.txt | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], 'Mpaths/s', d['roofline']['kernel_avg_ms'], 'ms', d['roofline']['frac'], d['roofline'].get('walk_info'), d['roofline'].get('walk_counts'))"
 done

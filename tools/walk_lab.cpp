@@ -264,7 +264,7 @@ bool slab_ok(const ANode& n, const Ray& ray) {
     return !(lo > hi || lo > ray.tmax || hi < ray.tmin);
 }
 
-std::atomic<uint64_t> g_boxes{0};
+std::atomic<uint64_t> g_boxes{0}, g_stale{0};
 
 bool alt_trace(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, uint64_t& nodes, uint64_t& prims) {
     const Tree& t = g_tree;
@@ -313,6 +313,12 @@ bool alt_trace(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, uint64_t& node
         st[tp++] = t.wroot;
         while (tp > 0) {
             const int x = st[--tp];
+            if (std::getenv("LAB_CULL")) {   // re-test the popped entry's box at the current tmax
+                ANode box;
+                if (x < 0) box = t.nodes[-1 - x];
+                else { box.bmin = t.wbox[x].bmin; box.bmax = t.wbox[x].bmax; }
+                if (x != t.wroot && !slab_ok(box, ray)) { g_stale++; continue; }
+            }
             nodes++;                       // iterations (pops)
             if (x < 0) { test(t.nodes[-1 - x].obj); continue; }
             const WNode& w = t.wide[x];
@@ -401,7 +407,9 @@ void lab_counts(uint64_t out[6]) {
     out[5] = lab::g_fallback;
     fprintf(stderr, "pretest misses: %llu, wide box tests/seg %.2f\n", (unsigned long long)lab::g_pretest_miss.load(),
             lab::g_segments ? (double)lab::g_boxes.load() / lab::g_segments : 0.0);
+    fprintf(stderr, "stale pops/seg %.3f\n", lab::g_segments ? (double)lab::g_stale.load() / lab::g_segments : 0.0);
     lab::g_boxes = 0;
+    lab::g_stale = 0;
     lab::g_pretest_miss = 0;
     lab::g_segments = lab::g_nodes = lab::g_prims = lab::g_diff = lab::g_diff_obj = lab::g_fallback = 0;
 }
