@@ -248,6 +248,27 @@ __device__ inline float asinf_(float xf) {
     return (float)atan(x / __builtin_sqrt((1.0 - x) * (1.0 + x)));
 }
 
+// (double)a / REF_PI, correctly rounded, for a float a, without the divide sequence:
+// q = RN(a y) with y = RN(1/pi) is within 1 ulp of the quotient, r = a - q pi is exact in one
+// fma, and RN(q + r y) is the correctly rounded quotient (Markstein's theorem; pi's
+// significand is not all ones).  a = +-0 returns q itself (keeps the zero's sign).
+// tests/test_exact_identities.py checks it against the IEEE divide for every float in
+// [-2, 2] (asinf_ returns |a| <= pi/2; atanf_ / 2 returns |a| <= pi/4).
+__device__ __forceinline__ double div_pi(float a) {
+    constexpr double INV_PI = 1.0 / REF_PI;
+    const double q = (double)a * INV_PI;
+    if (q == 0.0) return q;
+    const double r = __builtin_fma(-q, REF_PI, (double)a);
+    return __builtin_fma(r, INV_PI, q);
+}
+
+// (float)k / 255.0f for an integer 0 <= k <= 255: the exact-quotient rule of qdiv
+// (cpt_device.hpp) with the double reciprocal of 255 (every k/255 > 0 is a normal float, and
+// 0 gives +0), checked for all 256 k in tests/test_exact_identities.py.
+__device__ __forceinline__ float div255(uint32_t k) {
+    return (float)((double)k * (1.0 / 255.0));
+}
+
 }  // namespace dm
 
 // ------------------------------------------------------------------------------------

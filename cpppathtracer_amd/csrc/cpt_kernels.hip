@@ -151,13 +151,21 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             t2 = stamp();
             Shade sh;
             v3 attr_normal;
+#if CPT_STAMPS == 4
+            const unsigned long long s0 = stamp();
+#endif
             if (hit) {
                 if (STATS) cnt.hits++;
                 const Mat m = p.mats[code >> 2];
                 eval_material(m, h.normal, ray.d, L.s, sh);
                 attr_normal = h.normal;
                 ray.o = h.pos;                         // payload.hit_pos = position
-            } else {
+            }
+#if CPT_STAMPS == 4
+            const unsigned long long s1 = stamp();
+            st_refill += s1 - s0;                      // mode 4: hit shading / miss shading / rest
+#endif
+            if (!hit) {
                 if (STATS) cnt.misses++;
                 sh.radiance = miss_radiance(p, ray.d);
                 sh.attenuation = mk1(0.f);             // never read: the path ends here
@@ -165,6 +173,9 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
                 attr_normal = -ray.d;
                 depth = MAX_RECURSION_DEPTH_SET;       // termination sentinel (path_tracer.cu:121)
             }
+#if CPT_STAMPS == 4
+            st_trace += stamp() - s1;
+#endif
             rad = rad + att * sh.radiance;
             att = att * sh.attenuation;
             if (AUX && first) {
@@ -191,6 +202,7 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
                 }
             }
         }
+        if (CPT_STAMPS == 4) st_shade += stamp() - t0;
         if (CPT_STAMPS == 1) {
             const unsigned long long t3 = stamp();
             st_refill += t1 - t0;

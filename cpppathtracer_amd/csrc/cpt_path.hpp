@@ -20,6 +20,10 @@ namespace cpt {
 // order.
 // ======================================================================================
 __device__ __forceinline__ int mirror_index(int i, int n) {
+    if (i >= -n && i < 2 * n) {   // the range every sky fetch lands in: no integer division
+        const int m = i < 0 ? -1 - i : i;
+        return m >= n ? 2 * n - 1 - m : m;
+    }
     int period = 2 * n;
     int m = i % period;
     if (m < 0) m += period;
@@ -44,9 +48,9 @@ __device__ __forceinline__ void texel(const TexView& t, int i, int j, float out[
     int x = address_index<ADDR>(i, t.w), y = address_index<ADDR>(j, t.h);
     if (x < 0 || y < 0 || x >= t.cols) { out[0] = out[1] = out[2] = 0.0f; return; }
     uint32_t v = t.texels[(size_t)y * t.cols + x];
-    out[0] = (float)(v & 0xffu) / 255.0f;
-    out[1] = (float)((v >> 8) & 0xffu) / 255.0f;
-    out[2] = (float)((v >> 16) & 0xffu) / 255.0f;
+    out[0] = dm::div255(v & 0xffu);          // (float)c / 255.0f, exactly
+    out[1] = dm::div255((v >> 8) & 0xffu);
+    out[2] = dm::div255((v >> 16) & 0xffu);
 }
 
 // tex2D<float4> at normalized (u, v), rgb (textures.cu:68-71).  Linear: taps at
@@ -1020,8 +1024,8 @@ __device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow&
 // Miss (path_tracer.cu:117-122)
 __device__ __forceinline__ v3 miss_radiance(const KParams& p, v3 dir) {
     v3 d = normalize(dir);
-    float v = (float)((double)dm::asinf_(d.z) / REF_PI + 0.5);
-    float u = (float)((double)(dm::atanf_(d.y / d.x) / 2) / REF_PI);
+    float v = (float)(dm::div_pi(dm::asinf_(d.z)) + 0.5);     // (double)asinf / REF_PI + 0.5
+    float u = (float)dm::div_pi(dm::atanf_(d.y / d.x) / 2);    // (double)(atanf / 2) / REF_PI
     return tex2d(p, u, v);
 }
 

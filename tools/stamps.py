@@ -1,5 +1,6 @@
 """Per-phase cycle shares from CPT_STAMPS diagnostic builds (never timed).
   CPT_STAMPS=1: megakernel refill / trace / shade;  CPT_STAMPS=2: BVH walk leaf / slab / whole iteration;
+  CPT_STAMPS=4: hit shading / miss shading / rest of the megakernel loop;
   CPT_STAMPS=3: wave-level counts (walk iterations, iterations with a lane at a leaf / at an inner
   node, segment rounds) for the lane-efficiency breakdown.
 Build a diagnostic library with build.build(out=..., defines={"CPT_STAMPS": m}) and point
@@ -28,6 +29,10 @@ if mode == 1:
     tot = sum(c[5:8])
     print("refill %.1f%%  trace %.1f%%  shade+rest %.1f%%  (wave-cycles %d)" % (100 * c[5] / tot, 100 * c[6] / tot,
                                                                               100 * c[7] / tot, tot))
+elif mode == 4:
+    tot = c[7]
+    print("hit shading %.1f%%  miss shading %.1f%%  rest %.1f%%  (wave-cycles %d)" % (
+        100 * c[5] / tot, 100 * c[6] / tot, 100 * (tot - c[5] - c[6]) / tot, tot))
 elif mode == 3:
     seg, nodes, hits = c[0], c[1], c[3]
     w_seg = c[4] - (seg - hits)          # stats[4] = misses + segment rounds
