@@ -49,6 +49,14 @@ __device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int&
     return x < p.width && ri < p.n_rows;
 }
 
+#if CPT_LDS && defined(CPT_DEFER_MISS) && CPT_DEFER_MISS
+#error "CPT_DEFER_MISS assumes 256-lane blocks (the LDS-staged variant runs 256 * CPT_WAVES_PER_SIMD)"
+#endif
+#ifndef CPT_DEFER_MISS
+#define CPT_DEFER_MISS 32   // deferred sky fetches run when this many 64ths of the tracing lanes
+                            // hold one (0 = fetch at the miss)
+#endif
+
 template <bool STATS, bool AUX, bool LDS>
 __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVES_PER_SIMD) k_megakernel(const KParams p) {
     extern __shared__ Node lds_nodes[];
@@ -76,6 +84,12 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
     float dep_acc = 0.f, first_depth = 0.f;
 
     unsigned long long st_refill = 0, st_trace = 0, st_shade = 0;
+#if CPT_DEFER_MISS
+    // a lane's pending sky fetch: direction, the pass's radiance and attenuation so far
+    __shared__ float pending_q[9 * 256];
+    float* const pq = pending_q + threadIdx.x;
+    bool pend = false;
+#endif
     for (;;) {
         const unsigned long long t0 = stamp();
         // ---- refill idle lanes with new pixels (wave-aggregated dequeue) ----------------
@@ -165,14 +179,48 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             const unsigned long long s1 = stamp();
             st_refill += s1 - s0;                      // mode 4: hit shading / miss shading / rest
 #endif
+            bool deferred = false;
             if (!hit) {
                 if (STATS) cnt.misses++;
-                sh.radiance = miss_radiance(p, ray.d);
                 sh.attenuation = mk1(0.f);             // never read: the path ends here
                 sh.bounce = ray.d;
                 attr_normal = -ray.d;
-                depth = MAX_RECURSION_DEPTH_SET;       // termination sentinel (path_tracer.cu:121)
             }
+#if CPT_DEFER_MISS
+            // Deferred sky fetches.  A miss ends the pass, and the sky's radiance only feeds
+            // the pixel's running sum, so the lane may start its next pass first and add
+            // rad + att * sky later, as long as the sums are added in pass order.  Pending
+            // fetches run together once enough lanes hold one, instead of in every round
+            // where any lane misses; a lane that would end another pass (or its pixel) with
+            // one pending forces the round.  No RNG draw depends on the sky.
+            {
+                const bool ends = !hit || !(depth + 1 < max_depth);
+                const bool need_now = (pend && ends) || (!hit && L.left == 1);
+                const bool flush = __ballot(need_now) != 0 ||
+                                   __popcll(__ballot(pend || !hit)) * 64 >= CPT_DEFER_MISS * __popcll(__ballot(1));
+                if (flush) {
+                    if (pend) {   // older pending fetches first (their pass came first)
+                        const v3 pd = mk(pq[0 * 256], pq[1 * 256], pq[2 * 256]);
+                        const v3 sky = miss_radiance(p, pd);
+                        const v3 pr = mk(pq[3 * 256], pq[4 * 256], pq[5 * 256]);
+                        const v3 pa = mk(pq[6 * 256], pq[7 * 256], pq[8 * 256]);
+                        L.sum = L.sum + (pr + pa * sky);
+                        pend = false;
+                    }
+                    if (!hit) sh.radiance = miss_radiance(p, ray.d);
+                } else if (!hit) {
+                    pq[0 * 256] = ray.d.x; pq[1 * 256] = ray.d.y; pq[2 * 256] = ray.d.z;
+                    pq[3 * 256] = rad.x; pq[4 * 256] = rad.y; pq[5 * 256] = rad.z;
+                    pq[6 * 256] = att.x; pq[7 * 256] = att.y; pq[8 * 256] = att.z;
+                    pend = true;
+                    deferred = true;
+                    sh.radiance = mk1(0.f);            // placeholder: this pass's sum waits
+                }
+            }
+#else
+            if (!hit) sh.radiance = miss_radiance(p, ray.d);
+#endif
+            if (!hit) depth = MAX_RECURSION_DEPTH_SET;   // termination sentinel (path_tracer.cu:121)
 #if CPT_STAMPS == 4
             st_trace += stamp() - s1;
 #endif
@@ -188,7 +236,7 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             ray.tmax = DEFAULT_RAY_TMAX;
             depth++;
             if (!(depth < max_depth)) {
-                L.sum = L.sum + rad;
+                if (!deferred) L.sum = L.sum + rad;
                 L.passes += 1.0f;
                 if (AUX) { first_normal = nrm_acc; first_depth = dep_acc; }
                 if (--L.left > 0) {
@@ -548,6 +596,7 @@ hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t
     if (p.width <= 0 || p.n_rows <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(p.work, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
+#if CPT_LDS
     const bool lds = !p.ordered && p.n_nodes > 0 && p.n_nodes <= lds_node_capacity();
     if (lds) {
         if (stats && aux) return launch_mk<true, true, true>(p, stream);
@@ -555,6 +604,7 @@ hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t
         if (aux) return launch_mk<false, true, true>(p, stream);
         return launch_mk<false, false, true>(p, stream);
     }
+#endif
     if (stats && aux) return launch_mk<true, true, false>(p, stream);
     if (stats) return launch_mk<true, false, false>(p, stream);
     if (aux) return launch_mk<false, true, false>(p, stream);
