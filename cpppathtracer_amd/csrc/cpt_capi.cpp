@@ -343,8 +343,9 @@ struct cpt_ctx {
     uint32_t* d_work = nullptr;
     cpt::WfState wf{};           // wavefront path state (allocated on first use)
     bool wf_ready = false;
-    float* d_mix = nullptr;      // display running mean (Mix), rgb per pixel
-    uint8_t* d_bgra = nullptr;   // display frame
+    float* d_mix = nullptr;      // display running mean (Mix), rgb per pixel of the display band
+    uint8_t* d_bgra = nullptr;   // display frame (band rows)
+    int band_y0 = -1, band_y1 = -1;   // display band the buffers hold
     float last_kernel_ms = 0.f;
     int last_launches = 0;
 
@@ -399,6 +400,7 @@ void free_frame(cpt_ctx* c) {
     (void)hipFree(c->wf.counts); c->wf.counts = nullptr;
     c->wf_ready = false;
     (void)hipFree(c->d_bgra); c->d_bgra = nullptr;
+    c->band_y0 = c->band_y1 = -1;
     (void)hipFree(c->d_scratch_w); c->d_scratch_w = nullptr;
     (void)hipFree(c->d_scratch_m); c->d_scratch_m = nullptr;
     c->frame_set = c->rng_set = false;
@@ -1223,38 +1225,85 @@ int cpt_last_kernel_stats(cpt_ctx* c, float* avg_ms, int* launches) {
     return CPT_OK;
 }
 
+// Display path on output rows [y0, y1) of the 16-aligned launch (path_tracer.cu:177-254).
+// The context's frame rows must be one ascending run that covers the band and its 3-row halo
+// (clipped to [0, H')): every neighbour the linear-offset stencil reaches.  The running mean
+// and the BGRA8 rows belong to the band; a different band starts a fresh mean.
+static int denoise_band(cpt_ctx* c, uint32_t cur_sample_idx, int y0, int y1, uint8_t* bgra_host, size_t out_rows) {
+    if (!c->frame_set) return fail(c, CPT_ERR_STATE, "cpt_denoise_mix: cpt_set_frame first");
+    if (!c->d_normal || !c->d_depth) return fail(c, CPT_ERR_STATE, "cpt_denoise_mix: render with CPT_RENDER_AUX first");
+    if (cur_sample_idx == 0) return fail(c, CPT_ERR_INVALID_ARG, "cpt_denoise_mix: cur_sample_idx must be >= 1");
+    const int h_eff = 16 * (c->height / 16);
+    if (y0 < 0 || y1 > h_eff || y0 >= y1)
+        return fail(c, CPT_ERR_INVALID_ARG, "cpt_denoise_mix_band: band [%d, %d) outside [0, %d)", y0, y1, h_eff);
+    const int row0 = c->rows_h.empty() ? 0 : c->rows_h[0];
+    for (int i = 0; i < c->n_rows; ++i)
+        if (c->rows_h[i] != row0 + i)
+            return fail(c, CPT_ERR_STATE, "cpt_denoise_mix: the frame rows must be one ascending run");
+    const int need0 = std::max(0, y0 - 3), need1 = std::min(h_eff, y1 + 3);
+    if (row0 > need0 || row0 + c->n_rows < need1)
+        return fail(c, CPT_ERR_STATE, "cpt_denoise_mix_band: rows [%d, %d) rendered, band [%d, %d) needs [%d, %d)", row0,
+                    row0 + c->n_rows, y0, y1, need0, need1);
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream();
+    const size_t cap_rows = std::max<size_t>(out_rows, (size_t)(y1 - y0));
+    if (c->band_y0 != y0 || c->band_y1 != y1) {
+        (void)hipFree(c->d_mix); c->d_mix = nullptr;
+        (void)hipFree(c->d_bgra); c->d_bgra = nullptr;
+        const size_t n = cap_rows * c->width;
+        HIP_TRY(c, hipMalloc((void**)&c->d_mix, n * 3 * sizeof(float)));
+        HIP_TRY(c, hipMemsetAsync(c->d_mix, 0, n * 3 * sizeof(float), s));
+        HIP_TRY(c, hipMalloc((void**)&c->d_bgra, n * 4));
+        HIP_TRY(c, hipMemsetAsync(c->d_bgra, 0, n * 4, s));
+        c->band_y0 = y0;
+        c->band_y1 = y1;
+    }
+    HIP_TRY(c, cpt::launch_denoise_mix(c->d_accum, c->d_normal, c->d_depth, c->d_mix, c->d_bgra, c->width, c->height,
+                                      row0, y0, y1, cur_sample_idx, s));
+    if (bgra_host) {
+        HIP_TRY(c, hipMemcpyAsync(bgra_host, c->d_bgra, cap_rows * c->width * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipStreamSynchronize(s));
+    }
+    return CPT_OK;
+}
+
 int cpt_denoise_mix(cpt_ctx* c, uint32_t cur_sample_idx, uint8_t* bgra_host) {
     if (!c) return CPT_ERR_INVALID_ARG;
     if (!c->frame_set || c->n_rows != c->height) return fail(c, CPT_ERR_STATE, "cpt_denoise_mix: needs a full frame");
     for (int y = 0; y < c->height; ++y)
         if (c->rows_h[y] != y) return fail(c, CPT_ERR_STATE, "cpt_denoise_mix: needs rows 0..height-1 in order");
-    if (!c->d_normal || !c->d_depth) return fail(c, CPT_ERR_STATE, "cpt_denoise_mix: render with CPT_RENDER_AUX first");
-    if (cur_sample_idx == 0) return fail(c, CPT_ERR_INVALID_ARG, "cpt_denoise_mix: cur_sample_idx must be >= 1");
+    const int h_eff = 16 * (c->height / 16);
+    if (16 * (c->width / 16) == 0 || h_eff == 0) {   // nothing is launched; the frame stays 0
+        if (bgra_host) std::memset(bgra_host, 0, (size_t)c->width * c->height * 4);
+        return CPT_OK;
+    }
+    // the whole frame's rows (those past H' are never written and stay 0)
+    return denoise_band(c, cur_sample_idx, 0, h_eff, bgra_host, (size_t)c->height);
+}
+
+int cpt_denoise_mix_band(cpt_ctx* c, uint32_t cur_sample_idx, int y0, int y1, uint8_t* bgra_host) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    return denoise_band(c, cur_sample_idx, y0, y1, bgra_host, 0);
+}
+
+int cpt_copy_bgra_device(cpt_ctx* c, void* device_dst, size_t bytes) {
+    if (!c || !device_dst) return CPT_ERR_INVALID_ARG;
+    if (!c->d_bgra) return fail(c, CPT_ERR_STATE, "cpt_copy_bgra_device: no display frame yet");
+    const size_t have = (size_t)(c->band_y1 - c->band_y0) * c->width * 4;
+    if (bytes > have) return fail(c, CPT_ERR_INVALID_ARG, "cpt_copy_bgra_device: %zu bytes requested, band holds %zu", bytes, have);
     HIP_TRY(c, hipSetDevice(c->device));
-    const size_t npix = (size_t)c->width * c->height;
-    hipStream_t s = c->stream();
-    if (!c->d_mix) {
-        HIP_TRY(c, hipMalloc((void**)&c->d_mix, npix * 3 * sizeof(float)));
-        HIP_TRY(c, hipMemsetAsync(c->d_mix, 0, npix * 3 * sizeof(float), s));
-    }
-    if (!c->d_bgra) {
-        HIP_TRY(c, hipMalloc((void**)&c->d_bgra, npix * 4));
-        HIP_TRY(c, hipMemsetAsync(c->d_bgra, 0, npix * 4, s));
-    }
-    HIP_TRY(c, cpt::launch_denoise_mix(c->d_accum, c->d_normal, c->d_depth, c->d_mix, c->d_bgra, c->width, c->height,
-                                      cur_sample_idx, s));
-    if (bgra_host) {
-        HIP_TRY(c, hipMemcpyAsync(bgra_host, c->d_bgra, npix * 4, hipMemcpyDeviceToHost, s));
-        HIP_TRY(c, hipStreamSynchronize(s));
-    }
+    HIP_TRY(c, hipMemcpyAsync(device_dst, c->d_bgra, bytes, hipMemcpyDeviceToDevice, c->stream()));
     return CPT_OK;
 }
 
 int cpt_reset_display(cpt_ctx* c) {
     if (!c) return CPT_ERR_INVALID_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
-    const size_t npix = (size_t)c->width * c->height;
-    if (c->d_mix) HIP_TRY(c, hipMemsetAsync(c->d_mix, 0, npix * 3 * sizeof(float), c->stream()));
+    if (c->d_mix) {
+        const int h_eff = 16 * (c->height / 16);
+        const size_t rows = c->band_y0 == 0 && c->band_y1 == h_eff ? (size_t)c->height : (size_t)(c->band_y1 - c->band_y0);
+        HIP_TRY(c, hipMemsetAsync(c->d_mix, 0, rows * c->width * 3 * sizeof(float), c->stream()));
+    }
     return CPT_OK;
 }
 

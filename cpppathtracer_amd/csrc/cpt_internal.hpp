@@ -71,6 +71,7 @@ hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned l
                                 hipStream_t stream);
 int lds_node_capacity();
 hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
-                              int width, int height, uint32_t cur_sample_idx, hipStream_t stream);
+                              int width, int height, int row0, int y0, int y1, uint32_t cur_sample_idx,
+                              hipStream_t stream);
 
 }  // namespace cpt

@@ -461,12 +461,17 @@ __device__ __forceinline__ float dn_weight(float dist2) {
     return (float)(w < 1.0 ? w : 1.0);
 }
 
+// One band of output rows [y0, y1) of the W' x H' launch (W' = 16 floor(W/16), H' likewise).
+// accum/normal/depth hold the context's rows row0, row0 + 1, ... (row stride `width`): the
+// band plus a 3-row halo, enough for every neighbour the linear-offset stencil reaches (x +- 2
+// wraps into the adjacent row, so rows y - 3 .. y + 3).  mix and out hold the band's rows
+// only.  The full frame is the band [0, H') with row0 = 0.
 __global__ void k_denoise_mix(const float4* __restrict__ accum, const float* __restrict__ normal,
                               const float* __restrict__ depth, float* __restrict__ mix, uint8_t* __restrict__ out,
-                              int width, int height, int w_eff, int h_eff, float inv_idx) {
+                              int width, int row0, int y0, int y1, int w_eff, int h_eff, float inv_idx) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y * blockDim.y + threadIdx.y;
-    if (x >= w_eff || y >= h_eff) return;
+    const int y = y0 + blockIdx.y * blockDim.y + threadIdx.y;
+    if (x >= w_eff || y >= y1) return;
     const float kernel5[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
                                  {4.f, 16.f, 26.f, 16.f, 4.f},
                                  {7.f, 26.f, 41.f, 26.f, 7.f},
@@ -476,7 +481,8 @@ __global__ void k_denoise_mix(const float4* __restrict__ accum, const float* __r
         const float4 a = accum[px];
         return a.w != 0.f ? mk(a.x, a.y, a.z) / a.w : mk(a.x, a.y, a.z);
     };
-    const int self = y * width + x;
+    const int self = (y - row0) * width + x;        // this pixel in the rendered rows
+    const int bself = (y - y0) * width + x;         // ... and in the band's mix / out
     const v3 cval = radiance(self);
     const v3 nval = mk(normal[3 * self], normal[3 * self + 1], normal[3 * self + 2]);
     const float pval = depth[self];
@@ -493,7 +499,7 @@ __global__ void k_denoise_mix(const float4* __restrict__ accum, const float* __r
                 weight = 0.f * 0.f * 0.f;
                 ctmp = mk1(0.f);
             } else {
-                const int px = (cur_off / w_eff) * width + (cur_off % w_eff);
+                const int px = (cur_off / w_eff - row0) * width + (cur_off % w_eff);
                 ctmp = radiance(px);
                 v3 t = cval - ctmp;
                 const float c_w = dn_weight(dot(t, t));
@@ -512,24 +518,25 @@ __global__ void k_denoise_mix(const float4* __restrict__ accum, const float* __r
     const v3 dn = sum / cum_w;
     const v3 cl = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),
                      __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));
-    v3 m = mk(mix[3 * self], mix[3 * self + 1], mix[3 * self + 2]);
+    v3 m = mk(mix[3 * bself], mix[3 * bself + 1], mix[3 * bself + 2]);
     m = m + inv_idx * (cl - m);      // lerp(a, b, t) = a + t*(b-a) (helper_math.h:1154-1157)
-    mix[3 * self] = m.x;
-    mix[3 * self + 1] = m.y;
-    mix[3 * self + 2] = m.z;
-    out[4 * (size_t)self + 0] = (uint8_t)(255.99f * m.z);
-    out[4 * (size_t)self + 1] = (uint8_t)(255.99f * m.y);
-    out[4 * (size_t)self + 2] = (uint8_t)(255.99f * m.x);
+    mix[3 * bself] = m.x;
+    mix[3 * bself + 1] = m.y;
+    mix[3 * bself + 2] = m.z;
+    out[4 * (size_t)bself + 0] = (uint8_t)(255.99f * m.z);
+    out[4 * (size_t)bself + 1] = (uint8_t)(255.99f * m.y);
+    out[4 * (size_t)bself + 2] = (uint8_t)(255.99f * m.x);
 }
 
 hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
-                              int width, int height, uint32_t cur_sample_idx, hipStream_t stream) {
+                              int width, int height, int row0, int y0, int y1, uint32_t cur_sample_idx,
+                              hipStream_t stream) {
     const int w_eff = 16 * (width / 16), h_eff = 16 * (height / 16);
-    if (w_eff == 0 || h_eff == 0) return hipSuccess;
+    if (w_eff == 0 || h_eff == 0 || y1 <= y0) return hipSuccess;
     const float inv_idx = 1.f / float(cur_sample_idx);
-    dim3 block(16, 16), grid(w_eff / 16, h_eff / 16);
-    hipLaunchKernelGGL(k_denoise_mix, grid, block, 0, stream, accum, normal, depth, mix, out, width, height, w_eff,
-                       h_eff, inv_idx);
+    dim3 block(16, 16), grid(w_eff / 16, (y1 - y0 + 15) / 16);
+    hipLaunchKernelGGL(k_denoise_mix, grid, block, 0, stream, accum, normal, depth, mix, out, width, row0, y0, y1,
+                       w_eff, h_eff, inv_idx);
     return hipGetLastError();
 }
 

@@ -212,6 +212,18 @@ class Renderer:
         self._check(self._L.cpt_denoise_mix(self._ctx, cur_sample_idx, _p(out)))
         return out
 
+    def denoise_mix_band(self, cur_sample_idx, y0, y1, host=True):
+        """Display path for output rows [y0, y1) (cpt_denoise_mix_band): the frame's rows must be
+        one ascending run covering the band and its 3-row halo.  Returns the band's BGRA8 rows
+        (y1 - y0, width, 4), or None with host=False (then copy_bgra_device moves them)."""
+        out = np.zeros((y1 - y0, self.width, 4), dtype=np.uint8) if host else None
+        self._check(self._L.cpt_denoise_mix_band(self._ctx, cur_sample_idx, int(y0), int(y1),
+                                                 _p(out) if host else None))
+        return out
+
+    def copy_bgra_device(self, device_ptr, nbytes):
+        self._check(self._L.cpt_copy_bgra_device(self._ctx, ctypes.c_void_p(device_ptr), nbytes))
+
     def reset_display(self):
         self._check(self._L.cpt_reset_display(self._ctx))
 

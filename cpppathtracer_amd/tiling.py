@@ -43,6 +43,45 @@ def stitch(gathered: np.ndarray, height: int, width: int, world: int, block: int
     return out.reshape(height * width, c)
 
 
+# ---- display path (Denoising + Mix, path_tracer.cu:177-254) across ranks ------------------
+# The denoiser reads a 5x5 neighbourhood by LINEAR offset over the W' x H' launch
+# (W' = 16 floor(W/16), H' likewise), so x +- 2 wraps into the adjacent row: a pixel of row y
+# reads rows y - 3 .. y + 3.  Each rank owns a contiguous band of output rows and renders the
+# band plus a 3-row halo (the halo rows' streams depend only on (seed, x, y), so both ranks
+# that render a halo row compute it identically); no per-pass exchange is needed, and one
+# all-gather of the BGRA8 bands assembles the frame.
+HALO_ROWS = 3
+
+
+def display_band(height: int, world: int, rank: int) -> tuple:
+    """Output rows [y0, y1) of the display launch owned by `rank` (contiguous, near-equal)."""
+    he = 16 * (height // 16)
+    return rank * he // world, (rank + 1) * he // world
+
+
+def display_rows(height: int, world: int, rank: int) -> np.ndarray:
+    """The rows a display rank renders: its band and the halo, clipped to [0, H')."""
+    he = 16 * (height // 16)
+    y0, y1 = display_band(height, world, rank)
+    if y1 <= y0:
+        return np.zeros(0, dtype=np.int32)
+    return np.arange(max(0, y0 - HALO_ROWS), min(he, y1 + HALO_ROWS), dtype=np.int32)
+
+
+def max_band_rows(height: int, world: int) -> int:
+    return max(b - a for a, b in (display_band(height, world, r) for r in range(world)))
+
+
+def stitch_bands(gathered: np.ndarray, height: int, width: int, world: int) -> np.ndarray:
+    """gathered: [world, max_band_rows, width, 4] BGRA8 bands -> the (height, width, 4) frame
+    (rows past H' stay 0, as in the single-GPU display path)."""
+    out = np.zeros((height, width, 4), dtype=gathered.dtype)
+    for r in range(world):
+        y0, y1 = display_band(height, world, r)
+        out[y0:y1] = gathered[r, : y1 - y0]
+    return out
+
+
 def stitch_index(height: int, width: int, world: int, block: int = BLOCK_ROWS) -> np.ndarray:
     """Row gather index for an on-device stitch: framebuffer row y = gathered row idx[y]."""
     mr = max_rows(height, world, block)

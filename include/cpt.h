@@ -31,6 +31,9 @@
  *                                   written by SamplePixel (path_tracer.cu:172-174).
  *   cpt_denoise_mix                 Denoising + Mix + BGRA8 readback (path_tracer.cu:177-254,
  *                                   285-303).
+ *   cpt_denoise_mix_band            The same for one row band of a multi-GPU display (the
+ *                                   Denoising/Mix launch restricted to rows y0..y1-1; the
+ *                                   band's renderer also renders a 3-row halo).
  */
 #ifndef CPT_H_
 #define CPT_H_
@@ -233,6 +236,15 @@ int cpt_last_kernel_stats(cpt_ctx* ctx, float* avg_ms, int* launches);
  * radiance (accumulator / pass count), running-mean Mix with weight 1/cur_sample_idx,
  * BGRA8 out (alpha byte untouched).  Needs a full frame (rows == NULL). */
 int cpt_denoise_mix(cpt_ctx* ctx, uint32_t cur_sample_idx, uint8_t* bgra_host);
+/* Display path for output rows [y0, y1) of the 16-aligned launch (0 <= y0 < y1 <= 16*(H/16)),
+ * for row-banded multi-GPU display: the context's frame rows (cpt_set_frame) must be one
+ * ascending run covering [max(0, y0-3), min(16*(H/16), y1+3)) -- the band and the rows its
+ * linear-offset stencil reaches (x +- 2 wraps into the next row).  The Mix running mean and the
+ * BGRA8 output hold the band's rows only ((y1-y0) x W x 4 bytes to bgra_host, may be NULL); a
+ * new band starts a fresh (zeroed) mean.  Byte-identical to rows y0..y1-1 of cpt_denoise_mix. */
+int cpt_denoise_mix_band(cpt_ctx* ctx, uint32_t cur_sample_idx, int y0, int y1, uint8_t* bgra_host);
+/* Device-to-device copy of the current display band's BGRA8 rows (for an RCCL gather). */
+int cpt_copy_bgra_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
 /* Zero the Mix running mean (the reference's buffer starts uninitialised; here it is zeroed
  * when the frame is created and by this call). */
 int cpt_reset_display(cpt_ctx* ctx);

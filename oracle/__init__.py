@@ -65,6 +65,8 @@ def lib():
         L.or_build_bvh.restype = i32
         L.or_denoise_mix.argtypes = [P, P, P, P, P, i32, i32, ctypes.c_uint32]
         L.or_denoise_mix.restype = None
+        L.or_denoise_mix_band.argtypes = [P, P, P, P, P, i32, i32, i32, i32, i32, ctypes.c_uint32]
+        L.or_denoise_mix_band.restype = None
         L.or_render.argtypes = [P, i32, P, P, i32, i32, i32, P, i32, i32, i32, P, P, P, P, P, i32, i32]
         L.or_render.restype = i32
         L.or_render_edited.argtypes = [P, i32, P, P, i32, P, P, i32, i32, i32, P, i32, i32, i32, P, P, P, i32]
@@ -210,3 +212,17 @@ def denoise_mix(accum, normal, depth, mix, out, width, height, cur_sample_idx):
     for a, dt in ((accum, np.float32), (normal, np.float32), (depth, np.float32), (mix, np.float32), (out, np.uint8)):
         assert a.dtype == dt and a.flags.c_contiguous
     lib().or_denoise_mix(_ptr(accum), _ptr(normal), _ptr(depth), _ptr(mix), _ptr(out), width, height, cur_sample_idx)
+
+
+def denoise_mix_band(accum, normal, depth, mix, out, width, height, row0, y0, y1, cur_sample_idx):
+    """Denoising + Mix for output rows [y0, y1): accum [n,4] / normal [n,3] / depth [n] hold the
+    rendered rows row0, row0+1, ... (band + 3-row halo); mix [(y1-y0)*W,3] and out [y1-y0,W,4]
+    hold the band's rows (in/out)."""
+    for a, dt in ((accum, np.float32), (normal, np.float32), (depth, np.float32), (mix, np.float32), (out, np.uint8)):
+        assert a.dtype == dt and a.flags.c_contiguous
+    n_rows = accum.reshape(-1, 4).shape[0] // width
+    he = 16 * (height // 16)
+    assert 0 <= y0 < y1 <= he and row0 <= max(0, y0 - 3) and row0 + n_rows >= min(he, y1 + 3)
+    assert mix.size >= (y1 - y0) * width * 3 and out.size >= (y1 - y0) * width * 4
+    lib().or_denoise_mix_band(_ptr(accum), _ptr(normal), _ptr(depth), _ptr(mix), _ptr(out), width, height, row0, y0,
+                              y1, cur_sample_idx)

@@ -1495,8 +1495,19 @@ int or_render_edited(const void* objs, int n_objs, const int32_t* edit_idx, cons
 // pass count; neighbours by linear offset over the W' x H' = 16*floor(W/16) x 16*floor(H/16)
 // launch (rows wrap); weights in double; mix = lerp(mix, clamp(dn, 0, 1), 1/idx); bytes
 // 0..2 = 255.99*(b, g, r); alpha untouched.
+// The same for output rows [y0, y1) only: accum/normal/depth hold rows row0.. (stride W; they
+// must include every row the stencil reaches, y0 - 3 .. y1 + 2 within [0, H')), mix/out hold
+// the band's rows.  Row-banded multi-GPU display.
+void or_denoise_mix_band(const float* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
+                         int W, int H, int row0, int y0, int y1, uint32_t cur_sample_idx);
+
 void or_denoise_mix(const float* accum, const float* normal, const float* depth, float* mix, uint8_t* out, int W,
                     int H, uint32_t cur_sample_idx) {
+    or_denoise_mix_band(accum, normal, depth, mix, out, W, H, 0, 0, 16 * (H / 16), cur_sample_idx);
+}
+
+void or_denoise_mix_band(const float* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
+                         int W, int H, int row0, int y0, int y1, uint32_t cur_sample_idx) {
     const int we = 16 * (W / 16), he = 16 * (H / 16);
     const float kernel[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
                                 {4.f, 16.f, 26.f, 16.f, 4.f},
@@ -1513,9 +1524,10 @@ void or_denoise_mix(const float* accum, const float* normal, const float* depth,
         return (float)(w < 1.0 ? w : 1.0);
     };
     const float inv_idx = 1.f / float(cur_sample_idx);
-    for (int y = 0; y < he; ++y)
+    if (we == 0) return;
+    for (int y = y0; y < y1 && y < he; ++y)
         for (int x = 0; x < we; ++x) {
-            const int self = y * W + x;
+            const int self = (y - row0) * W + x, bself = (y - y0) * W + x;
             f3 cval = rad(self), nval = nrm(self);
             float pval = depth[self];
             f3 sum = mk1(0.f);
@@ -1530,7 +1542,7 @@ void or_denoise_mix(const float* accum, const float* normal, const float* depth,
                         weight = 0.f;
                         ctmp = mk1(0.f);
                     } else {
-                        int px = (cur_off / we) * W + (cur_off % we);
+                        int px = (cur_off / we - row0) * W + (cur_off % we);
                         ctmp = rad(px);
                         f3 t = sub(cval, ctmp);
                         float c_w = wgt(dot(t, t));
@@ -1546,13 +1558,13 @@ void or_denoise_mix(const float* accum, const float* normal, const float* depth,
                 }
             f3 dn = divs(sum, cum_w);
             f3 cl = mk(fmaxf(0.f, fminf(dn.x, 1.f)), fmaxf(0.f, fminf(dn.y, 1.f)), fmaxf(0.f, fminf(dn.z, 1.f)));
-            float* m = mix + 3 * (size_t)self;
+            float* m = mix + 3 * (size_t)bself;
             f3 mv = mk(m[0], m[1], m[2]);
             mv = add(mv, mul(inv_idx, sub(cl, mv)));
             m[0] = mv.x; m[1] = mv.y; m[2] = mv.z;
-            out[4 * (size_t)self + 0] = (uint8_t)(255.99f * mv.z);
-            out[4 * (size_t)self + 1] = (uint8_t)(255.99f * mv.y);
-            out[4 * (size_t)self + 2] = (uint8_t)(255.99f * mv.x);
+            out[4 * (size_t)bself + 0] = (uint8_t)(255.99f * mv.z);
+            out[4 * (size_t)bself + 1] = (uint8_t)(255.99f * mv.y);
+            out[4 * (size_t)bself + 2] = (uint8_t)(255.99f * mv.x);
         }
 }
 

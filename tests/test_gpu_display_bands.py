@@ -1,0 +1,66 @@
+"""Row-banded display path on the GPU (cpt_denoise_mix_band, cpppathtracer_amd.display).
+
+Each simulated rank is its own context on cuda:0 rendering its band plus the 3-row halo; the
+stitched BGRA8 frame must equal the single-GPU display path byte for byte (the committed
+golden, and cpt_denoise_mix on the same frame)."""
+import os
+
+import numpy as np
+import pytest
+
+from cpppathtracer_amd import camera_get_copy, scenes, tiling
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+pytestmark = pytest.mark.gpu
+
+
+def _banded(sky, objs, W, H, world, idxs, depth=8, ordered=False):
+    from cpppathtracer_amd import Renderer
+    from cpppathtracer_amd.display import BandedDisplay
+    cam = camera_get_copy(scenes.camera_for(W, H))
+    g = np.zeros((world, tiling.max_band_rows(H, world), W, 4), np.uint8)
+    for rank in range(world):
+        with Renderer(0) as r:
+            r.set_scene(objs)
+            r.set_env(sky)
+            d = BandedDisplay(r, W, H, 1234, rank, world)
+            for idx in idxs:
+                band = d.dispatch(cam, idx, depth, ordered=ordered)
+            g[rank, : band.shape[0]] = band
+    return tiling.stitch_bands(g, H, W, world)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_gpu_banded_display_equals_golden(gpu, sky, world):
+    z = np.load(os.path.join(GOLDEN, "display_s4_64x48_3frames.npz"))
+    np.testing.assert_array_equal(_banded(sky, scenes.scene_s4(), 64, 48, world, (2, 3, 4)), z["bgra"])
+
+
+@pytest.mark.parametrize("ordered", [False, True])
+def test_gpu_banded_display_equals_full_frame(gpu, sky, ordered):
+    """BVH scene, a height that is not a multiple of 16, both walks."""
+    W, H = 80, 53
+    objs = scenes.scene_s1000()
+    cam = camera_get_copy(scenes.camera_for(W, H))
+    gpu.set_scene(objs)
+    gpu.set_env(sky)
+    gpu.set_frame(W, H)
+    gpu.init_rng(1234)
+    for idx in (2, 3):
+        gpu.render(cam, 1, 8, aux=True, sync=True, ordered=ordered)
+        full = gpu.denoise_mix(idx)
+    np.testing.assert_array_equal(_banded(sky, objs, W, H, 3, (2, 3), ordered=ordered), full)
+
+
+def test_gpu_band_needs_halo_rows(gpu, sky):
+    from cpppathtracer_amd.renderer import CptError
+    W, H = 64, 48
+    gpu.set_scene(scenes.scene_s4())
+    gpu.set_env(sky)
+    gpu.set_frame(W, H, np.arange(16, 32, dtype=np.int32))   # the band alone, no halo
+    gpu.init_rng(1234)
+    gpu.render(camera_get_copy(scenes.camera_for(W, H)), 1, 8, aux=True, sync=True)
+    with pytest.raises(CptError):
+        gpu.denoise_mix_band(2, 16, 32)
+    with pytest.raises(CptError):
+        gpu.denoise_mix_band(2, 40, 64)   # past H'
