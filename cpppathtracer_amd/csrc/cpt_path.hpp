@@ -536,10 +536,10 @@ __device__ __forceinline__ bool sphere_cyl_test(const Node& nd, const RayK& ray,
     return ret;
 }
 
-template <bool FAST, bool CONS>
+template <bool FAST, bool CONS, bool PRETEST = true>
 __device__ __forceinline__ bool ranked_leaf_test(const Node& nd, const RayK& ray, float& tmax, int& kind, int& best_rank) {
     float tm = nd.miss < best_rank ? __int_as_float(__float_as_int(tmax) + 1) : tmax;
-    if (CONS && CPT_LEAF_PRETEST) {
+    if (CONS && PRETEST && CPT_LEAF_PRETEST) {
         const int type = nd.code & 3;
         if (type == 2 || (CPT_LEAF_PRETEST == 2 && type == 0)) {
             Node box;
@@ -734,6 +734,9 @@ __device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const R
 #ifndef CPT_WIDE_CULL
 #define CPT_WIDE_CULL 0    // keep each stack entry's entry distance; pops beyond the limit are dropped
 #endif
+#ifndef CPT_WIDE_SLOTS
+#define CPT_WIDE_SLOTS 1   // leaves a lane may park before it stops (1 or 2)
+#endif
 #ifndef CPT_WIDE_PARK2
 #define CPT_WIDE_PARK2 1   // park the nearest hit leaf in the node's own iteration (+2% A/B)
 #endif
@@ -807,7 +810,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         cur = ~p.n_nodes;
     }
     const uint32_t wbase = (uint32_t)(p.n_nodes + 8 * p.n_walk + 4 * oct * p.n_wide) * (uint32_t)sizeof(Node);
-    int parked = -1;
+    int parked = -1, parked2 = -1;   // parked leaves (the second slot with CPT_WIDE_SLOTS == 2)
     // next stack entry (NONE when empty); with CPT_WIDE_CULL entries whose box starts beyond the
     // current limit are dropped (the limit only shrinks, so they can no longer hold a winner)
     auto pop = [&]() -> int {
@@ -824,6 +827,9 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
 #endif
         if (cur <= -2 && parked < 0) {
             parked = ~cur;
+            cur = pop();
+        } else if (CPT_WIDE_SLOTS == 2 && cur <= -2 && parked2 < 0) {
+            parked2 = ~cur;
             cur = pop();
         }
         if (cur >= 0) {
@@ -853,10 +859,13 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
             if (CPT_WIDE_PARK2 && cur <= -2 && parked < 0) {   // park the nearest leaf at once
                 parked = ~cur;
                 cur = pop();
+            } else if (CPT_WIDE_PARK2 && CPT_WIDE_SLOTS == 2 && cur <= -2 && parked2 < 0) {
+                parked2 = ~cur;
+                cur = pop();
             }
         }
         const bool working = parked >= 0 || cur != NONE;
-        const bool stopped = parked >= 0 && cur <= -1;
+        const bool stopped = parked >= 0 && (cur == NONE || (cur <= -2 && (CPT_WIDE_SLOTS == 1 || parked2 >= 0)));
         const uint64_t w = __ballot(working);
         if (!w) break;
         const bool round = __popcll(__ballot(stopped)) * 64 >= CPT_SPEC_LEAF * __popcll(w);
@@ -870,17 +879,24 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         }
 #endif
         if (round) {
-            if (parked >= 0) {
-                if (STATS) cnt.prims++;
-                const Node lf = nodes(parked);
-                int k;
-                if (ranked_leaf_test<true, true>(lf, ray, tmax, k, best_rank)) {
-                    best = parked;
-                    kind = k;
-                    limit = walk_limit(tmax);
+#pragma nounroll
+            for (int slot = 0; slot < CPT_WIDE_SLOTS; ++slot) {
+                const int leaf = slot == 0 ? parked : parked2;
+                if (leaf >= 0) {
+                    if (STATS) cnt.prims++;
+                    const Node lf = nodes(leaf);
+                    int k;
+                    // no pretest: the parent's slab test already tested this leaf's own box
+                    // (measured: +2% without the repeat at the smaller limit)
+                    if (ranked_leaf_test<true, true, false>(lf, ray, tmax, k, best_rank)) {
+                        best = leaf;
+                        kind = k;
+                        limit = walk_limit(tmax);
+                    }
                 }
-                parked = -1;
             }
+            parked = -1;
+            parked2 = -1;
         }
 #if CPT_STAMPS == 2
         const unsigned long long t2 = stamp();
