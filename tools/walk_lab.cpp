@@ -28,7 +28,7 @@ struct ANode {
 };
 
 struct WNode {               // mode 7: 4-wide node, children per octant in near-first order
-    int child[8][4];
+    int child[8][8];
     int n = 0;
 };
 
@@ -198,7 +198,7 @@ void prepare(const Bvh& bvh) {
         // collapse: replace the largest-area internal child by its two children until 4
         std::function<int(int)> collapse = [&](int b) -> int {
             std::vector<int> ch = {t.nodes[b].left, t.nodes[b].right};
-            while (ch.size() < 4) {
+            while ((int)ch.size() < (std::getenv("LAB_WIDTH") ? std::atoi(std::getenv("LAB_WIDTH")) : 4)) {
                 int best = -1; float ba = -1.f;
                 for (size_t k = 0; k < ch.size(); ++k) {
                     const ANode& c = t.nodes[ch[k]];
@@ -322,7 +322,7 @@ bool alt_trace(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, uint64_t& node
             nodes++;                       // iterations (pops)
             if (x < 0) { test(t.nodes[-1 - x].obj); continue; }
             const WNode& w = t.wide[x];
-            int hit[4], nh = 0;
+            int hit[8], nh = 0;
             for (int k = 0; k < w.n; ++k) {
                 const int c = w.child[oct][k];
                 g_boxes++;
