@@ -346,3 +346,32 @@ def test_ordered_walk_platform_only_and_multiple_platforms(gpu, oracle_mod, sky,
     np.testing.assert_array_equal(gr, orng)
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
     _check_stats(gs, os_, path)
+
+
+def _chain_scene(n=90):
+    """Spheres on a geometric progression along x: the SAH peels one sphere off per split, so
+    the walk tree is a chain whose 4-wide form needs more than the device's 32 stack entries."""
+    objs = np.zeros(n + 1, dtype=types.OBJECT_DTYPE)
+    objs[0] = scenes.scene_s4()[0]                     # the floor
+    mat = scenes.scene_s4()[1]["material"]
+    for k in range(n):
+        objs[k + 1] = types.make_object(types.SPHERE, mat, center=(-40.0 + 1.12 ** k, 10.0, 0.0),
+                                         radius=0.05 * 1.12 ** k)
+    return objs
+
+
+def test_wide_walk_structure_and_deep_tree_fallback(gpu, oracle_mod, sky):
+    """The default ordered walk runs on 4-wide nodes for S1000; a walk tree too deep for the
+    per-lane LDS stack keeps the binary octant orders (cpt_get_walk_info n_wide == 0), with the
+    same bit-exact images."""
+    gpu.set_scene(scenes.scene_s1000())
+    info = gpu.walk_info()
+    assert info["n_wide"] > 0 and info["n_unb"] == 1 and info["n_walk"] == 2000
+    objs = _chain_scene()
+    gpu.set_scene(objs)
+    assert gpu.walk_info()["n_wide"] == 0
+    for path in ("megakernel:ordered", "megakernel"):
+        (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, objs, 48, 32, 2, 8, path=path)
+        np.testing.assert_array_equal(gr, orng)
+        np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
+        _check_stats(gs, os_, path)
