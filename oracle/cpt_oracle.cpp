@@ -282,33 +282,37 @@ float dm_cosf(float xf) {
 
 const double PI_2_D = 1.57079632679489655800e+00;  // pi/2 rounded to double
 
+// fdlibm s_atan.c constants (public domain): atan(0.5), atan(1), atan(1.5), atan(inf) as
+// hi + lo, and the minimax coefficients of atan(x) ~ x - x (aT0 z + aT1 z^2 + ...), z = x^2.
+constexpr double ATAN_HI0 = 4.63647609000806093515e-01, ATAN_LO0 = 2.26987774529616870924e-17;
+constexpr double ATAN_HI1 = 7.85398163397448278999e-01, ATAN_LO1 = 3.06161699786838301793e-17;
+constexpr double ATAN_HI2 = 9.82793723247329054082e-01, ATAN_LO2 = 1.39033110312309984516e-17;
+constexpr double ATAN_HI3 = 1.57079632679489655800e+00, ATAN_LO3 = 6.12323399573676603587e-17;
+constexpr double AT0 = 3.33333333333329318027e-01, AT1 = -1.99999999998764832476e-01;
+constexpr double AT2 = 1.42857142725034663711e-01, AT3 = -1.11111104054623557880e-01;
+constexpr double AT4 = 9.09088713343650656196e-02, AT5 = -7.69187620504482999495e-02;
+constexpr double AT6 = 6.66107313738753120669e-02, AT7 = -5.83357013379057348645e-02;
+constexpr double AT8 = 4.97687799461593236017e-02, AT9 = -3.65315727442169155270e-02;
+constexpr double AT10 = 1.62858201153657823623e-02;
+
 double dm_atan(double t) {
-    if (t != t) return t;
-    double sgn = 1.0;
-    double a = t;
-    if (a < 0.0) { a = -a; sgn = -1.0; }
+    // fdlibm's reduction to |x| < 7/16 around atan(0.5), atan(1), atan(1.5), atan(inf), with
+    // one division chosen by selects, and its odd/even split of an 11-term minimax polynomial
+    // (DESIGN.md §Numerics).  Identical operation sequence on the device (cpt_device.hpp dm::atan).
+    if (t != t || t == 0.0) return t;
+    const double sgn = t < 0.0 ? -1.0 : 1.0;
+    const double a = t < 0.0 ? -t : t;
     if (a == INFINITY) return sgn * PI_2_D;
-    bool inv = false;
-    if (a > 1.0) { a = 1.0 / a; inv = true; }
-    // two argument halvings: atan(a) = 2 atan(a / (1 + sqrt(1 + a^2)))
-    a = a / (1.0 + sqrt(1.0 + a * a));
-    a = a / (1.0 + sqrt(1.0 + a * a));       // a <= tan(pi/16) ~ 0.1989
-    double a2 = a * a;
-    double p = -1.0 / 27.0;
-    p = 1.0 / 25.0 + a2 * p;
-    p = -1.0 / 23.0 + a2 * p;
-    p = 1.0 / 21.0 + a2 * p;
-    p = -1.0 / 19.0 + a2 * p;
-    p = 1.0 / 17.0 + a2 * p;
-    p = -1.0 / 15.0 + a2 * p;
-    p = 1.0 / 13.0 + a2 * p;
-    p = -1.0 / 11.0 + a2 * p;
-    p = 1.0 / 9.0 + a2 * p;
-    p = -1.0 / 7.0 + a2 * p;
-    p = 1.0 / 5.0 + a2 * p;
-    p = -1.0 / 3.0 + a2 * p;
-    double r = 4.0 * (a + a * (a2 * p));
-    if (inv) r = PI_2_D - r;
+    const bool r0 = a < 0.4375, r1 = a < 0.6875, r2 = a < 1.1875, r3 = a < 2.4375;
+    const double num = r0 ? a : r1 ? 2.0 * a - 1.0 : r2 ? a - 1.0 : r3 ? a - 1.5 : -1.0;
+    const double den = r0 ? 1.0 : r1 ? 2.0 + a : r2 ? a + 1.0 : r3 ? 1.0 + 1.5 * a : a;
+    const double hi = r1 ? ATAN_HI0 : r2 ? ATAN_HI1 : r3 ? ATAN_HI2 : ATAN_HI3;
+    const double lo = r1 ? ATAN_LO0 : r2 ? ATAN_LO1 : r3 ? ATAN_LO2 : ATAN_LO3;
+    const double x = num / den;
+    const double z = x * x, w = z * z;
+    const double s1 = z * (AT0 + w * (AT2 + w * (AT4 + w * (AT6 + w * (AT8 + w * AT10)))));
+    const double s2 = w * (AT1 + w * (AT3 + w * (AT5 + w * (AT7 + w * AT9))));
+    const double r = r0 ? x - x * (s1 + s2) : hi - ((x * (s1 + s2) - lo) - x);
     return sgn * r;
 }
 

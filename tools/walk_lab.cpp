@@ -323,6 +323,7 @@ bool alt_trace(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, uint64_t& node
             if (x < 0) { test(t.nodes[-1 - x].obj); continue; }
             const WNode& w = t.wide[x];
             int hit[8], nh = 0;
+            float ent[8];
             for (int k = 0; k < w.n; ++k) {
                 const int c = w.child[oct][k];
                 g_boxes++;
@@ -330,8 +331,19 @@ bool alt_trace(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, uint64_t& node
                 ANode box;
                 if (c < 0) box = cn;
                 else { box.bmin = t.wbox[c].bmin; box.bmax = t.wbox[c].bmax; }
-                if (slab_ok(box, ray)) hit[nh++] = c;
+                if (slab_ok(box, ray)) {
+                    const float o3[3] = {ray.origin.x, ray.origin.y, ray.origin.z}, d3[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
+                    const float a3[3] = {box.bmin.x, box.bmin.y, box.bmin.z}, b3[3] = {box.bmax.x, box.bmax.y, box.bmax.z};
+                    float e = -1e30f;
+                    for (int q = 0; q < 3; ++q)
+                        if (d3[q] != 0.f) e = std::max(e, std::min((a3[q] - o3[q]) / d3[q], (b3[q] - o3[q]) / d3[q]));
+                    ent[nh] = e;
+                    hit[nh++] = c;
+                }
             }
+            if (std::getenv("LAB_SORT"))   // nearest entry distance first (dynamic order)
+                for (int i = 1; i < nh; ++i)
+                    for (int j = i; j > 0 && ent[j] < ent[j - 1]; --j) { std::swap(ent[j], ent[j - 1]); std::swap(hit[j], hit[j - 1]); }
             for (int k = nh - 1; k >= 0; --k) st[tp++] = hit[k];
         }
         return ret;
