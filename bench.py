@@ -84,6 +84,7 @@ def main():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: pixels per GPU fixed (image grows by sqrt(N) per axis); strong: fixed image")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-hbm-probe", action="store_true", help="skip the streaming-read ceiling probe")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM traffic measured by rocprofv3 PMC (profiles/*.json) for this config")
@@ -199,6 +200,8 @@ def main():
         return dict(zip(KEYS, (int(x) for x in v.tolist())))
 
     walk_info = r.walk_info()
+    # the box's measured HBM streaming-read ceiling (4 GiB, 10 passes), reported beside the spec peak
+    hbm_read_measured = r.measure_read_bandwidth(4 << 30, 10) if not args.no_hbm_probe else None
     walk_node_bytes = 128 if ordered and walk_info["n_wide"] > 0 else 32   # 4-wide walk nodes
     st = count_pass(False)
     walk_counts, walk_diff = None, None
@@ -293,6 +296,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "hbm_read_measured_gbs": round(hbm_read_measured, 1) if hbm_read_measured else None,
                 "achieved_reference_model": round(achieved_ref_model, 2),
                 "kernel": "k_megakernel" if args.path == "megakernel" else "wavefront (k_wf_extend+k_wf_shade per bounce)",
                 "kernel_avg_ms": round(avg_kernel_ms, 3),

@@ -45,6 +45,7 @@ PROTOTYPES = {
     "cpt_reset_stats": (_I, [_P]),
     "cpt_get_raw_counters": (_I, [_P, _P]),
     "cpt_get_walk_info": (_I, [_P, _P]),
+    "cpt_measure_read_bandwidth": (_I, [_P, _SZ, _I, _P]),
     "cpt_last_render_ms": (_I, [_P, _P]),
     "cpt_last_kernel_stats": (_I, [_P, _P, _P]),
     "cpt_denoise_mix": (_I, [_P, _U32, _P]),

@@ -1327,6 +1327,38 @@ int cpt_math_batch(cpt_ctx* c, int op, const float* a, const float* b, float* ou
     return CPT_OK;
 }
 
+int cpt_measure_read_bandwidth(cpt_ctx* c, size_t bytes, int iters, float* gbps) {
+    if (!c || !gbps || bytes < 16 || iters < 1) return CPT_ERR_INVALID_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t n = bytes / 16;
+    float4* d = nullptr;
+    float* o = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int dev = 0, cus = 0;
+    hipError_t e = hipMalloc((void**)&d, n * 16);
+    if (e == hipSuccess) e = hipMalloc((void**)&o, sizeof(float));
+    if (e == hipSuccess) e = hipMemsetAsync(d, 0, n * 16, c->stream());
+    if (e == hipSuccess) e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    const int grid = 8 * std::max(cus, 1);   // 8 blocks of 256 lanes per CU, grid-stride
+    if (e == hipSuccess) e = cpt::launch_stream_read(d, n, o, grid, c->stream());   // warm-up
+    if (e == hipSuccess) e = hipEventRecord(e0, c->stream());
+    for (int i = 0; e == hipSuccess && i < iters; ++i) e = cpt::launch_stream_read(d, n, o, grid, c->stream());
+    if (e == hipSuccess) e = hipEventRecord(e1, c->stream());
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(d);
+    (void)hipFree(o);
+    if (e != hipSuccess) return fail(c, CPT_ERR_HIP, "cpt_measure_read_bandwidth: %s", hipGetErrorString(e));
+    *gbps = (float)((double)n * 16.0 * iters / (ms * 1e-3) / 1e9);
+    return CPT_OK;
+}
+
 int cpt_selftest_qdiv(cpt_ctx* c, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len) {
     if (!c || !out || out_len < 1 || which < 0 || which > 2) return CPT_ERR_INVALID_ARG;
     HIP_TRY(c, hipSetDevice(c->device));

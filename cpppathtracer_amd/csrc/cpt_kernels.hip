@@ -642,6 +642,26 @@ hipError_t launch_math_batch(int op, const float* a, const float* b, float* out,
     return hipGetLastError();
 }
 
+// ======================================================================================
+// HBM streaming-read ceiling (confirm the roofline's peak on the box).
+// Grid-stride 16-B loads over a buffer far larger than the 256 MiB Infinity Cache; the sum
+// is stored only under a condition that never holds, so the kernel moves read bytes only.
+// ======================================================================================
+__global__ void __launch_bounds__(256) k_stream_read(const float4* __restrict__ p, size_t n, float* out) {
+    float acc = 0.f;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float4 v = p[i];
+        acc += (v.x + v.y) + (v.z + v.w);
+    }
+    if (acc == 1.2345e-30f) out[0] = acc;
+}
+
+hipError_t launch_stream_read(const float4* p, size_t n, float* out, int grid, hipStream_t stream) {
+    hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, stream, p, n, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len,
                                 hipStream_t stream) {
     hipLaunchKernelGGL(k_selftest_qdiv, dim3(4096), dim3(256), 0, stream, which, n, seed, out, out_len);

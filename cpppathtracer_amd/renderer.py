@@ -194,6 +194,12 @@ class Renderer:
         self._check(self._L.cpt_get_walk_info(self._ctx, _p(out)))
         return dict(zip(("n_bvh", "n_walk", "n_wide", "n_unb"), (int(x) for x in out)))
 
+    def measure_read_bandwidth(self, nbytes=4 << 30, iters=10):
+        """HBM streaming-read ceiling in GB/s (cpt_measure_read_bandwidth)."""
+        out = ctypes.c_float(0.0)
+        self._check(self._L.cpt_measure_read_bandwidth(self._ctx, int(nbytes), int(iters), ctypes.byref(out)))
+        return float(out.value)
+
     def reset_stats(self):
         self._check(self._L.cpt_reset_stats(self._ctx))
 

@@ -249,6 +249,10 @@ int cpt_copy_bgra_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
  * when the frame is created and by this call). */
 int cpt_reset_display(cpt_ctx* ctx);
 
+/* HBM streaming-read ceiling of the device (the roofline peak, measured on
+ * the box): `iters` grid-stride 16-B-per-lane read passes over a fresh `bytes`-byte buffer
+ * (use >> 256 MiB so the Infinity Cache cannot serve it), GB/s from HIP events. */
+int cpt_measure_read_bandwidth(cpt_ctx* ctx, size_t bytes, int iters, float* gbps);
 /* Device-math known-answer surface used by the parity tests: op 0 powf(a,b), 1 sinf(a),
  * 2 cosf(a), 3 asinf(a), 4 atanf(a), 5 (float)pow((double)a, 1.0/(double)b),
  * 6 (float)((double)a / (double)b) [IEEE f64 division], 7 a / b [f32 division],

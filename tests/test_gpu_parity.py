@@ -375,3 +375,10 @@ def test_wide_walk_structure_and_deep_tree_fallback(gpu, oracle_mod, sky):
         np.testing.assert_array_equal(gr, orng)
         np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
         _check_stats(gs, os_, path)
+
+
+def test_hbm_read_probe(gpu):
+    """cpt_measure_read_bandwidth (the bench's measured roofline ceiling) returns a sane GB/s
+    for a 1 GiB buffer: above 1 TB/s, below the 8 TB/s spec (with 5% slack for timer noise)."""
+    gbps = gpu.measure_read_bandwidth(1 << 30, 5)
+    assert 1000.0 < gbps < 8400.0, gbps
