@@ -16,6 +16,10 @@
 //      certificate: the winner's own AABB must pass the exact slab test at t = t_win, else
 //      the segment falls back to the reference walk (counted)
 //   6  as 4, with the margin and the certificate of mode 5
+//   7  as 5, on the 4-wide collapse of the SAH tree (cpt_capi.cpp linearise_wide) with a
+//      stack walk; LAB_WIDTH=8 collapses to 8 children, LAB_SORT orders the hit children by
+//      entry distance, LAB_CULL re-tests popped entries at the current tmax
+// LAB_NB sets the SAH bin count (default 16), LAB_MARGIN the conservative margin.
 #include "../oracle/cpt_oracle.cpp"
 #include <cstdlib>
 #include <functional>
