@@ -734,6 +734,9 @@ __device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const R
 #ifndef CPT_WIDE_CULL
 #define CPT_WIDE_CULL 0    // keep each stack entry's entry distance; pops beyond the limit are dropped
 #endif
+#ifndef CPT_WIDE_PLATFORMS_FIRST
+#define CPT_WIDE_PLATFORMS_FIRST 1   // test the unbounded leaves before the wide walk, wave-wide
+#endif
 #ifndef CPT_WIDE_SLOTS
 #define CPT_WIDE_SLOTS 1   // leaves a lane may park before it stops (1 or 2)
 #endif
@@ -801,7 +804,20 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     // start: the platforms (reference-rank order, as at the head of the binary orders), then
     // the tree's root
     int sp = 0, cur = 0;
-    if (p.n_unb > 0) {
+    if (CPT_WIDE_PLATFORMS_FIRST) {
+        // the platforms (every ray tests them) run first, by the whole wave at once, so the
+        // walk starts with their tmax; same rank rule, so the order does not matter
+        for (int k = 0; k < p.n_unb; ++k) {
+            if (STATS) cnt.prims++;
+            const Node pl = nodes(p.n_nodes + k);
+            int kk;
+            if (ranked_leaf_test<true, true, false>(pl, ray, tmax, kk, best_rank)) {
+                best = p.n_nodes + k;
+                kind = kk;
+            }
+        }
+        limit = walk_limit(tmax);
+    } else if (p.n_unb > 0) {
         for (int k = p.n_unb; k >= 1; --k) {   // the root, then platforms n_unb-1 .. 1
             stk[sp * WIDE_LANES] = k == p.n_unb ? 0 : ~(p.n_nodes + k);
             if (CPT_WIDE_CULL) stk_lo[sp * WIDE_LANES] = -3.0e38f;
