@@ -64,6 +64,8 @@ CPT_PATH_MEGAKERNEL = 0x000
 CPT_PATH_WAVEFRONT = 0x100
 CPT_TRAVERSAL_ORDERED = 0x200
 CPT_TRAVERSAL_PLAIN_LEAVES = 0x400
+CPT_SCHEDULE_COST = 0x800
+CPT_SCHEDULE_ROWS = 0x1000
 
 
 class CptError(RuntimeError):

@@ -48,8 +48,14 @@ struct KParams {
     float* depth;           // [n_rows*width]    (AUX)
     unsigned long long* stats;  // [5]           (STATS)
     uint32_t* work;         // pixel dequeue counter (zeroed before each launch)
+    const uint32_t* tile_order;  // megakernel dequeue order of the 8x8 tiles (nullptr: row-major)
     int spp, max_depth, accumulate;
 };
+
+// Longest-first tile schedule (cpt_kernels.hip k_tile_probe, DESIGN.md §Tile schedule):
+// scratch holds tile_schedule_scratch_words() u32, order one u32 per 8x8 tile.
+size_t tile_schedule_scratch_words(int width, int n_rows);
+hipError_t launch_tile_schedule(const KParams& p, int passes, uint32_t* scratch, uint32_t* order, hipStream_t stream);
 
 // Wavefront path state (cpt_wavefront.hip): SoA float4 arrays indexed by pixel + queues.
 struct WfState {
