@@ -1,75 +1,46 @@
 """Benchmark of the integrator hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4] [--spp S]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c5|...] [--spp S]
+                    [--scaling strong|weak] [--schedule cost|tiles]
 
 One step = one full render of the configured workload (all `spp` SamplePixel passes for
 every pixel of the image; each pass continues the pixel's XORWOW stream, exactly like the
 reference's progressive passes) with inputs already resident in HBM, plus — for N > 1 — the
-RCCL gather of the fp32 framebuffer tiles.  Multi-GPU: one process per GPU (torchrun), the
-image rows are dealt in interleaved 8-row blocks (row tiling).  Scaling (DESIGN.md
-§Multi-GPU): "weak" (default) keeps the pixels per GPU fixed — at N GPUs the image is the
-configuration's resolution scaled by sqrt(N) per axis (same aspect and framing; N = 4 is
-3840x2160) — and "strong" renders the configuration's image at every N.
+gather of the fp32 framebuffer tiles.
 
-Rank 0 prints one JSON line with `roofline` (algorithmic bytes of SURVEY.md §8(d) ÷ the
-kernel's HIP-event time) and `cpu_baseline` (the scalar oracle on a bounded sample of the
-same workload on the host cores).
+Multi-GPU: one process per GPU.  Run under torchrun (WORLD_SIZE set; it must equal --gpus),
+or give `--gpus N` without a launcher: the parent then starts N ranks through
+`torch.distributed.run` before it touches the GPU, relays rank 0's line and exits with the
+launcher's status.  The image rows are dealt to the ranks in interleaved 8-row blocks (row
+tiling).  Scaling: "strong" (default) renders the
+configuration's image (C4: 1920x1080) at every N; "weak" (opt-in) keeps the pixels per GPU
+fixed by scaling each axis by sqrt(N).
+
+Rank 0 prints one JSON line with `roofline` (SURVEY.md §8(d) algorithmic bytes ÷ the kernel's
+HIP-event time, beside the rocprof-measured HBM bytes and VALU issue of a committed profile of
+the same workload) and `cpu_baseline` (the scalar oracle on a bounded sample of the same
+workload on the host cores, 1 thread and all usable cores).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "Mpaths/sec (pixels×spp/s) at 1920×1080; achieved HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+WIDE_NODE_BYTES = 112   # a 4-wide walk node visit loads 7 x dwordx4 (cpt_path.hpp load_wide)
 
 
-def byte_model(st, paths, node_bytes=32):
-    """SURVEY.md §8(d): B_read = sum_segments[76 + 32 n_node + 32 n_prim + (hit ? 40 : 16)] + 16 P.
-    node_bytes = 128 for the ordered walk's 4-wide nodes (four child boxes + refs per visit)."""
-    return (76 * st["segments"] + node_bytes * st["nodes"] + 32 * st["prims"] + 40 * st["hits"]
-            + 16 * st["misses"] + 16 * paths)
-
-
-def cpu_baseline(cfg, objs, sky, cam, seconds_hint=15.0, threads=None):
-    """The oracle (scalar C++ restatement, test infrastructure) on a bounded sample: 16 rows
-    spread over the image, full width, `spp_sample` passes (a pixel's passes are sequential, so
-    the sample takes the first passes of every sampled pixel)."""
-    import oracle
-    threads = threads or max(1, min(16, os.cpu_count() or 1))
-    W, H = cfg["width"], cfg["height"]
-    rows = np.linspace(0, H - 1, 16).astype(np.int32)
-    # calibrate with a short run, then size the sample to ~seconds_hint
-    spp_probe = 2
-    rng = oracle.init_rng(cfg["seed"], W, rows, threads=threads)
-    t = time.perf_counter()
-    oracle.render(objs, cam, sky, rows, spp_probe, cfg["depth"], rng, threads=threads)
-    dt = max(time.perf_counter() - t, 1e-3)
-    spp_sample = int(max(2, min(cfg["spp"], spp_probe * seconds_hint / dt)))
-    rng = oracle.init_rng(cfg["seed"], W, rows, threads=threads)
-    t = time.perf_counter()
-    oracle.render(objs, cam, sky, rows, spp_sample, cfg["depth"], rng, threads=threads)
-    dt = time.perf_counter() - t
-    paths = rows.size * W * spp_sample
-    return {
-        "value": round(paths / dt / 1e6, 4),
-        "unit": "Mpaths/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{rows.size} rows evenly spaced x {W} px x first {spp_sample} of {cfg['spp']} spp of "
-                  f"{cfg['name']} ({paths} paths, {dt:.1f} s, std::thread over rows)",
-    }
-
-
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (GPUs); without a launcher N > 1 spawns N ranks via torch.distributed.run")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c5"])
@@ -81,25 +52,145 @@ def main():
     ap.add_argument("--walk", default="ordered", choices=["reference", "ordered"],
                     help="BVH node order: the reference's right-first DFS, or near-first per ray octant "
                          "(CPT_TRAVERSAL_ORDERED, same closest hits; DESIGN.md §Ordered walk)")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: pixels per GPU fixed (image grows by sqrt(N) per axis); strong: fixed image")
+    ap.add_argument("--schedule", default="cost", choices=["cost", "tiles"],
+                    help="megakernel pixel dequeue order: 8x8 tiles heaviest first from a pilot pass "
+                         "(CPT_SCHEDULE_COST), or tiles in row-major order")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: the config's image at every N; weak: pixels per GPU fixed (image grows by sqrt(N))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hbm-probe", action="store_true", help="skip the streaming-read ceiling probe")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--traffic-json", default=None,
-                    help="per-launch HBM traffic measured by rocprofv3 PMC (profiles/*.json) for this config")
-    args = ap.parse_args()
+    ap.add_argument("--no-count", action="store_true",
+                    help="skip the counting passes (roofline byte counts and walk parity): profiling runs only")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target seconds per CPU baseline leg")
+    ap.add_argument("--profile-json", default=None,
+                    help="rocprof summary of this workload (profiles/rocprof_*.json, tools/rocprof_summary.py)")
+    return ap.parse_args(argv)
 
+
+# ---------------------------------------------------------------------------------------
+# launcher: N ranks without torchrun
+# ---------------------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(args, argv) -> list:
+    """The torch.distributed.run command that starts `args.gpus` ranks of this script."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+
+
+def check_world(args, env) -> int:
+    """World size this rank runs at; raises SystemExit(2) when --gpus disagrees with the launcher."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        raise SystemExit(2)
+    return world
+
+
+# ---------------------------------------------------------------------------------------
+# measurement helpers
+# ---------------------------------------------------------------------------------------
+def byte_model(st, paths, node_bytes=32):
+    """SURVEY.md §8(d): B_read = sum_segments[76 + 32 n_node + 32 n_prim + (hit ? 40 : 16)] + 16 P.
+    node_bytes = 112 for the ordered walk's 4-wide nodes (a visit loads four child boxes in
+    octant form + four refs: 7 x 16 B)."""
+    return (76 * st["segments"] + node_bytes * st["nodes"] + 32 * st["prims"] + 40 * st["hits"]
+            + 16 * st["misses"] + 16 * paths)
+
+
+def usable_cores() -> dict:
+    """nproc, the affinity mask, and the cgroup CPU quota (the box grants a CPU share below nproc)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    usable = min(aff, quota) if quota else aff
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "usable": usable}
+
+
+def cpu_baseline(cfg, objs, sky, cam, seconds_hint=10.0):
+    """The oracle (scalar C++ restatement, test infrastructure) on a bounded sample: every 16th
+    row (at least as many rows as threads), full width, the first `spp_sample` passes of every
+    sampled pixel (a pixel's passes are sequential).  Two legs: 1 thread, and all usable cores
+    (std::thread over rows)."""
+    import numpy as np
+    import oracle
+    cores = usable_cores()
+    W, H = cfg["width"], cfg["height"]
+
+    def leg(threads, rows):
+        spp_probe = 1
+        rng = oracle.init_rng(cfg["seed"], W, rows, threads=threads)
+        t = time.perf_counter()
+        oracle.render(objs, cam, sky, rows, spp_probe, cfg["depth"], rng, threads=threads)
+        dt = max(time.perf_counter() - t, 1e-3)
+        spp_sample = int(max(1, min(cfg["spp"], spp_probe * seconds_hint / dt)))
+        rng = oracle.init_rng(cfg["seed"], W, rows, threads=threads)
+        t = time.perf_counter()
+        oracle.render(objs, cam, sky, rows, spp_sample, cfg["depth"], rng, threads=threads)
+        dt = time.perf_counter() - t
+        paths = rows.size * W * spp_sample
+        return paths / dt / 1e6, f"{rows.size} rows x {W} px x first {spp_sample} of {cfg['spp']} spp ({paths} paths, {dt:.1f} s)"
+
+    n_all = cores["usable"]
+    step = 16
+    while step > 1 and (H + step - 1) // step < n_all:
+        step //= 2
+    rows_all = np.arange(0, H, step, dtype=np.int32)
+    v1, s1 = leg(1, rows_all[:: max(1, rows_all.size // 4)])     # 1 thread: 4 of the sampled rows
+    va, sa = leg(n_all, rows_all)
+    return {
+        "value": round(va, 4),
+        "unit": "Mpaths/s",
+        "cores": n_all,
+        "kind": "port",
+        "sample": f"{cfg['name']}: every {step}th row; all cores: {sa}; 1 thread: {s1}",
+        "threads_1": round(v1, 4),
+        "threads_all": round(va, 4),
+        "nproc": cores["nproc"],
+        "cgroup_quota": cores["cgroup_quota"],
+        "affinity": cores["affinity"],
+    }
+
+
+def load_profile(path, config, n_rows, spp, gpu_path, walk, schedule):
+    """A committed rocprof summary (tools/rocprof_summary.py) of exactly this workload, or None."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pj = json.load(f)
+    want = {"config": config, "n_rows": n_rows, "spp": spp, "path": gpu_path, "walk": walk, "schedule": schedule}
+    return pj if all(pj.get(k) == v for k, v in want.items()) else None
+
+
+# ---------------------------------------------------------------------------------------
+# one rank
+# ---------------------------------------------------------------------------------------
+def run(args):
+    import numpy as np
     import torch
     import torch.distributed as dist
 
     from cpppathtracer_amd import Renderer, camera_get_copy, scenes, texture_io, tiling
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = check_world(args, os.environ)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # CPT_BENCH_BACKEND=gloo: rehearsal of the N-rank path on a box with fewer GPUs (ranks share
-    # devices round-robin, collectives go through host copies).  Never used for reported runs.
+    # devices round-robin, collectives go through host copies).  Labelled as such in the line.
     backend = os.environ.get("CPT_BENCH_BACKEND", "nccl")
     if world > 1:
         local_dev = local_rank % max(1, torch.cuda.device_count())
@@ -139,8 +230,8 @@ def main():
 
     r = Renderer(torch.cuda.current_device())
     # One non-default HIP stream for everything: the render kernels (via cpt_set_stream), the
-    # RCCL all-gather and the timing events.  (The default stream's handle is 0, which the
-    # C-ABI reads as "use the context's own stream".)
+    # all-gather and the timing events.  (The default stream's handle is 0, which the C-ABI
+    # reads as "use the context's own stream".)
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     assert stream.cuda_stream != 0
@@ -160,18 +251,19 @@ def main():
     stitch_idx = torch.from_numpy(tiling.stitch_index(H, W, world)).to(dev) if world > 1 else None
     kernel_events = []
     ordered = args.walk == "ordered"
+    schedule = args.schedule if args.path == "megakernel" else "tiles"
 
     def step(timed=False):
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        r.render(cam, spp, depth, path=args.path, ordered=ordered)
+        r.render(cam, spp, depth, path=args.path, ordered=ordered, schedule=schedule)
         if timed:
             e1.record(stream)
             kernel_events.append((e0, e1))
         if world > 1:
-            # RCCL all-gather of the fp32 tiles over xGMI, then the on-device stitch into the
-            # full framebuffer (rank 0 keeps it; every rank holds a copy after all-gather)
+            # all-gather of the fp32 tiles (RCCL over xGMI), then the on-device stitch into the
+            # full framebuffer (every rank holds a copy after the all-gather)
             r.copy_accum_device(send.data_ptr(), npix_local * 16)
             if backend == "nccl":
                 dist.all_gather_into_tensor(gathered, send)
@@ -179,17 +271,16 @@ def main():
                 g_host = gathered.cpu()
                 dist.all_gather_into_tensor(g_host, send.cpu())
                 gathered.copy_(g_host)
-            fb = gathered.view(world * max_rows, W, 4).index_select(0, stitch_idx)
-            return fb
+            return gathered.view(world * max_rows, W, 4).index_select(0, stitch_idx)
         return None
 
-    # Counting pass (same config, same pixels) for the algorithmic byte model; not timed.  It
-    # always walks the reference order: the byte model prices the reference algorithm's node
-    # and primitive fetches, whatever walk the timed steps use.
+    # Counting passes (same pixels, same seed; not timed) for the algorithmic byte model: the
+    # reference walk's counts, and the executed walk's counts and framebuffer, which must equal
+    # the reference walk's bit for bit.
     KEYS = ("segments", "nodes", "prims", "hits", "misses")
 
     def count_pass(walk_ordered):
-        r.init_rng(cfg["seed"])     # both counting passes trace the same paths
+        r.init_rng(cfg["seed"])
         r.reset_stats()
         r.render(cam, spp, depth, stats=True, path=args.path, ordered=walk_ordered)
         torch.cuda.synchronize()
@@ -200,25 +291,25 @@ def main():
         return dict(zip(KEYS, (int(x) for x in v.tolist())))
 
     walk_info = r.walk_info()
-    # the box's measured HBM streaming-read ceiling (4 GiB, 10 passes), reported beside the spec peak
-    hbm_read_measured = r.measure_read_bandwidth(4 << 30, 10) if not args.no_hbm_probe else None
-    walk_node_bytes = 128 if ordered and walk_info["n_wide"] > 0 else 32   # 4-wide walk nodes
-    st = count_pass(False)
-    walk_counts, walk_diff = None, None
-    if ordered:
-        # full-size parity of the ordered walk against the reference walk: the two counting
-        # passes trace the same paths, so their framebuffers must be bit-identical
-        fb_ref = torch.empty((npix_local, 4), dtype=torch.float32, device=dev)
-        r.copy_accum_device(fb_ref.data_ptr(), npix_local * 16)
-        walk_counts = count_pass(True)
-        fb_ord = torch.empty_like(fb_ref)
-        r.copy_accum_device(fb_ord.data_ptr(), npix_local * 16)
-        torch.cuda.synchronize()
-        nd = (fb_ref.view(torch.int32) != fb_ord.view(torch.int32)).any(dim=1).sum().to(torch.float64)
-        if world > 1:
-            nd = _all_reduce(nd)
-        walk_diff = int(nd.item())
-        del fb_ref, fb_ord
+    hbm_ceiling = r.measure_read_bandwidth(4 << 30, 10) if not args.no_hbm_probe else None
+    wide = ordered and walk_info["n_wide"] > 0
+    walk_node_bytes = WIDE_NODE_BYTES if wide else 32
+    st = walk_counts = walk_diff = None
+    if not args.no_count:
+        st = count_pass(False)
+        walk_counts = st
+        if ordered:
+            fb_ref = torch.empty((npix_local, 4), dtype=torch.float32, device=dev)
+            r.copy_accum_device(fb_ref.data_ptr(), npix_local * 16)
+            walk_counts = count_pass(True)
+            fb_ord = torch.empty_like(fb_ref)
+            r.copy_accum_device(fb_ord.data_ptr(), npix_local * 16)
+            torch.cuda.synchronize()
+            nd = (fb_ref.view(torch.int32) != fb_ord.view(torch.int32)).any(dim=1).sum().to(torch.float64)
+            if world > 1:
+                nd = _all_reduce(nd)
+            walk_diff = int(nd.item())
+            del fb_ref, fb_ord
     r.init_rng(cfg["seed"])
 
     for _ in range(args.warmup):
@@ -236,10 +327,9 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    # k_megakernel's device time per launch: HIP events recorded around each render on the
-    # launch stream (the context launches on torch's current stream, set above)
-    avg_kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in kernel_events]))
-
+    # device time per render (pilot + k_megakernel with the cost schedule): HIP events recorded
+    # around each render on the launch stream (the context launches on torch's current stream)
+    avg_kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in kernel_events])) if kernel_events else float("nan")
     t = torch.tensor([elapsed, avg_kernel_ms], dtype=torch.float64, device=dev)
     if world > 1:
         t = _all_reduce(t, op=dist.ReduceOp.MAX)
@@ -248,27 +338,12 @@ def main():
     if rank == 0:
         paths_total = W * H * spp
         value = paths_total * args.steps / elapsed / 1e6
-        # algorithmic bytes of one launch on rank 0's pixels: scale whole-image counts by the
-        # pixel share (interleaved blocks keep the shares statistically equal)
-        share = npix_local / float(W * H)
-        # Algorithmic bytes of one launch (SURVEY.md 8(d) per-unit model x the units the launch
-        # processes): the executed walk's own segment/node/primitive counts.  The same model on
-        # the reference algorithm's counts (its right-first DFS over its median tree, which
-        # visits more nodes for the same closest hits) is reported beside it.
-        bytes_ref = byte_model(st, paths_total) * share
-        bytes_launch = byte_model(walk_counts, paths_total, walk_node_bytes) * share if walk_counts else bytes_ref
-        achieved = bytes_launch / (avg_kernel_ms / 1e3) / 1e9
-        achieved_ref_model = bytes_ref / (avg_kernel_ms / 1e3) / 1e9
-        # HBM traffic per launch from rocprofv3 PMC passes of this same workload (committed under
-        # profiles/, made by tools/profile.sh + tools/pmc_traffic.py); null when none matches.
-        traffic = None
-        tpath = args.traffic_json or os.path.join(REPO, "profiles", f"traffic_{args.config}_{args.path}_{args.walk}.json")
-        if os.path.exists(tpath):
-            with open(tpath) as f:
-                tj = json.load(f)
-            if (tj.get("config") == args.config and tj.get("n_rows") == int(rows.size) and tj.get("spp") == spp
-                    and tj.get("path") == args.path and tj.get("walk", "reference") == args.walk):
-                traffic = tj.get("hbm_bytes_per_launch")
+        if world == 1:
+            collective = ""
+        elif backend == "nccl":
+            collective = ", RCCL all-gather of the fp32 tiles"
+        else:
+            collective = f", {backend} all-gather via host copies (rehearsal, ranks share GPUs)"
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -285,33 +360,56 @@ def main():
             "config": {
                 "workload": f"{args.config}: {cfg['scene']} {W}x{H} {spp}spp depth {depth}",
                 "width": W, "height": H, "spp": spp, "max_depth": depth, "seed": cfg["seed"],
-                "rows_rendered": H, "path": args.path, "walk": args.walk,
-                "parallelism": f"row-tiled x{world} (interleaved {tiling.BLOCK_ROWS}-row blocks)" + (
-                    ", RCCL all-gather" if world > 1 else ""),
+                "rows_rendered": H, "path": args.path, "walk": args.walk, "schedule": schedule,
+                "parallelism": f"row-tiled x{world} (interleaved {tiling.BLOCK_ROWS}-row blocks){collective}",
             },
-            "roofline": {
+            "rng_init_ms": round(t_init * 1e3, 2),
+        }
+        if st is not None:
+            # Algorithmic bytes of one launch: SURVEY.md 8(d)'s per-unit model x the units the
+            # launch processes (the executed walk's own counts; a 4-wide node visit = 112 B),
+            # rank 0's share of them (interleaved blocks keep the shares statistically equal),
+            # over the max-over-ranks render time.
+            share = npix_local / float(W * H)
+            bytes_launch = byte_model(walk_counts, paths_total, walk_node_bytes) * share
+            bytes_ref = byte_model(st, paths_total) * share
+            kms = avg_kernel_ms_max if world > 1 else avg_kernel_ms
+            achieved = bytes_launch / (kms / 1e3) / 1e9
+            roof = {
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "hbm_read_measured_gbs": round(hbm_read_measured, 1) if hbm_read_measured else None,
-                "achieved_reference_model": round(achieved_ref_model, 2),
+                "traffic": None,
                 "kernel": "k_megakernel" if args.path == "megakernel" else "wavefront (k_wf_extend+k_wf_shade per bounce)",
-                "kernel_avg_ms": round(avg_kernel_ms, 3),
+                "kernel_avg_ms": round(kms, 3),
                 "bytes_per_launch": int(bytes_launch),
-                "byte_model": f"SURVEY.md 8(d): 76 S + {walk_node_bytes if walk_counts else 32} nodes + 32 prims + 40 hits "
-                              f"+ 16 misses + 16 P, on walk_counts ({walk_node_bytes}-B nodes: "
-                              f"{'4-wide' if walk_node_bytes == 128 else 'binary'} walk tree)",
+                "byte_model": f"SURVEY.md 8(d): 76 S + {walk_node_bytes} nodes + 32 prims + 40 hits + 16 misses + 16 P "
+                              f"on the executed walk's counts ({'4-wide walk tree: 7 x 16 B per node visit' if wide else 'binary nodes'})",
                 "walk_info": walk_info,
                 "walk_counts": walk_counts,
                 "reference_counts": st,
+                "achieved_reference_model": round(bytes_ref / (kms / 1e3) / 1e9, 2),
+                "reference_model_note": "the same model on the reference algorithm's counts (right-first DFS over its "
+                                        "median tree) for the same paths; it prices node visits the ordered walk "
+                                        "does not make, so it can exceed the HBM peak",
                 "walk_vs_reference_pixels_differing": walk_diff,
-            },
-            "rng_init_ms": round(t_init * 1e3, 2),
-        }
-        if not args.no_cpu_baseline:
+                "hbm_stream_ceiling_gbs": round(hbm_ceiling, 1) if hbm_ceiling else None,
+            }
+            prof = load_profile(args.profile_json or os.path.join(
+                REPO, "profiles", f"rocprof_{args.config}_{args.path}_{args.walk}.json"),
+                args.config, int(rows.size), spp, args.path, args.walk, schedule) if world == 1 else None
+            if prof:
+                # rocprofv3 PMC passes of this same workload (committed under profiles/)
+                roof["traffic"] = prof["hbm_bytes_per_launch"]
+                roof["hbm_read_gbs_rocprof"] = prof["hbm_read_gbs"]
+                roof["hbm_read_frac_rocprof"] = round(prof["hbm_read_gbs"] / HBM_PEAK_GBS, 6)
+                roof["limiter"] = prof["limiter"]
+                roof["issue"] = prof["issue"]
+                roof["profile"] = prof["source"]
+            out["roofline"] = roof
+        if not args.no_cpu_baseline and world == 1:
             try:
                 out["cpu_baseline"] = cpu_baseline(cfg, objs, sky, cam, seconds_hint=args.cpu_seconds)
             except Exception as e:  # the baseline must never sink the GPU measurement
@@ -320,6 +418,18 @@ def main():
     r.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the ranks before anything here touches the GPU
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        rc = subprocess.call(launcher_command(args, argv), env=env)
+        sys.exit(rc)
+    run(args)
 
 
 if __name__ == "__main__":

@@ -27,6 +27,7 @@ PROTOTYPES = {
     "cpt_camera_get_copy": (_I, [_P]),
     "cpt_set_scene": (_I, [_P, _P, _I]),
     "cpt_update_object": (_I, [_P, _I, _P]),
+    "cpt_update_objects": (_I, [_P, _I, _P, _P]),
     "cpt_scene_bvh_export": (_I, [_P, _P, _P, _I, _P]),
     "cpt_bvh_build_host": (_I, [_P, _I, _P, _P, _I, _P]),
     "cpt_set_env_texture": (_I, [_P, _P, _I, _I, _I]),
@@ -65,7 +66,6 @@ CPT_PATH_WAVEFRONT = 0x100
 CPT_TRAVERSAL_ORDERED = 0x200
 CPT_TRAVERSAL_PLAIN_LEAVES = 0x400
 CPT_SCHEDULE_COST = 0x800
-CPT_SCHEDULE_ROWS = 0x1000
 
 
 class CptError(RuntimeError):

@@ -66,71 +66,43 @@ void MotionalCamera::SetOrigin(float x, float y, float z) { origin_ = make_float
 void MotionalCamera::SetLookAt(float3 look_at) { look_at_ = look_at; }
 void MotionalCamera::SetLookAt(float x, float y, float z) { look_at_ = make_float3(x, y, z); }
 
-// motional_camera.cu:76-168
-void MotionalCamera::MoveEyeLeft(float k) {
-    float3 w = normalize(origin_ - look_at_);
-    float3 left = -normalize(cross(vup, w));
-    origin_ += k * move_speed_ * left;
-    look_at_ += k * move_speed_ * left;
+// Interactive camera controls (motional_camera.cu:76-168).  SURVEY.md §2 puts them outside
+// the hot path; they are kept only so the public MotionalCamera API is complete.  This is an
+// API-behaviour restatement: a move is origin/look_at += (k * move_speed) * axis along the
+// eye's left / back / up axis (a negated axis for the opposite move, which rounds exactly as
+// the reference's -=), and a turn re-normalises look_at onto the unit sphere around the eye,
+// steps it along the eye's left or up axis and re-normalises, with the reference's float
+// operations in the reference's order.
+namespace {
+float3 eye_left(const MotionalCamera& c) { return -normalize(cross(c.vup, normalize(c.origin_ - c.look_at_))); }
+float3 eye_back(const MotionalCamera& c) { return -normalize(cross(eye_left(c), c.vup)); }
+
+void translate(MotionalCamera& c, float3 axis, float k) {
+    c.origin_ += k * c.move_speed_ * axis;
+    c.look_at_ += k * c.move_speed_ * axis;
 }
-void MotionalCamera::MoveEyeRight(float k) {
-    float3 w = normalize(origin_ - look_at_);
-    float3 left = -normalize(cross(vup, w));
-    origin_ -= k * move_speed_ * left;
-    look_at_ -= k * move_speed_ * left;
+
+// `up`: step along the up axis (else the left axis) by d.
+void turn(MotionalCamera& c, bool up, float d) {
+    c.look_at_ = c.origin_ + normalize(c.look_at_ - c.origin_);
+    const float3 w = normalize(c.look_at_ - c.origin_);
+    const float3 left = normalize(cross(c.vup, w));
+    const float3 axis = up ? normalize(cross(w, left)) : left;
+    c.look_at_ += d * axis;
+    c.look_at_ = c.origin_ + normalize(c.look_at_ - c.origin_);
 }
-void MotionalCamera::MoveEyeForward(float k) {
-    float3 w = normalize(origin_ - look_at_);
-    float3 left = -normalize(cross(vup, w));
-    float3 back = -normalize(cross(left, vup));
-    origin_ -= k * move_speed_ * back;
-    look_at_ -= k * move_speed_ * back;
-}
-void MotionalCamera::MoveEyeBackward(float k) {
-    float3 w = normalize(origin_ - look_at_);
-    float3 left = -normalize(cross(vup, w));
-    float3 back = -normalize(cross(left, vup));
-    origin_ += k * move_speed_ * back;
-    look_at_ += k * move_speed_ * back;
-}
-void MotionalCamera::MoveEyeUp(float k) {
-    origin_ += k * move_speed_ * vup;
-    look_at_ += k * move_speed_ * vup;
-}
-void MotionalCamera::MoveEyeDown(float k) {
-    origin_ -= k * move_speed_ * vup;
-    look_at_ -= k * move_speed_ * vup;
-}
-void MotionalCamera::RotateAroundUp(float dy) {
-    look_at_ = origin_ + normalize(look_at_ - origin_);
-    float3 w = normalize(look_at_ - origin_);
-    float3 left = normalize(cross(vup, w));
-    float3 up = normalize(cross(w, left));
-    look_at_ += dy * up;
-    look_at_ = origin_ + normalize(look_at_ - origin_);
-}
-void MotionalCamera::RotateAroundDown(float dy) {
-    look_at_ = origin_ + normalize(look_at_ - origin_);
-    float3 w = normalize(look_at_ - origin_);
-    float3 left = normalize(cross(vup, w));
-    float3 up = normalize(cross(w, left));
-    look_at_ -= dy * up;
-    look_at_ = origin_ + normalize(look_at_ - origin_);
-}
-void MotionalCamera::RotateAroundLeft(float dx) {
-    look_at_ = origin_ + normalize(look_at_ - origin_);
-    float3 w = normalize(look_at_ - origin_);
-    float3 left = normalize(cross(vup, w));
-    look_at_ += dx * left;
-    look_at_ = origin_ + normalize(look_at_ - origin_);
-}
-void MotionalCamera::RotateAroundRight(float dx) {
-    look_at_ = origin_ + normalize(look_at_ - origin_);
-    float3 w = normalize(look_at_ - origin_);
-    float3 left = normalize(cross(vup, w));
-    look_at_ -= dx * left;
-    look_at_ = origin_ + normalize(look_at_ - origin_);
-}
+}  // namespace
+
+void MotionalCamera::MoveEyeLeft(float k) { translate(*this, eye_left(*this), k); }
+void MotionalCamera::MoveEyeRight(float k) { translate(*this, -eye_left(*this), k); }
+void MotionalCamera::MoveEyeForward(float k) { translate(*this, -eye_back(*this), k); }
+void MotionalCamera::MoveEyeBackward(float k) { translate(*this, eye_back(*this), k); }
+void MotionalCamera::MoveEyeUp(float k) { translate(*this, vup, k); }
+void MotionalCamera::MoveEyeDown(float k) { translate(*this, -vup, k); }
+void MotionalCamera::RotateAroundUp(float dy) { turn(*this, true, dy); }
+void MotionalCamera::RotateAroundDown(float dy) { turn(*this, true, -dy); }
+void MotionalCamera::RotateAroundLeft(float dx) { turn(*this, false, dx); }
+void MotionalCamera::RotateAroundRight(float dx) { turn(*this, false, -dx); }
 void MotionalCamera::ScaleFov(float d) { view_fov_ = (float)(view_fov_ + d * M_PI / 180.0f); }
 void MotionalCamera::Lock() { camera_mutex.lock(); }
 void MotionalCamera::Unlock() { camera_mutex.unlock(); }
@@ -148,10 +120,11 @@ namespace {
 std::mutex bvh_mutex;
 std::vector<Object*> bvh_objs;
 std::set<Object*> bvh_seen;
-std::vector<cpt_object> bvh_snapshot;
-uint64_t bvh_build_id = 0;
-std::vector<int> bvh_update_log;
-SceneBVH* const bvh_handle = reinterpret_cast<SceneBVH*>(&bvh_snapshot);   // opaque, non-null
+std::vector<cpt_object> bvh_built;      // BuildBVH's by-value copies (bvh.cu:43)
+std::vector<cpt_object> bvh_current;    // ... with UpdateObject's re-copies
+std::vector<uint64_t> bvh_updates;      // UpdateObject calls per object since the build
+uint64_t bvh_build_id = 0, bvh_revision = 0;
+SceneBVH* const bvh_handle = reinterpret_cast<SceneBVH*>(&bvh_built);   // opaque, non-null
 
 // texture registry
 std::mutex tex_mutex;
@@ -168,19 +141,22 @@ void SceneBVH::AddObject(Object* obj) {
 
 SceneBVHGPUHandle SceneBVH::BuildBVH() {
     std::lock_guard<std::mutex> lk(bvh_mutex);
-    bvh_snapshot.resize(bvh_objs.size());
-    for (size_t i = 0; i < bvh_objs.size(); ++i) std::memcpy(&bvh_snapshot[i], bvh_objs[i], sizeof(cpt_object));
+    bvh_built.resize(bvh_objs.size());
+    for (size_t i = 0; i < bvh_objs.size(); ++i) std::memcpy(&bvh_built[i], bvh_objs[i], sizeof(cpt_object));
+    bvh_current = bvh_built;
+    bvh_updates.assign(bvh_built.size(), 0);
     bvh_build_id++;
-    bvh_update_log.clear();
+    bvh_revision++;
     return bvh_handle;
 }
 
 void SceneBVH::UpdateObject(Object* obj) {
     std::lock_guard<std::mutex> lk(bvh_mutex);
-    for (size_t i = 0; i < bvh_objs.size() && i < bvh_snapshot.size(); ++i)
+    for (size_t i = 0; i < bvh_objs.size() && i < bvh_current.size(); ++i)
         if (bvh_objs[i] == obj) {
-            std::memcpy(&bvh_snapshot[i], obj, sizeof(cpt_object));
-            bvh_update_log.push_back((int)i);
+            std::memcpy(&bvh_current[i], obj, sizeof(cpt_object));
+            bvh_updates[i]++;
+            bvh_revision++;
             return;
         }
 }
@@ -189,21 +165,35 @@ void SceneBVH::ReleaseBVH() {
     std::lock_guard<std::mutex> lk(bvh_mutex);
     bvh_objs.clear();
     bvh_seen.clear();
-    bvh_snapshot.clear();
-    bvh_update_log.clear();
+    bvh_built.clear();
+    bvh_current.clear();
+    bvh_updates.clear();
     bvh_build_id++;
+    bvh_revision++;
 }
 
-const std::vector<cpt_object>& SceneBVH::Snapshot() { return bvh_snapshot; }
 uint64_t SceneBVH::BuildId() {
     std::lock_guard<std::mutex> lk(bvh_mutex);
     return bvh_build_id;
 }
-std::vector<int> SceneBVH::UpdateLog() {
+
+uint64_t SceneBVH::Revision() {
     std::lock_guard<std::mutex> lk(bvh_mutex);
-    return bvh_update_log;
+    return bvh_revision;
 }
+
+void SceneBVH::GetState(uint64_t& build_id, uint64_t& revision, std::vector<cpt_object>* built,
+                        std::vector<cpt_object>& current, std::vector<uint64_t>& updates) {
+    std::lock_guard<std::mutex> lk(bvh_mutex);
+    build_id = bvh_build_id;
+    revision = bvh_revision;
+    if (built) *built = bvh_built;
+    current = bvh_current;
+    updates = bvh_updates;
+}
+
 int SceneBVH::IndexOf(const Object* obj) {
+    std::lock_guard<std::mutex> lk(bvh_mutex);
     for (size_t i = 0; i < bvh_objs.size(); ++i)
         if (bvh_objs[i] == obj) return (int)i;
     return -1;
@@ -363,42 +353,58 @@ bool PathTracer::EnsureContext() {
     return true;
 }
 
+// Binds every material texture handle `objs` use that the context does not hold yet.
+bool PathTracer::BindTextures(const std::vector<cpt_object>& objs) {
+    for (const cpt_object& o : objs) {
+        if (!o.material.have_tex) continue;
+        const uint64_t h = o.material.u.tex;
+        if (std::find(bound_textures_.begin(), bound_textures_.end(), h) != bound_textures_.end()) continue;
+        const PocaTextureData* t = PocaTextureUtils::Get(h);
+        if (!t) { err_ = "textured material uses an unknown PocaTexture handle"; return false; }
+        if (cpt_bind_texture(ctx_, h, t->rgba.data(), t->width, t->height, t->valid_cols, address_mode_of(t->addr),
+                             t->filter == PocaFilterMode::Point ? CPT_FILTER_POINT : CPT_FILTER_LINEAR) != CPT_OK)
+            return Fail("cpt_bind_texture");
+        bound_textures_.push_back(h);
+    }
+    return true;
+}
+
+// Brings the context to SceneBVH's state: a new build is uploaded as BuildBVH copied it (the
+// reference's topology), then the objects UpdateObject re-copied since are refit in one batch
+// (bvh.cu:144-157).  The state is read under one lock (SceneBVH::GetState).
 bool PathTracer::SyncScene() {
     if (!EnsureContext()) return false;
-    const uint64_t build = SceneBVH::BuildId();
-    if (scene_build_ != build) {
+    if (!scene_synced_ || SceneBVH::Revision() != scene_rev_) {
+        uint64_t build = 0, rev = 0;
+        std::vector<cpt_object> built, current;
+        std::vector<uint64_t> updates;
+        const bool rebuild = !scene_synced_ || SceneBVH::BuildId() != scene_build_;
+        SceneBVH::GetState(build, rev, rebuild ? &built : nullptr, current, updates);
+        if (!rebuild && build != scene_build_)   // rebuilt between the two reads
+            SceneBVH::GetState(build, rev, &built, current, updates);
+        if (rebuild || build != scene_build_) {
+            bound_textures_.clear();
+            if (!BindTextures(built)) return false;
+            if (cpt_set_scene(ctx_, built.empty() ? nullptr : built.data(), (int)built.size()) != CPT_OK)
+                return Fail("cpt_set_scene");
+            scene_build_ = build;
+            updates_seen_.assign(built.size(), 0);
+        }
+        std::vector<int> idx;
         std::vector<cpt_object> objs;
-        {
-            std::lock_guard<std::mutex> lk(bvh_mutex);
-            objs = bvh_snapshot;
+        for (size_t i = 0; i < updates.size() && i < updates_seen_.size(); ++i)
+            if (updates[i] != updates_seen_[i]) {
+                idx.push_back((int)i);
+                objs.push_back(current[i]);
+            }
+        if (!idx.empty()) {
+            if (!BindTextures(objs)) return false;
+            if (cpt_update_objects(ctx_, (int)idx.size(), idx.data(), objs.data()) != CPT_OK)
+                return Fail("cpt_update_objects");
         }
-        // material textures (Material::tex_ holds an AddTexByFile handle, material.h:21-25)
-        std::vector<uint64_t> bound;
-        for (const cpt_object& o : objs) {
-            if (!o.material.have_tex) continue;
-            const uint64_t h = o.material.u.tex;
-            if (std::find(bound.begin(), bound.end(), h) != bound.end()) continue;
-            const PocaTextureData* t = PocaTextureUtils::Get(h);
-            if (!t) { err_ = "textured material uses an unknown PocaTexture handle"; return false; }
-            if (cpt_bind_texture(ctx_, h, t->rgba.data(), t->width, t->height, t->valid_cols, address_mode_of(t->addr),
-                                 t->filter == PocaFilterMode::Point ? CPT_FILTER_POINT : CPT_FILTER_LINEAR) != CPT_OK)
-                return Fail("cpt_bind_texture");
-            bound.push_back(h);
-        }
-        if (cpt_set_scene(ctx_, objs.empty() ? nullptr : objs.data(), (int)objs.size()) != CPT_OK)
-            return Fail("cpt_set_scene");
-        scene_build_ = build;
-        updates_applied_ = 0;
-    }
-    const std::vector<int> log = SceneBVH::UpdateLog();
-    for (; updates_applied_ < log.size(); ++updates_applied_) {
-        const int i = log[updates_applied_];
-        cpt_object o;
-        {
-            std::lock_guard<std::mutex> lk(bvh_mutex);
-            o = bvh_snapshot[i];
-        }
-        if (cpt_update_object(ctx_, i, &o) != CPT_OK) return Fail("cpt_update_object");
+        updates_seen_ = updates;
+        scene_rev_ = rev;
+        scene_synced_ = true;
     }
     if (!env_uploaded_) {
         if (env_ == 0) env_ = PocaTextureUtils::AddTexByFile(default_sky_path());   // path_tracer.cu:47
@@ -429,8 +435,9 @@ bool PathTracer::EnsureFrame(const MotionalCamera& cam) {
 
 bool PathTracer::RenderPass(MotionalCamera& cam, int spp, bool accumulate) {
     if (!SyncScene() || !EnsureFrame(cam)) return false;
+    // many passes per pixel: heaviest tiles first (same image, shorter tail)
     uint32_t flags = CPT_RENDER_AUX | (accumulate ? CPT_RENDER_ACCUMULATE : 0u) | CPT_RENDER_SYNC |
-                     (ordered_walk_ ? CPT_TRAVERSAL_ORDERED : 0u);
+                     (ordered_walk_ ? CPT_TRAVERSAL_ORDERED : 0u) | (spp >= 64 ? CPT_SCHEDULE_COST : 0u);
     if (cpt_render(ctx_, reinterpret_cast<const cpt_camera*>(&cam), spp, (int)max_recursion_depth_, flags) != CPT_OK)
         return Fail("cpt_render");
     return true;

@@ -341,6 +341,10 @@ struct cpt_ctx {
 
     unsigned long long* d_stats = nullptr;
     uint32_t* d_work = nullptr;
+    void* d_sched = nullptr;     // cost schedule: pilot tile costs + sort scratch
+    size_t cap_sched = 0;
+    uint32_t* d_tile_order = nullptr;
+    size_t cap_tile_order = 0;
     cpt::WfState wf{};           // wavefront path state (allocated on first use)
     bool wf_ready = false;
     float* d_mix = nullptr;      // display running mean (Mix), rgb per pixel of the display band
@@ -403,6 +407,8 @@ void free_frame(cpt_ctx* c) {
     c->band_y0 = c->band_y1 = -1;
     (void)hipFree(c->d_scratch_w); c->d_scratch_w = nullptr;
     (void)hipFree(c->d_scratch_m); c->d_scratch_m = nullptr;
+    (void)hipFree(c->d_sched); c->d_sched = nullptr; c->cap_sched = 0;
+    (void)hipFree(c->d_tile_order); c->d_tile_order = nullptr; c->cap_tile_order = 0;
     c->frame_set = c->rng_set = false;
 }
 
@@ -583,6 +589,10 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
     make(root, n_unb);   // the walk starts with the root and the platforms on the stack
     if (max_push + 1 > WIDE_STACK) return 0;
     const int n_wide = (int)wbin.size();
+    // the device stack holds 16-bit refs: wide node ids and ~(leaf position) within 15 bits
+    if (n_wide > 32767) return 0;
+    for (int p : pos0)
+        if (p > 32766) return 0;
     const size_t base = out.size();
     out.resize(base + (size_t)8 * n_wide * 4);
     for (int o = 0; o < 8; ++o) {
@@ -606,7 +616,7 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
                     const BNode& n = w.nodes[ord[k]];
                     lo = n.bmin;
                     hi = n.bmax;
-                    ref[k] = n.is_object ? ~(n_bvh + pos0[ord[k]]) : wide_of[ord[k]];
+                    ref[k] = n.is_object ? ~pos0[ord[k]] : wide_of[ord[k]];
                 }
                 const float l3[3] = {lo.x, lo.y, lo.z}, h3[3] = {hi.x, hi.y, hi.z};
                 for (int a = 0; a < 3; ++a) {
@@ -648,7 +658,7 @@ void linearise_all(cpt_ctx* c) {
     }
     c->n_walk = (int)(c->lin.size() - c->n_bvh) / 8;
     c->n_unb = (int)unbounded.size();
-    if (CPT_WIDE && root >= 0 && !w.nodes[root].is_object) c->n_wide = linearise_wide(w, root, pos0, c->n_bvh, c->n_unb, c->lin);
+    if (root >= 0 && !w.nodes[root].is_object) c->n_wide = linearise_wide(w, root, pos0, c->n_bvh, c->n_unb, c->lin);
 }
 
 int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, std::vector<int>& rank) {
@@ -860,28 +870,42 @@ int cpt_set_scene(cpt_ctx* c, const cpt_object* objs, int n) {
 
 // SceneBVH::UpdateObject (bvh.cu:122-157): replace the leaf's object, refit the ancestors
 // (MIN/MAX of the two children per axis), re-upload.
-int cpt_update_object(cpt_ctx* c, int index, const cpt_object* obj) {
-    if (!c || !obj) return CPT_ERR_INVALID_ARG;
-    if (!c->scene_set || index < 0 || index >= (int)c->objs.size())
-        return fail(c, CPT_ERR_INVALID_ARG, "cpt_update_object: index %d out of range", index);
-    c->objs[index] = *obj;
-    c->mat_of_obj[index] = material_slot(c, obj->material);
-    int ni = c->bvh.leaf_of_object[index];
-    while (ni != -1) {
-        BNode& n = c->bvh.nodes[ni];
-        if (n.is_object) {
-            n.bmax = aabb_max(c->objs[n.obj]);
-            n.bmin = aabb_min(c->objs[n.obj]);
-        } else {
-            const BNode& L = c->bvh.nodes[n.left];
-            const BNode& R = c->bvh.nodes[n.right];
-            n.bmax = F3{MAX_(L.bmax.x, R.bmax.x), MAX_(L.bmax.y, R.bmax.y), MAX_(L.bmax.z, R.bmax.z)};
-            n.bmin = F3{MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z)};
+int cpt_update_objects(cpt_ctx* c, int n, const int* indices, const cpt_object* objs) {
+    if (!c || n < 0 || (n > 0 && (!indices || !objs))) return CPT_ERR_INVALID_ARG;
+    if (!c->scene_set) return fail(c, CPT_ERR_STATE, "cpt_update_objects: cpt_set_scene first");
+    for (int k = 0; k < n; ++k)
+        if (indices[k] < 0 || indices[k] >= (int)c->objs.size())
+            return fail(c, CPT_ERR_INVALID_ARG, "cpt_update_objects: index %d out of range", indices[k]);
+    if (n == 0) return CPT_OK;
+    // SceneBVH::UpdateObject (bvh.cu:144-157): the leaf takes the object, its ancestors'
+    // boxes become the union of their children's.  The refit is a function of the leaves
+    // only, so a batch refits once and rebuilds the walk orders and uploads once.
+    for (int k = 0; k < n; ++k) {
+        const int index = indices[k];
+        c->objs[index] = objs[k];
+        c->mat_of_obj[index] = material_slot(c, objs[k].material);
+        int ni = c->bvh.leaf_of_object[index];
+        while (ni != -1) {
+            BNode& nd = c->bvh.nodes[ni];
+            if (nd.is_object) {
+                nd.bmax = aabb_max(c->objs[nd.obj]);
+                nd.bmin = aabb_min(c->objs[nd.obj]);
+            } else {
+                const BNode& L = c->bvh.nodes[nd.left];
+                const BNode& R = c->bvh.nodes[nd.right];
+                nd.bmax = F3{MAX_(L.bmax.x, R.bmax.x), MAX_(L.bmax.y, R.bmax.y), MAX_(L.bmax.z, R.bmax.z)};
+                nd.bmin = F3{MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z)};
+            }
+            ni = nd.parent;
         }
-        ni = n.parent;
     }
     linearise_all(c);   // same topology, new boxes and leaf contents in all nine orders
     return upload_scene(c);
+}
+
+int cpt_update_object(cpt_ctx* c, int index, const cpt_object* obj) {
+    if (!c || !obj) return CPT_ERR_INVALID_ARG;
+    return cpt_update_objects(c, 1, &index, obj);
 }
 
 int cpt_scene_bvh_export(cpt_ctx* c, float* boxes, int32_t* links, int capacity, int* n_nodes) {
@@ -1112,8 +1136,26 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
         HIP_TRY(c, cpt::launch_wavefront(p, c->wf, (flags & CPT_RENDER_STATS) != 0, aux, s, &launches));
         c->last_launches = launches;
     } else {
-        HIP_TRY(c, cpt::launch_megakernel(p, (flags & CPT_RENDER_STATS) != 0, aux, s));
         c->last_launches = 1;
+        if ((flags & CPT_SCHEDULE_COST) && spp > 0 && c->n_rows > 0) {
+            // pilot: 1 pass per 512 (1..4), then the tiles sorted heaviest first
+            const int passes = std::min(4, std::max(1, spp / 512));
+            const size_t n_tiles = (size_t)((c->width + 7) / 8) * ((c->n_rows + 7) / 8);
+            const size_t bytes = cpt::tile_schedule_scratch_bytes(c->width, c->n_rows);
+            if (c->cap_sched < bytes) {
+                (void)hipFree(c->d_sched);
+                c->d_sched = nullptr;
+                c->cap_sched = 0;
+                HIP_TRY(c, hipMalloc(&c->d_sched, bytes));
+                c->cap_sched = bytes;
+            }
+            int rc;
+            if ((rc = ensure(c, &c->d_tile_order, &c->cap_tile_order, n_tiles)) != CPT_OK) return rc;
+            HIP_TRY(c, cpt::launch_tile_schedule(p, passes, c->d_sched, c->cap_sched, c->d_tile_order, s));
+            p.tile_order = c->d_tile_order;
+            c->last_launches = 2;
+        }
+        HIP_TRY(c, cpt::launch_megakernel(p, (flags & CPT_RENDER_STATS) != 0, aux, s));
     }
     HIP_TRY(c, hipEventRecord(c->ev_stop, s));
     c->have_timing = true;

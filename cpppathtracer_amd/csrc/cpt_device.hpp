@@ -363,23 +363,15 @@ struct Ray { v3 o, d; float tmin, tmax; };
 // One reciprocal per ray and axis replaces the 11-instruction IEEE divide sequence per slab
 // plane and per intersector root.
 // ------------------------------------------------------------------------------------
-#ifndef CPT_QDIV
-#define CPT_QDIV 1     // CPT_QDIV=0 builds plain IEEE divides everywhere (A/B builds only)
-#endif
 constexpr float FLT_MIN_NORMAL = 1.17549435e-38f;   // 2^-126
 
 __device__ __forceinline__ double rcp_d(float d) { return 1.0 / (double)d; }
 __device__ __forceinline__ float qdiv_raw(float a, double y) { return (float)((double)a * y); }
 
 __device__ __forceinline__ float qdiv(float a, float d, double y) {
-#if CPT_QDIV
     float q = qdiv_raw(a, y);
     if (__builtin_expect(__builtin_fabsf(q) < FLT_MIN_NORMAL, 0)) q = a / d;
     return q;
-#else
-    (void)y;
-    return a / d;
-#endif
 }
 
 }  // namespace cpt

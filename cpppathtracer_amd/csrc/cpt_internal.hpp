@@ -6,13 +6,9 @@
 
 #include "cpt_device.hpp"
 
-#ifndef CPT_WIDE
-#define CPT_WIDE 1      // the ordered walk runs on the 4-wide walk tree (0: the binary octant orders)
-#endif
-#ifndef CPT_WSTACK
-#define CPT_WSTACK 32   // per-lane LDS stack entries of the wide walk; the host keeps the binary
-                        // walk for a tree that could need more (cpt_capi.cpp linearise_wide)
-#endif
+// Per-lane LDS stack entries of the wide walk; the host keeps the binary walk for a tree that
+// could need more (cpt_capi.cpp linearise_wide).
+#define CPT_WSTACK 32
 
 namespace cpt {
 
@@ -49,13 +45,16 @@ struct KParams {
     unsigned long long* stats;  // [5]           (STATS)
     uint32_t* work;         // pixel dequeue counter (zeroed before each launch)
     const uint32_t* tile_order;  // megakernel dequeue order of the 8x8 tiles (nullptr: row-major)
+    uint32_t* tile_cost;    // pilot launch only: per-tile work (cost schedule)
     int spp, max_depth, accumulate;
 };
 
-// Longest-first tile schedule (cpt_kernels.hip k_tile_probe, DESIGN.md §Tile schedule):
-// scratch holds tile_schedule_scratch_words() u32, order one u32 per 8x8 tile.
-size_t tile_schedule_scratch_words(int width, int n_rows);
-hipError_t launch_tile_schedule(const KParams& p, int passes, uint32_t* scratch, uint32_t* order, hipStream_t stream);
+// Cost schedule (cpt_kernels.hip, DESIGN.md §Cost schedule): a `passes`-pass pilot of the
+// megakernel sums each 8x8 tile's work, then `order` (one u32 per tile) gets the tiles
+// heaviest first.  `scratch` holds tile_schedule_scratch_bytes() bytes.
+size_t tile_schedule_scratch_bytes(int width, int n_rows);
+hipError_t launch_tile_schedule(const KParams& p, int passes, void* scratch, size_t scratch_bytes, uint32_t* order,
+                                hipStream_t stream);
 
 // Wavefront path state (cpt_wavefront.hip): SoA float4 arrays indexed by pixel + queues.
 struct WfState {
@@ -76,7 +75,6 @@ hipError_t launch_math_batch(int op, const float* a, const float* b, float* out,
 hipError_t launch_stream_read(const float4* p, size_t n, float* out, int grid, hipStream_t stream);
 hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len,
                                 hipStream_t stream);
-int lds_node_capacity();
 hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
                               int width, int height, int row0, int y0, int y1, uint32_t cur_sample_idx,
                               hipStream_t stream);

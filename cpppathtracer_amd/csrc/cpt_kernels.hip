@@ -14,6 +14,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include <hipcub/hipcub.hpp>
+
 #include "cpt_path.hpp"
 
 namespace cpt {
@@ -29,49 +31,44 @@ namespace cpt {
 // from a device-wide counter (one aggregated atomic per wave and refill), so every lane of
 // every wave does useful work until the image runs out — no per-pass kernel boundaries and
 // no idle lanes behind a wave's slowest path.  Pixels are handed out in 8x8 tiles so a fresh
-// wave starts coherent.  LDS variant: the BVH (32 B nodes, leaves inline) is staged in LDS
-// once per resident block.
+// wave starts coherent; with the cost schedule the tiles come heaviest first (p.tile_order).
+//
+// PROBE (the cost schedule's pilot, DESIGN.md §Cost schedule): the same passes from the same
+// RNG states, but nothing is written back except each pixel's work (segments + node visits +
+// primitive tests) added to its tile's cost.
 // ======================================================================================
 struct Lane {
     int x, y;
     size_t pix;
+    uint32_t tile;
     Xorwow s;
     v3 sum;
     float passes;
     int left;
 };
 
-__device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int& x, int& ri) {
+__device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int& x, int& ri, uint32_t& tile) {
     const int tiles_x = (p.width + 7) >> 3;
-    const uint32_t tile = id >> 6, k = id & 63;
+    tile = id >> 6;
+    if (p.tile_order) tile = p.tile_order[tile];
+    const uint32_t k = id & 63;
     x = (int)(tile % tiles_x) * 8 + (int)(k & 7);
     ri = (int)(tile / tiles_x) * 8 + (int)(k >> 3);
     return x < p.width && ri < p.n_rows;
 }
 
-#if CPT_LDS && defined(CPT_DEFER_MISS) && CPT_DEFER_MISS
-#error "CPT_DEFER_MISS assumes 256-lane blocks (the LDS-staged variant runs 256 * CPT_WAVES_PER_SIMD)"
-#endif
-#ifndef CPT_DEFER_MISS
-#define CPT_DEFER_MISS 32   // deferred sky fetches run when this many 64ths of the tracing lanes
-                            // hold one (0 = fetch at the miss)
-#endif
+// Deferred sky fetches run when this many 64ths of the tracing lanes hold one.
+constexpr int DEFER_MISS_ROUND = 32;
 
-template <bool STATS, bool AUX, bool LDS>
-__global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVES_PER_SIMD) k_megakernel(const KParams p) {
-    extern __shared__ Node lds_nodes[];
-    if (LDS) {
-        const float4* src = reinterpret_cast<const float4*>(p.nodes);
-        float4* dst = reinterpret_cast<float4*>(lds_nodes);
-        for (int i = threadIdx.x; i < 2 * p.n_nodes; i += blockDim.x) dst[i] = src[i];
-        __syncthreads();
-    }
-    const Node* __restrict__ nodes = LDS ? lds_nodes : p.nodes;
+template <bool STATS, bool AUX, bool PROBE>
+__global__ void __launch_bounds__(256, CPT_WAVES_PER_SIMD) k_megakernel(const KParams p) {
+    constexpr bool COUNT = STATS || PROBE;
     const int lane = threadIdx.x & 63;
     const size_t npix = (size_t)p.n_rows * p.width;
     const uint32_t n_work = (uint32_t)(((p.width + 7) >> 3) * ((p.n_rows + 7) >> 3)) * 64u;
     const uint32_t max_depth = (uint32_t)p.max_depth;
     Counters cnt{};
+    uint32_t work_at_take = 0;   // PROBE: the lane's counters when it took its pixel
 
     Lane L;
     bool busy = false;
@@ -83,15 +80,11 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
     v3 nrm_acc = mk1(0.f), first_normal = mk1(0.f);
     float dep_acc = 0.f, first_depth = 0.f;
 
-    unsigned long long st_refill = 0, st_trace = 0, st_shade = 0;
-#if CPT_DEFER_MISS
     // a lane's pending sky fetch: direction, the pass's radiance and attenuation so far
     __shared__ float pending_q[9 * 256];
     float* const pq = pending_q + threadIdx.x;
     bool pend = false;
-#endif
     for (;;) {
-        const unsigned long long t0 = stamp();
         // ---- refill idle lanes with new pixels (wave-aggregated dequeue) ----------------
         if (!exhausted) {
             const uint64_t need = __ballot(!busy);
@@ -106,7 +99,7 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                     const uint32_t id = base + rank;
                     int x, ri;
-                    if (id < n_work && decode_pixel(p, id, x, ri)) {
+                    if (id < n_work && decode_pixel(p, id, x, ri, L.tile)) {
                         L.x = x;
                         L.y = p.rows[ri];
                         L.pix = (size_t)ri * p.width + x;
@@ -116,12 +109,13 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
                         L.s.v3 = p.rng[3 * npix + L.pix];
                         L.s.v4 = p.rng[4 * npix + L.pix];
                         L.s.d = p.rng[5 * npix + L.pix];
-                        float4 acc = p.accumulate ? p.accum[L.pix] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        float4 acc = (p.accumulate && !PROBE) ? p.accum[L.pix] : make_float4(0.f, 0.f, 0.f, 0.f);
                         L.sum = mk(acc.x, acc.y, acc.z);
                         L.passes = acc.w;
                         L.left = p.spp;
                         first_normal = mk1(0.f);
                         first_depth = 0.f;
+                        if (PROBE) work_at_take = cnt.segments + cnt.nodes + cnt.prims;
                         if (max_depth == 0) {
                             // while (0 < 0) never runs: each pass is RayGen's draws and zero radiance
                             for (; L.left > 0; --L.left) {
@@ -145,59 +139,41 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
             }
         }
         if (!__any(busy)) break;
-        const unsigned long long t1 = stamp();
-        unsigned long long t2 = t1;
         if (busy && L.left > 0) {
             // ---- one path segment: TraceRay + ClosetHit/Miss (path_tracer.cu:141-169) ----
             Hit h;
             int code = -1;
-            if (STATS) cnt.segments++;
-#if CPT_STAMPS == 3
-            if (lowest_active_lane()) cnt.st_seg++;
-#endif
+            if (COUNT) cnt.segments++;
             const RayK rk = make_rayk(ray);
             const bool finite_ray = !(ray.o.x != ray.o.x || ray.o.y != ray.o.y || ray.o.z != ray.o.z ||
                                       ray.d.x != ray.d.x || ray.d.y != ray.d.y || ray.d.z != ray.d.z);
-            bool hit;
-            if (LDS) hit = finite_ray ? trace<STATS, true>(PtrSrc{nodes}, p.n_nodes, rk, h, code, cnt) > 0
-                                      : trace<STATS, false>(PtrSrc{nodes}, p.n_nodes, rk, h, code, cnt) > 0;
-            else hit = trace_segment<STATS>(p, rk, finite_ray, h, code, cnt);
-            t2 = stamp();
+            const bool hit = trace_segment<COUNT>(p, rk, finite_ray, h, code, cnt);
             Shade sh;
             v3 attr_normal;
-#if CPT_STAMPS == 4
-            const unsigned long long s0 = stamp();
-#endif
             if (hit) {
-                if (STATS) cnt.hits++;
+                if (COUNT) cnt.hits++;
                 const Mat m = p.mats[code >> 2];
                 eval_material(m, h.normal, ray.d, L.s, sh);
                 attr_normal = h.normal;
                 ray.o = h.pos;                         // payload.hit_pos = position
-            }
-#if CPT_STAMPS == 4
-            const unsigned long long s1 = stamp();
-            st_refill += s1 - s0;                      // mode 4: hit shading / miss shading / rest
-#endif
-            bool deferred = false;
-            if (!hit) {
-                if (STATS) cnt.misses++;
+            } else {
+                if (COUNT) cnt.misses++;
                 sh.attenuation = mk1(0.f);             // never read: the path ends here
                 sh.bounce = ray.d;
                 attr_normal = -ray.d;
             }
-#if CPT_DEFER_MISS
             // Deferred sky fetches.  A miss ends the pass, and the sky's radiance only feeds
             // the pixel's running sum, so the lane may start its next pass first and add
             // rad + att * sky later, as long as the sums are added in pass order.  Pending
             // fetches run together once enough lanes hold one, instead of in every round
             // where any lane misses; a lane that would end another pass (or its pixel) with
             // one pending forces the round.  No RNG draw depends on the sky.
+            bool deferred = false;
             {
                 const bool ends = !hit || !(depth + 1 < max_depth);
                 const bool need_now = (pend && ends) || (!hit && L.left == 1);
                 const bool flush = __ballot(need_now) != 0 ||
-                                   __popcll(__ballot(pend || !hit)) * 64 >= CPT_DEFER_MISS * __popcll(__ballot(1));
+                                   __popcll(__ballot(pend || !hit)) * 64 >= DEFER_MISS_ROUND * __popcll(__ballot(1));
                 if (flush) {
                     if (pend) {   // older pending fetches first (their pass came first)
                         const v3 pd = mk(pq[0 * 256], pq[1 * 256], pq[2 * 256]);
@@ -217,13 +193,7 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
                     sh.radiance = mk1(0.f);            // placeholder: this pass's sum waits
                 }
             }
-#else
-            if (!hit) sh.radiance = miss_radiance(p, ray.d);
-#endif
             if (!hit) depth = MAX_RECURSION_DEPTH_SET;   // termination sentinel (path_tracer.cu:121)
-#if CPT_STAMPS == 4
-            st_trace += stamp() - s1;
-#endif
             rad = rad + att * sh.radiance;
             att = att * sh.attenuation;
             if (AUX && first) {
@@ -250,63 +220,41 @@ __global__ void __launch_bounds__(LDS ? 256 * CPT_WAVES_PER_SIMD : 256, CPT_WAVE
                 }
             }
         }
-        if (CPT_STAMPS == 4) st_shade += stamp() - t0;
-        if (CPT_STAMPS == 1) {
-            const unsigned long long t3 = stamp();
-            st_refill += t1 - t0;
-            st_trace += t2 - t1;
-            st_shade += t3 - t2;
-        }
         if (busy && L.left == 0) {
-            // ---- pixel finished: write back (path_tracer.cu:172-174) ---------------------
-            p.accum[L.pix] = make_float4(L.sum.x, L.sum.y, L.sum.z, L.passes);
-            if (AUX && p.spp > 0) {
-                p.normal[3 * L.pix + 0] = first_normal.x;
-                p.normal[3 * L.pix + 1] = first_normal.y;
-                p.normal[3 * L.pix + 2] = first_normal.z;
-                p.depth[L.pix] = first_depth;
+            if (PROBE) {
+                // ---- pilot: the pixel's work goes to its tile's cost ----------------------
+                atomicAdd(&p.tile_cost[L.tile], cnt.segments + cnt.nodes + cnt.prims - work_at_take);
+            } else {
+                // ---- pixel finished: write back (path_tracer.cu:172-174) -----------------
+                p.accum[L.pix] = make_float4(L.sum.x, L.sum.y, L.sum.z, L.passes);
+                if (AUX && p.spp > 0) {
+                    p.normal[3 * L.pix + 0] = first_normal.x;
+                    p.normal[3 * L.pix + 1] = first_normal.y;
+                    p.normal[3 * L.pix + 2] = first_normal.z;
+                    p.depth[L.pix] = first_depth;
+                }
+                p.rng[L.pix] = L.s.v0;
+                p.rng[npix + L.pix] = L.s.v1;
+                p.rng[2 * npix + L.pix] = L.s.v2;
+                p.rng[3 * npix + L.pix] = L.s.v3;
+                p.rng[4 * npix + L.pix] = L.s.v4;
+                p.rng[5 * npix + L.pix] = L.s.d;
             }
-            p.rng[L.pix] = L.s.v0;
-            p.rng[npix + L.pix] = L.s.v1;
-            p.rng[2 * npix + L.pix] = L.s.v2;
-            p.rng[3 * npix + L.pix] = L.s.v3;
-            p.rng[4 * npix + L.pix] = L.s.v4;
-            p.rng[5 * npix + L.pix] = L.s.d;
             busy = false;
         }
     }
-#if CPT_STAMPS == 2
-    st_refill = cnt.st_leaf;
-    st_trace = cnt.st_slab;
-    st_shade = cnt.st_iter;
-#elif CPT_STAMPS == 3
-    // wave-level counts: iterations with any lane at a leaf / at an inner node, all walk
-    // iterations, and segment rounds (stats[4] is replaced by the last, misses are not needed)
-    st_refill = wave_sum((uint32_t)cnt.st_leaf);
-    st_trace = wave_sum((uint32_t)cnt.st_slab);
-    st_shade = wave_sum((uint32_t)cnt.st_iter);
-    {
-        const uint64_t ws = wave_sum((uint32_t)cnt.st_seg);
-        if (lane == 0) atomicAdd(&p.stats[4], (unsigned long long)ws);
-    }
-#endif
-    if (CPT_STAMPS && lane == 0) {
-        atomicAdd(&p.stats[5], st_refill);
-        atomicAdd(&p.stats[6], st_trace);
-        atomicAdd(&p.stats[7], st_shade);
-    }
-    if (STATS) {
+    if (STATS && !PROBE) {
         uint64_t a = wave_sum(cnt.segments), b = wave_sum(cnt.nodes), c = wave_sum(cnt.prims);
         uint64_t d = wave_sum(cnt.hits), e = wave_sum(cnt.misses);
+        const uint64_t f = wave_sum(cnt.fallbacks);   // ordered walk: certificate fallbacks
         if (lane == 0) {
             atomicAdd((unsigned long long*)&p.stats[0], (unsigned long long)a);
             atomicAdd((unsigned long long*)&p.stats[1], (unsigned long long)b);
             atomicAdd((unsigned long long*)&p.stats[2], (unsigned long long)c);
             atomicAdd((unsigned long long*)&p.stats[3], (unsigned long long)d);
             atomicAdd((unsigned long long*)&p.stats[4], (unsigned long long)e);
+            if (f) atomicAdd((unsigned long long*)&p.stats[5], (unsigned long long)f);
         }
-        const uint64_t f = wave_sum(cnt.fallbacks);   // ordered walk: certificate fallbacks
-        if (!CPT_STAMPS && lane == 0 && f) atomicAdd((unsigned long long*)&p.stats[5], (unsigned long long)f);
     }
 }
 
@@ -565,37 +513,25 @@ __global__ void k_math_batch(int op, const float* a, const float* b, float* out,
 // ======================================================================================
 // Host-side launchers (called from cpt_capi.cpp).
 // ======================================================================================
-#ifndef CPT_LDS
-#define CPT_LDS 0   // A/B: LDS-staged BVH measured 9% slower than L1/L2 (bank conflicts), see DESIGN.md
-#endif
-// LDS variant: one block per CU holding all of the CU's waves, BVH up to 96 KB in LDS.
-int lds_node_capacity() { return CPT_LDS ? (96 * 1024) / (int)sizeof(Node) : 0; }
-
-template <bool S, bool A, bool L>
+template <bool S, bool A, bool P>
 static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
     static int blocks_per_cu = -1, cus = 0;
-    const int block = L ? 256 * CPT_WAVES_PER_SIMD : 256;
-    const size_t shmem = L ? (size_t)lds_node_capacity() * sizeof(Node) : 0;
+    constexpr int block = 256;
     if (blocks_per_cu < 0) {
         int dev = 0;
         hipError_t e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_megakernel<S, A, L>, block, shmem);
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_megakernel<S, A, P>, block, 0);
         if (e != hipSuccess) return e;
         if (blocks_per_cu < 1) blocks_per_cu = 1;
-        // tuning knob (experiments only): cap the resident 256-lane blocks per CU
-        if (const char* v = getenv("CPT_MK_BLOCKS_PER_CU")) {
-            const int cap = atoi(v);
-            if (cap >= 1 && cap < blocks_per_cu) blocks_per_cu = cap;
-        }
     }
     // persistent grid: every resident slot once; lanes pull pixels from p.work
     const long long tiles = (long long)((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
     long long want = (tiles * 64 + block - 1) / block;
     long long grid = std::min<long long>(want, (long long)blocks_per_cu * cus);
     if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL((k_megakernel<S, A, L>), dim3((unsigned)grid), dim3(block), shmem, stream, p);
+    hipLaunchKernelGGL((k_megakernel<S, A, P>), dim3((unsigned)grid), dim3(block), 0, stream, p);
     return hipGetLastError();
 }
 
@@ -603,19 +539,55 @@ hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t
     if (p.width <= 0 || p.n_rows <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(p.work, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-#if CPT_LDS
-    const bool lds = !p.ordered && p.n_nodes > 0 && p.n_nodes <= lds_node_capacity();
-    if (lds) {
-        if (stats && aux) return launch_mk<true, true, true>(p, stream);
-        if (stats) return launch_mk<true, false, true>(p, stream);
-        if (aux) return launch_mk<false, true, true>(p, stream);
-        return launch_mk<false, false, true>(p, stream);
-    }
-#endif
     if (stats && aux) return launch_mk<true, true, false>(p, stream);
     if (stats) return launch_mk<true, false, false>(p, stream);
     if (aux) return launch_mk<false, true, false>(p, stream);
     return launch_mk<false, false, false>(p, stream);
+}
+
+// ======================================================================================
+// Cost schedule (CPT_SCHEDULE_COST, DESIGN.md §Cost schedule).  A pilot of `passes` passes
+// from the current RNG states (nothing written back) sums each 8x8 tile's work; the tiles are
+// then sorted heaviest first and the render dequeues them in that order (longest processing
+// time first), so the heaviest pixel chains start at once instead of behind the light ones.
+// ======================================================================================
+__global__ void k_iota(uint32_t* v, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = i;
+}
+
+size_t tile_schedule_scratch_bytes(int width, int n_rows) {
+    const int n = ((width + 7) / 8) * ((n_rows + 7) / 8);
+    size_t temp = 0;
+    (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                       (const uint32_t*)nullptr, (uint32_t*)nullptr, n);
+    return 3 * (size_t)n * sizeof(uint32_t) + temp + 256;
+}
+
+hipError_t launch_tile_schedule(const KParams& p0, int passes, void* scratch, size_t scratch_bytes, uint32_t* order,
+                                hipStream_t stream) {
+    const int n = ((p0.width + 7) / 8) * ((p0.n_rows + 7) / 8);
+    if (n <= 0) return hipSuccess;
+    uint32_t* cost = (uint32_t*)scratch;
+    uint32_t* cost_sorted = cost + n;
+    uint32_t* ids = cost_sorted + n;
+    void* temp = (void*)(((uintptr_t)(ids + n) + 255) & ~(uintptr_t)255);
+    size_t temp_bytes = scratch_bytes - ((char*)temp - (char*)scratch);
+    hipError_t e = hipMemsetAsync(cost, 0, (size_t)n * sizeof(uint32_t), stream);
+    if (e == hipSuccess) e = hipMemsetAsync(p0.work, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    KParams p = p0;
+    p.spp = passes;
+    p.tile_cost = cost;
+    p.tile_order = nullptr;
+    p.accumulate = 0;
+    e = launch_mk<false, false, true>(p, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_iota, dim3((n + 255) / 256), dim3(256), 0, stream, ids, (uint32_t)n);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, cost, cost_sorted, ids, order, n, 0, 32,
+                                                        stream);
 }
 
 hipError_t launch_prepare_materials(Mat* mats, const int32_t* tex_of_mat, const TexDesc* texs, int n,

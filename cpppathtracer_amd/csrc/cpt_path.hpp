@@ -273,38 +273,12 @@ __device__ __forceinline__ Hit hit_attributes(const Node& nd, const RayK& ray, f
 // one for one — no stack, no scratch memory.
 // ======================================================================================
 #ifndef CPT_WAVES_PER_SIMD
-#define CPT_WAVES_PER_SIMD 3   // occupancy target of k_megakernel (VGPR budget 168)
+#define CPT_WAVES_PER_SIMD 3   // occupancy target of k_megakernel (launch bounds)
 #endif
-
-#ifndef CPT_STAMPS
-#define CPT_STAMPS 0   // diagnostic builds (never timed): 1 = per-phase s_memtime sums of the
-                       // megakernel (refill / trace / shade), 2 = inside the BVH walk (leaf / slab / rest)
-#endif
-__device__ __forceinline__ unsigned long long stamp() {
-#if CPT_STAMPS
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-#else
-    return 0;
-#endif
-}
 
 struct Counters {
     uint32_t segments, nodes, prims, hits, misses, fallbacks;
-#if CPT_STAMPS >= 2
-    unsigned long long st_leaf, st_slab, st_iter, st_seg;
-#endif
 };
-
-// CPT_STAMPS == 3 (diagnostic): count wave-level events in the lowest active lane, so that a
-// wave_sum over the lanes gives the wave's count.
-__device__ __forceinline__ bool lowest_active_lane() {
-    const uint64_t m = __ballot(1);
-    return (int)(__lane_id()) == __ffsll((unsigned long long)m) - 1;
-}
 
 // Slab test of one internal node (bvh.cu:181-200).  The six plane distances use the exact
 // quotient; if any of them is zero/subnormal the node is redone with the IEEE divide.
@@ -345,14 +319,10 @@ __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, flo
     float t0x = qdiv_raw(nd.a0 - ray.o.x, ray.yx), t1x = qdiv_raw(nd.b0 - ray.o.x, ray.yx);
     float t0y = qdiv_raw(nd.a1 - ray.o.y, ray.yy), t1y = qdiv_raw(nd.b1 - ray.o.y, ray.yy);
     float t0z = qdiv_raw(nd.a2 - ray.o.z, ray.yz), t1z = qdiv_raw(nd.b2 - ray.o.z, ray.yz);
-#if CPT_QDIV
     float mn = __builtin_fminf(__builtin_fminf(__builtin_fminf(__builtin_fabsf(t0x), __builtin_fabsf(t1x)),
                                                __builtin_fminf(__builtin_fabsf(t0y), __builtin_fabsf(t1y))),
                                __builtin_fminf(__builtin_fabsf(t0z), __builtin_fabsf(t1z)));
     if (__builtin_expect(mn < FLT_MIN_NORMAL, 0)) {
-#else
-    {
-#endif
         t0x = (nd.a0 - ray.o.x) / ray.d.x; t1x = (nd.b0 - ray.o.x) / ray.d.x;
         t0y = (nd.a1 - ray.o.y) / ray.d.y; t1y = (nd.b1 - ray.o.y) / ray.d.y;
         t0z = (nd.a2 - ray.o.z) / ray.d.z; t1z = (nd.b2 - ray.o.z) / ray.d.z;
@@ -415,8 +385,7 @@ __device__ __forceinline__ bool slab_reject_octant(const Node& nd, const RayK& r
 // Node fetch.  BufSrc reads through a buffer descriptor over the whole node array (built from
 // kernel arguments, so it is wave-uniform and lives in SGPRs): a 32-bit per-lane byte offset
 // instead of 64-bit address arithmetic, and out-of-range offsets read 0 instead of needing a
-// clamp (the walk never uses a node past its order's end).  PtrSrc is the plain pointer form
-// (LDS-staged variant).
+// clamp (the walk never uses a node past its order's end).
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 
 struct BufSrc {
@@ -431,11 +400,6 @@ struct BufSrc {
         n.b0 = __uint_as_float(b.x); n.b1 = __uint_as_float(b.y); n.b2 = __uint_as_float(b.z); n.code = (int32_t)b.w;
         return n;
     }
-};
-
-struct PtrSrc {
-    const Node* __restrict__ p;
-    __device__ __forceinline__ Node operator()(uint32_t i) const { return p[i]; }
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(const KParams& p) {
@@ -476,21 +440,6 @@ __device__ __forceinline__ void leaf_aabb(const Node& nd, Node& box) {
         box.a0 = box.a1 = box.a2 = box.b0 = box.b1 = box.b2 = 0.f;
     }
 }
-
-#ifndef CPT_PREFETCH
-#define CPT_PREFETCH 0   // load both successors before the node's test (else the chosen one after)
-#endif
-
-
-#ifndef CPT_LEAF_PRETEST
-#define CPT_LEAF_PRETEST 1   // ordered walk: conservative slab test of a leaf's own box before
-                             // its exact test (1 = cylinders, 2 = spheres and cylinders)
-#endif
-
-#ifndef CPT_UNIFIED_LEAF
-#define CPT_UNIFIED_LEAF 1   // ordered walk's leaf rounds: spheres and cylinder sides share one
-                             // quadratic (a wave with both kinds runs the root code once)
-#endif
 
 // Sphere (object.cu:10-35) and cylinder (object.cu:50-112) in one code path for a wave that
 // holds both.  Each lane computes exactly its own type's expressions in the reference's
@@ -536,18 +485,18 @@ __device__ __forceinline__ bool sphere_cyl_test(const Node& nd, const RayK& ray,
     return ret;
 }
 
+// The ordered walk (CONS) pretests a cylinder's own box with the conservative slab before its
+// exact test (PRETEST; the wide walk's parent already tested it), and runs spheres and
+// cylinder sides through one quadratic (sphere_cyl_test).
 template <bool FAST, bool CONS, bool PRETEST = true>
 __device__ __forceinline__ bool ranked_leaf_test(const Node& nd, const RayK& ray, float& tmax, int& kind, int& best_rank) {
     float tm = nd.miss < best_rank ? __int_as_float(__float_as_int(tmax) + 1) : tmax;
-    if (CONS && PRETEST && CPT_LEAF_PRETEST) {
-        const int type = nd.code & 3;
-        if (type == 2 || (CPT_LEAF_PRETEST == 2 && type == 0)) {
-            Node box;
-            leaf_aabb(nd, box);
-            if (slab_reject<FAST, true>(box, ray, walk_limit(tm))) return false;
-        }
+    if (CONS && PRETEST && (nd.code & 3) == 2) {
+        Node box;
+        leaf_aabb(nd, box);
+        if (slab_reject<FAST, true>(box, ray, walk_limit(tm))) return false;
     }
-    if (CONS && CPT_UNIFIED_LEAF && ((nd.code & 1) == 0)) {   // sphere (0) or cylinder (2)
+    if (CONS && ((nd.code & 1) == 0)) {   // sphere (0) or cylinder (2)
         if (!sphere_cyl_test(nd, ray, tm, kind)) return false;
     } else if (!leaf_test(nd, ray, tm, kind)) {
         return false;
@@ -569,50 +518,22 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
     Node nd{};
     if (n_nodes > 0) nd = nodes(0);
     // The successor of node ni is ni + 1 (box hit: its first child; after a leaf) or nd.miss
-    // (box miss).  With CPT_PREFETCH both are loaded before the node's test; by default the
-    // chosen one is loaded after it (the other waves of the SIMD hide the latency).
+    // (box miss); the chosen one is loaded after the node's test (the other waves of the SIMD
+    // hide the latency).
     while (ni < n_nodes) {
-#if CPT_STAMPS == 2
-        const unsigned long long t0 = stamp();
-#endif
         const bool leaf = nd.code >= 0;
-        const int na = ni + 1, nb = leaf ? na : nd.miss;
-#if CPT_PREFETCH
-        const Node pa = nodes(na);   // past the order's end: never used (the loop ends)
-        const Node pb = nodes(nb);
-#endif
         if (STATS) cnt.nodes++;
-#if CPT_STAMPS == 3
-        {
-            const bool any_leaf = __ballot(leaf) != 0, any_inner = __ballot(!leaf) != 0;
-            if (lowest_active_lane()) { cnt.st_iter++; cnt.st_leaf += any_leaf; cnt.st_slab += any_inner; }
-        }
-#endif
         bool take_a = false;
         if (leaf) {
             // IntersectionTest first (bvh.cu:175-180); the leaf's own box test is moot
             if (STATS) cnt.prims++;
             int k;
             if (ranked_leaf_test<FAST, CONS>(nd, ray, tmax, k, best_rank)) { best = ni; kind = k; }
+        } else {
+            take_a = CONS ? !slab_reject_octant(nd, ray, walk_limit(tmax)) : !slab_reject<FAST>(nd, ray, tmax);
         }
-#if CPT_STAMPS == 2
-        const unsigned long long t1 = stamp();
-#endif
-        if (!leaf) take_a = CONS ? !slab_reject_octant(nd, ray, walk_limit(tmax)) : !slab_reject<FAST>(nd, ray, tmax);
-#if CPT_STAMPS == 2
-        const unsigned long long t2 = stamp();
-        cnt.st_leaf += t1 - t0;
-        cnt.st_slab += t2 - t1;
-#endif
-        ni = take_a ? na : nb;
-#if CPT_PREFETCH
-        nd = take_a ? pa : pb;
-#else
+        ni = take_a || leaf ? ni + 1 : nd.miss;
         nd = nodes(ni);
-#endif
-#if CPT_STAMPS == 2
-        cnt.st_iter += stamp() - t0;
-#endif
     }
     if (best < 0) return 0;
     const Node w = nodes(best);
@@ -630,119 +551,22 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
     return 1;
 }
 
-#ifndef CPT_SPEC_LEAF
-#define CPT_SPEC_LEAF 32  // ordered walk: postpone leaf tests and run them wave-wide (0 = off;
-                          // else the share of working lanes, in 64ths, that must be waiting
-                          // on a leaf before the wave runs its leaf round)
-#endif
-
-#ifndef CPT_SPEC_ONLY_STOPPED
-#define CPT_SPEC_ONLY_STOPPED 0
-#endif
-
-// The ordered walk with postponed leaves (Aila & Laine's speculative traversal, on the skip
-// links).  A lane that meets a leaf parks its index and walks on through inner nodes; it
-// stops when it meets a second leaf or the order's end.  Leaf tests then run for every parked
-// lane at once when enough working lanes are stopped, instead of in every iteration where
-// one lane is at a leaf.  Inner nodes are culled with the tmax of the leaves tested so far,
-// which is never below the final one: a superset of the plain walk's tests, so the same
-// closest hit under the rank rule, and the same certificate.
-template <bool STATS, bool FAST, typename SRC>
-__device__ __forceinline__ int trace_spec(const SRC& nodes, int n_nodes, const RayK& ray, Hit& h, int& code_out,
-                                          Counters& cnt) {
-    float tmax = DEFAULT_RAY_TMAX;
-    int best = -1, kind = 0;
-    int best_rank = 0x7fffffff;
-    int ni = 0, parked = -1;
-    float limit = walk_limit(tmax);   // changes only in leaf rounds
-    Node nd{};
-    if (n_nodes > 0) nd = nodes(0);
-    for (;;) {
-#if CPT_STAMPS == 2
-        const unsigned long long t0 = stamp();
-#endif
-        const bool leaf = nd.code >= 0;
-        if (ni < n_nodes && !(leaf && parked >= 0)) {
-            if (STATS) cnt.nodes++;
-            if (leaf) {
-                parked = ni;
-                ni = ni + 1;
-            } else {
-                ni = slab_reject_octant(nd, ray, limit) ? nd.miss : ni + 1;
-            }
-            nd = nodes(ni);
-        }
-        const bool working = parked >= 0 || ni < n_nodes;
-        const bool stopped = parked >= 0 && (ni >= n_nodes || nd.code >= 0);
-        const uint64_t w = __ballot(working);
-        if (!w) break;
-        const bool round = __popcll(__ballot(stopped)) * 64 >= CPT_SPEC_LEAF * __popcll(w);
-#if CPT_STAMPS == 2
-        const unsigned long long t1 = stamp();
-        cnt.st_slab += t1 - t0;   // stepping (and the ballots)
-#endif
-#if CPT_STAMPS == 3
-        // wave-level: walk iterations, leaf rounds, iterations with a lane stepping an inner node
-        if (lowest_active_lane()) {
-            cnt.st_iter++;
-            cnt.st_leaf += round;
-        }
-        {
-            const bool stepping = ni < n_nodes && parked < 0;
-            if (__ballot(stepping) != 0 && lowest_active_lane()) cnt.st_slab++;
-        }
-#endif
-        if (round) {
-            if (CPT_SPEC_ONLY_STOPPED ? stopped : parked >= 0) {
-                if (STATS) cnt.prims++;
-                const Node lf = nodes(parked);
-                int k;
-                if (ranked_leaf_test<FAST, true>(lf, ray, tmax, k, best_rank)) {
-                    best = parked;
-                    kind = k;
-                    limit = walk_limit(tmax);
-                }
-                parked = -1;
-            }
-        }
-#if CPT_STAMPS == 2
-        const unsigned long long t2 = stamp();
-        cnt.st_leaf += t2 - t1;   // leaf round
-        cnt.st_iter += t2 - t0;
-#endif
-    }
-    if (best < 0) return 0;
-    const Node w = nodes(best);
-    Node box;
-    leaf_aabb(w, box);
-    if (slab_reject<FAST>(box, ray, tmax)) return -1;
-    h = hit_attributes(w, ray, tmax, kind);
-    code_out = w.code;
-    return 1;
-}
+// Leaf rounds of the wide walk run when this many 64ths of the wave's working lanes are
+// stopped at a parked leaf.
+constexpr int SPEC_LEAF_ROUND = 32;
 
 // ======================================================================================
-// The ordered walk on the 4-wide walk tree (CPT_WIDE, DESIGN.md §Wide walk).  One
-// iteration loads a 128-B node (cpt_capi.cpp linearise_wide) and tests its four children's
-// boxes with the conservative octant-form slab; the nearest hit child is taken next, the
-// other hits go onto a per-lane stack in LDS (far ones first).  Leaves are parked and tested
-// in wave-wide rounds as in trace_spec; a leaf is parked without a node iteration.  The
-// boxes tested are the binary tree's, so the same superset argument holds: every primitive
-// the plain walk tests, whose box passes the conservative test, is tested here too, under a
-// limit that is never below the final tmax; the rank rule and the certificate are unchanged.
+// The ordered walk on the 4-wide walk tree (DESIGN.md §Wide walk).  One iteration loads a
+// 128-B node (cpt_capi.cpp linearise_wide; 112 B of it are read) and tests its four
+// children's boxes with the conservative octant-form slab; the nearest hit child is taken
+// next, the other hits go onto a per-lane stack in LDS (far ones first).  Leaves are parked
+// and tested in wave-wide rounds: a lane that meets a leaf parks it and walks on; it stops at
+// a second leaf or when its stack is empty, and once enough lanes are stopped every lane
+// with a parked leaf tests it (Aila & Laine's speculative traversal).  The boxes tested are
+// the binary walk tree's, so the superset argument holds: every primitive the plain walk
+// tests, whose box passes the conservative test, is tested here too, under a limit that is
+// never below the final tmax; the rank rule and the certificate are unchanged.
 // ======================================================================================
-#ifndef CPT_WIDE_CULL
-#define CPT_WIDE_CULL 0    // keep each stack entry's entry distance; pops beyond the limit are dropped
-#endif
-#ifndef CPT_WIDE_PLATFORMS_FIRST
-#define CPT_WIDE_PLATFORMS_FIRST 1   // test the unbounded leaves before the wide walk, wave-wide
-#endif
-#ifndef CPT_WIDE_SLOTS
-#define CPT_WIDE_SLOTS 1   // leaves a lane may park before it stops (1 or 2)
-#endif
-#ifndef CPT_WIDE_PARK2
-#define CPT_WIDE_PARK2 1   // park the nearest hit leaf in the node's own iteration (+2% A/B)
-#endif
 constexpr int WIDE_LANES = 256;   // block size of every kernel that walks (stack stride)
 
 struct WideNode {
@@ -765,7 +589,7 @@ __device__ __forceinline__ WideNode load_wide(__amdgpu_buffer_rsrc_t rsrc, uint3
 }
 
 // Hit mask of the four children: slab_reject_octant for each, two children per packed op.
-__device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], const RayK& ray, float limit, f2v& los) {
+__device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], const RayK& ray, float limit) {
     const f2v ox = {ray.o.x, ray.o.x}, oy = {ray.o.y, ray.o.y}, oz = {ray.o.z, ray.o.z};
     const f2v ix = {ray.ix, ray.ix}, iy = {ray.iy, ray.iy}, iz = {ray.iz, ray.iz};
     const f2v bx = {ray.bx, ray.bx}, by = {ray.by, ray.by}, bz = {ray.bz, ray.bz};
@@ -780,72 +604,42 @@ __device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], co
     const float m1 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo1) + __builtin_fabsf(hi1), 2.0f * WALK_MARGIN_ABS);
     const bool rej0 = lo0 - hi0 > m0 || lo0 > limit || hi0 < ray.t3;
     const bool rej1 = lo1 - hi1 > m1 || lo1 > limit || hi1 < ray.t3;
-    los = {lo0, lo1};
     return (rej0 ? 0u : 1u) | (rej1 ? 0u : 2u);
 }
 
+// Child refs (node words 24..27, cpt_capi.cpp linearise_wide): >= 0 a wide node of the same
+// octant, -1 none, <= -2 a leaf as ~k with k its position in the octant-0 binary order
+// (absolute Node index n_nodes + k).  The host keeps both ranges within 15 bits, so the LDS
+// stack holds 16-bit entries (16 KB per 256-lane block).
 template <bool STATS>
 __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc_t rsrc, int oct, const RayK& ray,
                                           Hit& h, int& code_out, Counters& cnt) {
-    __shared__ int wstack[CPT_WSTACK * WIDE_LANES];
-    int* const stk = wstack + threadIdx.x;
-#if CPT_WIDE_CULL
-    __shared__ float wstack_lo[CPT_WSTACK * WIDE_LANES];
-    float* const stk_lo = wstack_lo + threadIdx.x;
-#else
-    float* const stk_lo = nullptr;
-#endif
+    __shared__ int16_t wstack[CPT_WSTACK * WIDE_LANES];
+    int16_t* const stk = wstack + threadIdx.x;
     const BufSrc nodes{rsrc, 0u};   // leaves by absolute Node index
-    constexpr int NONE = -1;        // refs: >= 0 wide node, -1 none, <= -2 leaf ~index
+    constexpr int NONE = -1;
     float tmax = DEFAULT_RAY_TMAX;
     int best = -1, kind = 0;
     int best_rank = 0x7fffffff;
-    float limit = walk_limit(tmax);
-    // start: the platforms (reference-rank order, as at the head of the binary orders), then
-    // the tree's root
-    int sp = 0, cur = 0;
-    if (CPT_WIDE_PLATFORMS_FIRST) {
-        // the platforms (every ray tests them) run first, by the whole wave at once, so the
-        // walk starts with their tmax; same rank rule, so the order does not matter
-        for (int k = 0; k < p.n_unb; ++k) {
-            if (STATS) cnt.prims++;
-            const Node pl = nodes(p.n_nodes + k);
-            int kk;
-            if (ranked_leaf_test<true, true, false>(pl, ray, tmax, kk, best_rank)) {
-                best = p.n_nodes + k;
-                kind = kk;
-            }
+    // the platforms (every ray tests them) run first, by the whole wave at once, so the walk
+    // starts with their tmax; same rank rule, so the order does not matter
+    for (int k = 0; k < p.n_unb; ++k) {
+        if (STATS) cnt.prims++;
+        const Node pl = nodes(p.n_nodes + k);
+        int kk;
+        if (ranked_leaf_test<true, true, false>(pl, ray, tmax, kk, best_rank)) {
+            best = p.n_nodes + k;
+            kind = kk;
         }
-        limit = walk_limit(tmax);
-    } else if (p.n_unb > 0) {
-        for (int k = p.n_unb; k >= 1; --k) {   // the root, then platforms n_unb-1 .. 1
-            stk[sp * WIDE_LANES] = k == p.n_unb ? 0 : ~(p.n_nodes + k);
-            if (CPT_WIDE_CULL) stk_lo[sp * WIDE_LANES] = -3.0e38f;
-            sp++;
-        }
-        cur = ~p.n_nodes;
     }
+    float limit = walk_limit(tmax);   // changes only in leaf rounds
     const uint32_t wbase = (uint32_t)(p.n_nodes + 8 * p.n_walk + 4 * oct * p.n_wide) * (uint32_t)sizeof(Node);
-    int parked = -1, parked2 = -1;   // parked leaves (the second slot with CPT_WIDE_SLOTS == 2)
-    // next stack entry (NONE when empty); with CPT_WIDE_CULL entries whose box starts beyond the
-    // current limit are dropped (the limit only shrinks, so they can no longer hold a winner)
-    auto pop = [&]() -> int {
-        while (sp > 0) {
-            --sp;
-            const int e = stk[sp * WIDE_LANES];
-            if (!CPT_WIDE_CULL || stk_lo[sp * WIDE_LANES] <= limit) return e;
-        }
-        return NONE;
-    };
+    int sp = 0, cur = 0;   // the root
+    int parked = -1;       // absolute Node index of the parked leaf
+    auto pop = [&]() -> int { return sp > 0 ? (int)stk[--sp * WIDE_LANES] : NONE; };
     for (;;) {
-#if CPT_STAMPS == 2
-        const unsigned long long t0 = stamp();
-#endif
         if (cur <= -2 && parked < 0) {
-            parked = ~cur;
-            cur = pop();
-        } else if (CPT_WIDE_SLOTS == 2 && cur <= -2 && parked2 < 0) {
-            parked2 = ~cur;
+            parked = p.n_nodes + ~cur;
             cur = pop();
         }
         if (cur >= 0) {
@@ -853,72 +647,38 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
             const WideNode n = load_wide(rsrc, wbase + (uint32_t)cur * 128u);
             const f2v e01[3] = {n.e[0][0], n.e[1][0], n.e[2][0]}, x01[3] = {n.x[0][0], n.x[1][0], n.x[2][0]};
             const f2v e23[3] = {n.e[0][1], n.e[1][1], n.e[2][1]}, x23[3] = {n.x[0][1], n.x[1][1], n.x[2][1]};
-            f2v lo01, lo23;
-            const uint32_t m = wide_pair(e01, x01, ray, limit, lo01) | (wide_pair(e23, x23, ray, limit, lo23) << 2);
-            const float lo[4] = {lo01.x, lo01.y, lo23.x, lo23.y};
+            const uint32_t m = wide_pair(e01, x01, ray, limit) | (wide_pair(e23, x23, ray, limit) << 2);
             int next = NONE;
-            float next_lo = 0.f;
 #pragma unroll
             for (int k = 3; k >= 0; --k) {
                 if ((m >> k) & 1u) {
-                    if (next != NONE) {
-                        stk[sp * WIDE_LANES] = next;
-                        if (CPT_WIDE_CULL) stk_lo[sp * WIDE_LANES] = next_lo;
-                        sp++;
-                    }
+                    if (next != NONE) stk[sp++ * WIDE_LANES] = (int16_t)next;
                     next = n.ref[k];
-                    next_lo = lo[k];
                 }
             }
             if (next == NONE) next = pop();
             cur = next;
-            if (CPT_WIDE_PARK2 && cur <= -2 && parked < 0) {   // park the nearest leaf at once
-                parked = ~cur;
-                cur = pop();
-            } else if (CPT_WIDE_PARK2 && CPT_WIDE_SLOTS == 2 && cur <= -2 && parked2 < 0) {
-                parked2 = ~cur;
+            if (cur <= -2 && parked < 0) {   // park the nearest leaf at once
+                parked = p.n_nodes + ~cur;
                 cur = pop();
             }
         }
         const bool working = parked >= 0 || cur != NONE;
-        const bool stopped = parked >= 0 && (cur == NONE || (cur <= -2 && (CPT_WIDE_SLOTS == 1 || parked2 >= 0)));
+        const bool stopped = parked >= 0 && (cur == NONE || cur <= -2);
         const uint64_t w = __ballot(working);
         if (!w) break;
-        const bool round = __popcll(__ballot(stopped)) * 64 >= CPT_SPEC_LEAF * __popcll(w);
-#if CPT_STAMPS == 2
-        const unsigned long long t1 = stamp();
-        cnt.st_slab += t1 - t0;
-#elif CPT_STAMPS == 3
-        if (lowest_active_lane()) {
-            cnt.st_iter++;
-            cnt.st_leaf += round;
-        }
-#endif
-        if (round) {
-#pragma nounroll
-            for (int slot = 0; slot < CPT_WIDE_SLOTS; ++slot) {
-                const int leaf = slot == 0 ? parked : parked2;
-                if (leaf >= 0) {
-                    if (STATS) cnt.prims++;
-                    const Node lf = nodes(leaf);
-                    int k;
-                    // no pretest: the parent's slab test already tested this leaf's own box
-                    // (measured: +2% without the repeat at the smaller limit)
-                    if (ranked_leaf_test<true, true, false>(lf, ray, tmax, k, best_rank)) {
-                        best = leaf;
-                        kind = k;
-                        limit = walk_limit(tmax);
-                    }
-                }
+        if (__popcll(__ballot(stopped)) * 64 >= SPEC_LEAF_ROUND * __popcll(w) && parked >= 0) {
+            if (STATS) cnt.prims++;
+            const Node lf = nodes(parked);
+            int k;
+            // no pretest: the parent's slab test already tested this leaf's own box
+            if (ranked_leaf_test<true, true, false>(lf, ray, tmax, k, best_rank)) {
+                best = parked;
+                kind = k;
+                limit = walk_limit(tmax);
             }
             parked = -1;
-            parked2 = -1;
         }
-#if CPT_STAMPS == 2
-        const unsigned long long t2 = stamp();
-        cnt.st_leaf += t2 - t1;
-        cnt.st_iter += t2 - t0;
-#endif
     }
     if (best < 0) return 0;
     const Node wn = nodes(best);
@@ -931,20 +691,21 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
 }
 
 // TraceRay for one segment: the reference order, or the ordered walk with its certificate
-// and the reference-order fallback (CPT_TRAVERSAL_ORDERED).
+// and the reference-order fallback (CPT_TRAVERSAL_ORDERED): the 4-wide walk with parked
+// leaves (ordered == 1 and a wide tree), else the binary octant orders testing each leaf
+// where the walk meets it.
 template <bool STATS>
 __device__ __forceinline__ bool trace_segment(const KParams& p, const RayK& rk, bool finite, Hit& h, int& code,
                                               Counters& cnt) {
     const __amdgpu_buffer_rsrc_t rsrc = node_rsrc(p);
     if (p.ordered && __builtin_expect(finite, 1)) {
         int n, r;
-        if (p.ordered == 1 && p.n_wide > 0) {   // n_wide = 0 unless CPT_WIDE
+        if (p.ordered == 1 && p.n_wide > 0) {
             const int oct = (rk.d.x < 0.f ? 1 : 0) | (rk.d.y < 0.f ? 2 : 0) | (rk.d.z < 0.f ? 4 : 0);
             r = trace_wide<STATS>(p, rsrc, oct, rk, h, code, cnt);
         } else {
             const BufSrc order{rsrc, walk_order(p, rk.d, n) * (uint32_t)sizeof(Node)};
-            r = CPT_SPEC_LEAF && p.ordered == 1 ? trace_spec<STATS, true>(order, n, rk, h, code, cnt)
-                                                : trace<STATS, true, true>(order, n, rk, h, code, cnt);
+            r = trace<STATS, true, true>(order, n, rk, h, code, cnt);
         }
         if (__builtin_expect(r >= 0, 1)) return r > 0;
         if (STATS) cnt.fallbacks++;

@@ -9,8 +9,8 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import (CPT_PATH_WAVEFRONT, CPT_TRAVERSAL_ORDERED, CPT_TRAVERSAL_PLAIN_LEAVES, CPT_RENDER_ACCUMULATE, CPT_RENDER_AUX, CPT_RENDER_STATS, CPT_RENDER_SYNC,
-                   CptError, check)
+from ._lib import (CPT_PATH_WAVEFRONT, CPT_RENDER_ACCUMULATE, CPT_RENDER_AUX, CPT_RENDER_STATS, CPT_RENDER_SYNC,
+                   CPT_SCHEDULE_COST, CPT_TRAVERSAL_ORDERED, CPT_TRAVERSAL_PLAIN_LEAVES, CptError, check)
 
 PATHS = ("megakernel", "wavefront")
 from .types import CAMERA_DTYPE, OBJECT_DTYPE
@@ -119,15 +119,20 @@ class Renderer:
 
     # -- render ----------------------------------------------------------------------
     def render(self, cam, spp, max_depth, accumulate=False, aux=False, stats=False, sync=False, flags=0,
-               path="megakernel", ordered=False):
+               path="megakernel", ordered=False, schedule="tiles"):
         """path: "megakernel" (per-lane regeneration, state in VGPRs) or "wavefront" (SoA state in
         HBM, extend/shade kernels with ballot compaction).  Both give identical results.
         ordered: near-first BVH walk per direction octant (CPT_TRAVERSAL_ORDERED); same closest
         hits as the reference order up to box/primitive rounding (DESIGN.md §Ordered walk).
         ordered="plain": the same walk testing each leaf where it meets it (per-ray node/prim
-        counts, CPT_TRAVERSAL_PLAIN_LEAVES) instead of parking leaves for wave-wide rounds."""
+        counts, CPT_TRAVERSAL_PLAIN_LEAVES) instead of parking leaves for wave-wide rounds.
+        schedule: "tiles" (8x8 tiles dequeued in row-major order) or "cost" (CPT_SCHEDULE_COST: a
+        short pilot render measures each tile's work and the megakernel dequeues the tiles
+        heaviest first; same results, DESIGN.md §Cost schedule)."""
         if path not in PATHS:
             raise ValueError(f"path must be one of {PATHS}")
+        if schedule not in ("tiles", "cost"):
+            raise ValueError("schedule must be 'tiles' or 'cost'")
         c = np.ascontiguousarray(np.array(cam, dtype=CAMERA_DTYPE))
         f = flags | (CPT_PATH_WAVEFRONT if path == "wavefront" else 0)
         f |= CPT_TRAVERSAL_ORDERED if ordered else 0
@@ -136,6 +141,7 @@ class Renderer:
         f |= CPT_RENDER_AUX if aux else 0
         f |= CPT_RENDER_STATS if stats else 0
         f |= CPT_RENDER_SYNC if sync else 0
+        f |= CPT_SCHEDULE_COST if schedule == "cost" else 0
         self._check(self._L.cpt_render(self._ctx, _p(c), spp, max_depth, f))
 
     def synchronize(self):

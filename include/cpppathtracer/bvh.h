@@ -21,13 +21,18 @@ public:
     static void UpdateObject(Object* obj);
     static void ReleaseBVH();
 
-    // Build-time snapshot shared with PathTracer (by-value copies in AddObject order).
-    static const std::vector<cpt_object>& Snapshot();
+    // ---- additions: the state a renderer uploads ---------------------------------------
     // Bumped by BuildBVH (and ReleaseBVH); renderers rebuild when it changes.
     static uint64_t BuildId();
-    // Snapshot indices UpdateObject touched since the last BuildBVH, in call order;
-    // renderers refit them (cpt_update_object) instead of rebuilding, like bvh.cu:144-157.
-    static std::vector<int> UpdateLog();
+    // Bumped by every BuildBVH / UpdateObject / ReleaseBVH: a renderer whose copy is at this
+    // revision has nothing to do.
+    static uint64_t Revision();
+    // One consistent copy, taken under one lock: the build id and revision, the objects as
+    // BuildBVH copied them (`built`, the topology the reference builds; filled only when
+    // non-null), their current values and a per-object count of UpdateObject calls since the
+    // build.  A renderer refits the objects whose count moved (cpt_update_objects).
+    static void GetState(uint64_t& build_id, uint64_t& revision, std::vector<cpt_object>* built,
+                         std::vector<cpt_object>& current, std::vector<uint64_t>& updates);
     // Index of `obj` in the snapshot (-1 if unknown).
     static int IndexOf(const Object* obj);
 };

@@ -65,6 +65,7 @@ public:
 private:
     bool EnsureContext();
     bool SyncScene();
+    bool BindTextures(const std::vector<cpt_object>& objs);
     bool EnsureFrame(const MotionalCamera& cam);
     bool RenderPass(MotionalCamera& cam, int spp, bool accumulate);
     void PipelineLoop();
@@ -76,8 +77,11 @@ private:
     uint max_recursion_depth_ = 8;
     bool ordered_walk_ = true;
     int width_ = 0, height_ = 0;
+    bool scene_synced_ = false;
     uint64_t scene_build_ = 0;      // SceneBVH::BuildId() uploaded to the context
-    size_t updates_applied_ = 0;    // prefix of SceneBVH::UpdateLog() refitted on the context
+    uint64_t scene_rev_ = 0;        // SceneBVH::Revision() the context is at
+    std::vector<uint64_t> updates_seen_;       // per-object UpdateObject counts refit so far
+    std::vector<uint64_t> bound_textures_;     // material texture handles bound on the context
     bool rng_ready_ = false;
     PocaTexture env_ = 0;
     bool env_uploaded_ = false;

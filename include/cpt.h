@@ -15,7 +15,7 @@
  *   cpt_set_scene                   SceneBVH::AddObject + BuildBVH + BuildBVHInGpu
  *                                   (bvh.cu:22-29, 116-120, 97-114), reached from
  *                                   PathTracer::AddObject / InitPipeline (path_tracer.cu:29-34, 308-314).
- *   cpt_update_object               SceneBVH::UpdateObject (bvh.cu:144-157).
+ *   cpt_update_object(s)            SceneBVH::UpdateObject (bvh.cu:144-157).
  *   cpt_set_env_texture             PocaTextureUtils::AddTexByFile (textures.cu:14-62) +
  *                                   the sky load in InitBuffers (path_tracer.cu:47).
  *   cpt_bind_texture                AddTexByFile for a material texture: the handle the app
@@ -144,6 +144,13 @@ typedef struct cpt_ctx cpt_ctx;
  * leaves); the closest hits are the same, but the node/prim counts then depend on which rays
  * share a wave.  This flag makes them a per-ray property (the oracle's diagnostic walk). */
 #define CPT_TRAVERSAL_PLAIN_LEAVES 0x400u
+/* Megakernel pixel schedule: a short pilot render (1..4 passes from the current RNG states,
+ * nothing written back) measures each 8x8 tile's work, and the render then dequeues the tiles
+ * heaviest first (longest processing time first).  Results are identical to the row-major
+ * tile order (a pixel's stream depends only on (seed, x, y)); the heaviest pixel chains start
+ * at once, which shortens the tail when the image has few pixels per lane (row tiles on many
+ * GPUs, DESIGN.md §Cost schedule).  Ignored by CPT_PATH_WAVEFRONT. */
+#define CPT_SCHEDULE_COST 0x800u
 
 int cpt_abi_version(void);
 const char* cpt_status_string(int status);
@@ -165,6 +172,10 @@ int cpt_camera_get_copy(cpt_camera* cam);
 int cpt_set_scene(cpt_ctx* ctx, const cpt_object* objs, int n_objs);
 /* Replace object `index` (AddObject order) and refit the ancestors' boxes. */
 int cpt_update_object(cpt_ctx* ctx, int index, const cpt_object* obj);
+/* The same for n objects at once (one refit pass, one walk-order rebuild, one upload); the
+ * refit is a function of the leaves only, so the result equals n single updates in any order
+ * (SceneBVH::UpdateObject, bvh.cu:122-157). */
+int cpt_update_objects(cpt_ctx* ctx, int n, const int* indices, const cpt_object* objs);
 /* Exports the BVH in the reference's node order (Divide creation order): per node
  * boxes[6] = {min xyz, max xyz}, links[4] = {is_object, left, right, object index}. */
 int cpt_scene_bvh_export(cpt_ctx* ctx, float* boxes, int32_t* links, int capacity, int* n_nodes);

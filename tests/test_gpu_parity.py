@@ -86,9 +86,11 @@ def _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, rows=None, seed=1234
     gpu.set_frame(W, H, rows)
     gpu.init_rng(seed)
     gpu.reset_stats()
-    gpu.render(cam, spp, depth, aux=aux, stats=True, sync=True, **_kw(path))
-    g_acc, g_rng, g_st = gpu.read_accum(), gpu.read_rng(), gpu.stats()
-    if _kw(path)["ordered"]:
+    stats = not _timed(path)
+    gpu.render(cam, spp, depth, aux=aux, stats=stats, sync=True, **_kw(path))
+    g_acc, g_rng = gpu.read_accum(), gpu.read_rng()
+    g_st = gpu.stats() if stats else None
+    if stats and _kw(path)["ordered"]:
         g_st["fallbacks"] = gpu.raw_counters()[5]
     g_aux = gpu.read_aux() if aux else None
     rng = oracle_mod.init_rng(seed, W, rows, threads=8)
@@ -111,8 +113,18 @@ def _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, rows=None, seed=1234
 
 
 def _kw(path):
+    path, _, timed = path.partition("+")
     base, _, mode = path.partition(":")
-    return dict(path=base, ordered={"": False, "ordered": True, "plain": "plain"}[mode])
+    kw = dict(path=base, ordered={"": False, "ordered": True, "plain": "plain"}[mode])
+    if timed:
+        kw["schedule"] = "cost" if base == "megakernel" else "tiles"
+    return kw
+
+
+def _timed(path):
+    """"<path>+timed": the instantiation bench.py times — no STATS counters, and for the
+    megakernel the cost schedule (pilot pass + heaviest-tiles-first order)."""
+    return path.endswith("+timed")
 
 
 CASES = [
@@ -132,10 +144,12 @@ CASES = [
 # of segments whose winner certificate failed (reference-walk fallback).  The default
 # ordered walk runs on 4-wide nodes and parks leaves for wave-wide rounds.
 PATHS = ["megakernel", "wavefront", "megakernel:ordered", "wavefront:ordered", "megakernel:plain",
-         "wavefront:plain"]
+         "wavefront:plain", "megakernel+timed", "megakernel:ordered+timed", "wavefront:ordered+timed"]
 
 
 def _check_stats(gs, os_, path):
+    if gs is None:   # "+timed": images and RNG states only
+        return
     if path.endswith(":plain"):
         for k in ("segments", "hits", "misses"):
             assert gs[k] == os_[k], k
@@ -223,13 +237,13 @@ def test_empty_scene_and_no_env(gpu, oracle_mod, sky, path):
     (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, empty, 32, 16, 2, 8, path=path)
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
     np.testing.assert_array_equal(gr, orng)
-    assert gs["hits"] == 0
+    assert gs is None or gs["hits"] == 0
     _check_stats(gs, os_, path)
     (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, scenes.scene_s3(), 32, 16, 2, 8, env=False)
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
 
 
-@pytest.mark.parametrize("path", ["megakernel", "megakernel:ordered", "megakernel:plain"])
+@pytest.mark.parametrize("path", ["megakernel", "megakernel:ordered", "megakernel:plain", "megakernel:ordered+timed"])
 def test_single_object_and_cylinders(gpu, oracle_mod, sky, path):
     objs = scenes.scene_s1000(n=3)
     for sl in (slice(0, 1), slice(1, 2), slice(0, 4)):
@@ -276,7 +290,8 @@ def test_invalid_arguments(gpu):
         gpu.set_frame(16, 16, [16])
 
 
-@pytest.mark.parametrize("path", ["megakernel", "wavefront", "megakernel:ordered", "megakernel:plain"])
+@pytest.mark.parametrize("path", ["megakernel", "wavefront", "megakernel:ordered", "megakernel:plain",
+                                  "megakernel:ordered+timed"])
 def test_update_object_refit(gpu, oracle_mod, sky, path):
     """SceneBVH::UpdateObject (bvh.cu:122-157): the leaf takes the new object, its ancestors'
     boxes are refit and the topology is kept.  Moves a sphere far out (boxes grow), shrinks a
@@ -306,9 +321,11 @@ def test_update_object_refit(gpu, oracle_mod, sky, path):
     gpu.set_frame(W, H)
     gpu.init_rng(11)
     gpu.reset_stats()
-    gpu.render(cam, spp, depth, stats=True, sync=True, **_kw(path))
-    ga, gs = gpu.read_accum(), gpu.stats()
-    if _kw(path)["ordered"]:
+    stats = not _timed(path)
+    gpu.render(cam, spp, depth, stats=stats, sync=True, **_kw(path))
+    ga = gpu.read_accum()
+    gs = gpu.stats() if stats else None
+    if stats and _kw(path)["ordered"]:
         gs["fallbacks"] = gpu.raw_counters()[5]
     rows = np.arange(H, dtype=np.int32)
     rng = oracle_mod.init_rng(11, W, rows, threads=8)
@@ -327,7 +344,8 @@ def test_update_object_refit(gpu, oracle_mod, sky, path):
     _check_stats(gs, os_, path)
 
 
-@pytest.mark.parametrize("path", ["megakernel:ordered", "wavefront:ordered", "megakernel:plain"])
+@pytest.mark.parametrize("path", ["megakernel:ordered", "wavefront:ordered", "megakernel:plain",
+                                  "megakernel:ordered+timed"])
 def test_ordered_walk_platform_only_and_multiple_platforms(gpu, oracle_mod, sky, path):
     """Walk-tree edge cases: a scene that is only a platform (no tree left after splicing),
     and several platforms (floor, a ceiling plane, a duplicate floor) mixed with primitives."""
@@ -370,7 +388,7 @@ def test_wide_walk_structure_and_deep_tree_fallback(gpu, oracle_mod, sky):
     objs = _chain_scene()
     gpu.set_scene(objs)
     assert gpu.walk_info()["n_wide"] == 0
-    for path in ("megakernel:ordered", "megakernel"):
+    for path in ("megakernel:ordered", "megakernel", "megakernel:ordered+timed"):
         (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, objs, 48, 32, 2, 8, path=path)
         np.testing.assert_array_equal(gr, orng)
         np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))

@@ -2,7 +2,7 @@
 # A/B the kernel variants built under build/ab/ (CPT_LIB_PATH picks the library): each
 # variant first passes the bit-exact render parity subset, then runs the bench.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-args="${AB_ARGS:---spp 32 --steps 2 --warmup 1 --no-cpu-baseline}"
+args="${AB_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-hbm-probe --no-count}"
 for lib in cpppathtracer_amd/libcpt.so build/ab/*.so; do
     echo "### $lib"
     if [ -z "${AB_NOTEST:-}" ]; then
@@ -14,5 +14,5 @@ for lib in cpppathtracer_amd/libcpt.so build/ab/*.so; do
     CPT_LIB_PATH=$PWD/$lib timeout -k 10 300 python bench.py $args > /tmp/ab_out.txt 2>&1
     rc=$?
     [ $rc -eq 0 ] || { echo "bench rc=$rc"; tail -n 5 /tmp/ab_out.txt; exit $rc; }
-    tail -n 1 /tmp/ab_out.txt | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], 'Mpaths/s', d['roofline']['kernel_avg_ms'], 'ms', d['roofline']['frac'], d['roofline'].get('walk_info'), d['roofline'].get('walk_counts'))"
+    tail -n 1 /tmp/ab_out.txt | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], 'Mpaths/s', d['ms_per_step'], 'ms/step', d['config']['workload'], d['config']['schedule'])"
 done

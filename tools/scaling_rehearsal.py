@@ -1,7 +1,7 @@
 """1-GPU rehearsal of the row-tiled strong scaling: renders rank 0's rows of
 an N-way partition (tiling.partition_rows) and reports the projected efficiency
 t(1) / (N * t(N, rank 0)).  The real N-GPU run adds one all-gather of the tiles.
-    python tools/scaling_rehearsal.py [--config c4] [--spp 256] [--block 16] [--ns 1,2,4,8]"""
+    python tools/scaling_rehearsal.py [--config c4] [--spp 1024] [--block 8] [--ns 1,2,4,8] [--schedule cost]"""
 import argparse
 import json
 import os
@@ -14,10 +14,11 @@ sys.path.insert(0, REPO)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c4")
-    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--schedule", default="cost", choices=["cost", "tiles"])
     ap.add_argument("--block", type=int, default=None)
     ap.add_argument("--ns", default="1,2,4,8")
-    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--reps", type=int, default=1)
     a = ap.parse_args()
     import torch
     from cpppathtracer_amd import Renderer, camera_get_copy, scenes, texture_io, tiling
@@ -43,7 +44,7 @@ def main():
                     r.init_rng(1234)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(stream)
-                    r.render(cam, a.spp, depth, ordered=True)
+                    r.render(cam, a.spp, depth, ordered=True, schedule=a.schedule)
                     e1.record(stream)
                     torch.cuda.synchronize()
                     ms = e0.elapsed_time(e1)
@@ -54,7 +55,8 @@ def main():
     t1 = res[min(res)]["max_rank_ms"]
     for n, v in res.items():
         v["projected_efficiency"] = round(t1 / (n * v["max_rank_ms"]), 4)
-    print(json.dumps({"config": a.config, "spp": a.spp, "block_rows": block, "results": res}))
+    print(json.dumps({"config": a.config, "spp": a.spp, "block_rows": block, "schedule": a.schedule, "results": res}),
+          flush=True)
 
 
 if __name__ == "__main__":
