@@ -1,9 +1,12 @@
 // headless_render.cpp — the reference app's scene setup (cppSrc/video_renderer.cpp:32-120)
 // written against the drop-in C++ API, with the Win32 window replaced by file output.
 //
-//   cpt_headless [--scene s3|s4] [--width W] [--height H] [--spp N] [--depth D] [--seed S]
+//   cpt_headless [--scene s3|s4|s1000] [--width W] [--height H] [--spp N] [--depth D] [--seed S]
 //                [--out radiance.bin] [--dispatch K --bgra frame.bin] [--pfm image.pfm]
-//                [--texture file.ppm|file.cptex]
+//                [--texture file.ppm|file.cptex] [--dump-scene objects.bin]
+//
+// --dump-scene writes the objects as SceneBVH::BuildBVH copied them (cpt_object records, the
+// C-ABI layout) and exits without rendering (no GPU needed).
 //
 // --texture makes the floor, the Glass and the Metal sphere of s4 textured materials
 // (Material::have_tex_/tex_, material.h:21-25) sampling that file (AddTexByFile defaults).
@@ -46,6 +49,71 @@ Material make_material(MaterialType::Enum t, float3 kd, float ior = 0.f, float s
     return m;
 }
 
+Object* make_object(PrimitiveType::Enum t, const Material& m, float3 c, float r, float h) {
+    Object* o = make_sphere(m, c, r);
+    o->type_ = t;
+    o->height_ = h;
+    return o;
+}
+
+// MSVC rand() (RAND_MAX 32767) and the reference's random() (ray_tracing_math.hpp:30-37),
+// seeded with a constant instead of time(0) so every run builds the same scene.
+struct MsvcRand {
+    uint32_t x;
+    int rand() {
+        x = x * 214013u + 2531011u;
+        return (int)((x >> 16) & 0x7FFF);
+    }
+    float random() { return static_cast<float>(rand()) / static_cast<float>(32767); }
+    float3 random3() {
+        float a = random(), b = random(), c = random();
+        return make_float3(a, b, c);
+    }
+};
+
+// S1000: the floor + n random spheres / cylinders with 20 random materials, the reference
+// scene script's distributions (video_renderer.cpp:41-117), identical to scenes.scene_s1000.
+void add_s1000(PathTracer& tracer, uint32_t seed = 20250124u, int n = 1000) {
+    MsvcRand rng{seed};
+    std::vector<Material> mats;
+    mats.push_back(make_material(MaterialType::Diffuse, make_float3(0.95f, 0.95f, 0.95f)));
+    for (int i = 1; i < 20; ++i) {
+        const float3 kd = rng.random3();
+        const int rnd = (int)(rng.random() * 2048.0f) % 5;
+        if (rnd == 1) {
+            const float sm = rng.random() * 4.0f + 1.0f;
+            const float refl = rng.random() * 0.8f;
+            mats.push_back(make_material(MaterialType::Metal, kd, 0.f, sm, refl));
+        } else if (rnd == 2) {
+            const float3 u = rng.random3();
+            const float3 kd2 = make_float3(0.5f + 0.5f * u.x, 0.5f + 0.5f * u.y, 0.5f + 0.5f * u.z);
+            mats.push_back(make_material(MaterialType::Mirror, kd2, 0.f, rng.random() * 4.0f + 0.5f));
+        } else if (rnd == 3) {
+            const float sm = rng.random() * 4.0f + 2.0f;
+            const float ior = rng.random() * 2.0f + 1.2f;
+            mats.push_back(make_material(MaterialType::Glass, make_float3(1.f, 1.f, 1.f), ior, sm));
+        } else {
+            mats.push_back(make_material(MaterialType::Diffuse, kd));
+        }
+    }
+    Object* floor = make_object(PrimitiveType::Platform, mats[0], make_float3(0, -10000.f, 0), 10000.f, 0.f);
+    tracer.AddObject(floor);
+    for (int k = 0; k < n; ++k) {
+        const float z = -550.0f + 1.1f * (float)k;
+        const int rnd = (int)(rng.random() * 2048.0f) % 2;
+        const Material& mat = mats[rng.rand() % 20];
+        const float r = rng.random() * 15.0f + 1.0f;
+        if (rnd == 0) {
+            const float x = rng.random() * 300.0f - 150.0f;
+            tracer.AddObject(make_object(PrimitiveType::Sphere, mat, make_float3(x, r, z), r, 0.f));
+        } else {
+            const float h = r / 2.0f + rng.random() * 20.0f;
+            const float x = rng.random() * 300.0f - 150.0f;
+            tracer.AddObject(make_object(PrimitiveType::Cylinder, mat, make_float3(x, h / 2.0f, z), r, h));
+        }
+    }
+}
+
 struct FrameSink {
     std::atomic<int> frames{0};
     std::vector<uint8_t> last;
@@ -60,7 +128,7 @@ void on_frame(uint8_t* data, int width, int height, void* param) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    std::string scene = "s4", out, bgra_out, pfm, texture;
+    std::string scene = "s4", out, bgra_out, pfm, texture, dump_scene;
     int W = 64, H = 36, spp = 2, depth = 8, dispatch = 0;
     unsigned long long seed = 1234;
     for (int i = 1; i + 1 < argc; i += 2) {
@@ -76,6 +144,7 @@ int main(int argc, char** argv) {
         else if (k == "--bgra") bgra_out = v;
         else if (k == "--pfm") pfm = v;
         else if (k == "--texture") texture = v;
+        else if (k == "--dump-scene") dump_scene = v;
         else { fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
     }
 
@@ -86,8 +155,10 @@ int main(int argc, char** argv) {
     tracer.SetSeed(seed);
     if (!tracer.SetMaxRecursionDepth((uint)depth)) { fprintf(stderr, "%s\n", tracer.LastError().c_str()); return 1; }
 
-    // The same scenes as cpppathtracer_amd/scenes.py (S3, S4).
-    if (scene == "s3") {
+    // The same scenes as cpppathtracer_amd/scenes.py (S3, S4, S1000).
+    if (scene == "s1000") {
+        add_s1000(tracer);
+    } else if (scene == "s3") {
         tracer.AddObject(make_sphere(make_material(MaterialType::Diffuse, make_float3(0.8f, 0.3f, 0.3f)), make_float3(-35.f, 15.f, 0.f), 15.f));
         tracer.AddObject(make_sphere(make_material(MaterialType::Diffuse, make_float3(0.3f, 0.8f, 0.3f)), make_float3(0.f, 15.f, 0.f), 15.f));
         tracer.AddObject(make_sphere(make_material(MaterialType::Diffuse, make_float3(0.3f, 0.3f, 0.8f)), make_float3(35.f, 15.f, 0.f), 15.f));
@@ -113,6 +184,18 @@ int main(int argc, char** argv) {
         tracer.AddObject(make_sphere(textured(make_material(MaterialType::Glass, make_float3(1.f), 1.5f, 4.f)), make_float3(-35.f, 15.f, 0.f), 15.f));
         tracer.AddObject(make_sphere(textured(make_material(MaterialType::Metal, make_float3(0.8f, 0.6f, 0.2f), 0.f, 2.5f)), make_float3(0.f, 15.f, 0.f), 15.f));
         tracer.AddObject(make_sphere(make_material(MaterialType::Mirror, make_float3(0.9f), 0.f, 3.f, 0.6f), make_float3(35.f, 15.f, 0.f), 15.f));
+    }
+
+    if (!dump_scene.empty()) {
+        SceneBVH::BuildBVH();
+        uint64_t build = 0, rev = 0;
+        std::vector<cpt_object> built, current;
+        std::vector<uint64_t> updates;
+        SceneBVH::GetState(build, rev, &built, current, updates);
+        std::ofstream f(dump_scene, std::ios::binary);
+        f.write(reinterpret_cast<const char*>(built.data()), (std::streamsize)(built.size() * sizeof(cpt_object)));
+        printf("dumped %zu objects\n", built.size());
+        return f ? 0 : 1;
     }
 
     if (dispatch > 0) {

@@ -67,7 +67,8 @@ def _headless():
     return build.build_examples()
 
 
-@pytest.mark.parametrize("scene,W,H,spp,depth", [("s4", 64, 36, 2, 8), ("s3", 48, 32, 3, 4)])
+@pytest.mark.parametrize("scene,W,H,spp,depth", [("s4", 64, 36, 2, 8), ("s3", 48, 32, 3, 4), ("s1000", 64, 36, 2, 16),
+                                                  ("s1000", 32, 18, 64, 8)])
 def test_cpp_api_render_matches_oracle(oracle_mod, sky, tmp_path, scene, W, H, spp, depth):
     out = tmp_path / "rad.bin"
     r = subprocess.run([_headless(), "--scene", scene, "--width", str(W), "--height", str(H), "--spp", str(spp),
@@ -78,7 +79,7 @@ def test_cpp_api_render_matches_oracle(oracle_mod, sky, tmp_path, scene, W, H, s
     cam = oracle_mod.camera_get_copy(scenes.camera_for(W, H))
     rows = np.arange(H, dtype=np.int32)
     rng = oracle_mod.init_rng(1234, W, rows)
-    acc, _, _, _ = oracle_mod.render(scenes.SCENES[scene](), cam, sky, rows, spp, depth, rng)
+    acc, _, _, _ = oracle_mod.render(scenes.SCENES[scene](), cam, sky, rows, spp, depth, rng, threads=8)
     want = acc[:, :3] / acc[:, 3:4]
     np.testing.assert_array_equal(rgb.view(np.uint32), want.astype(np.float32).view(np.uint32))
 

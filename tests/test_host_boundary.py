@@ -123,3 +123,19 @@ def test_camera_get_copy_matches_oracle(oracle_mod, wh):
     assert a.tobytes() == b.tobytes()
     assert int(a["cur_sample_idx"]) == 1
     assert np.allclose(np.linalg.norm(a["w"]), 1.0, atol=1e-6)
+
+
+@pytest.mark.parametrize("scene", ["s3", "s4", "s1000"])
+def test_cpp_driver_scenes_equal_python_scenes(tmp_path, scene):
+    """The C++ headless driver builds S3/S4/S1000 through the drop-in API (AddObject +
+    BuildBVH); the objects BuildBVH copied equal scenes.py's byte for byte, so the C++ API
+    parity tests on the GPU render exactly the oracle's scenes."""
+    import subprocess
+    from cpppathtracer_amd import build
+    out = tmp_path / "objs.bin"
+    r = subprocess.run([build.build_examples(), "--scene", scene, "--dump-scene", str(out)], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(out, dtype=np.uint8)
+    want = np.ascontiguousarray(scenes.SCENES[scene]()).view(np.uint8).ravel()
+    np.testing.assert_array_equal(got, want)
