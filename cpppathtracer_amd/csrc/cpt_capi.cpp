@@ -291,6 +291,7 @@ struct cpt_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t user_stream = nullptr;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    hipEvent_t ev_main = nullptr;   // after the cost schedule's pilot: the dominant kernel(s) only
     bool have_timing = false;
     std::string err;
 
@@ -594,7 +595,16 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
     for (int p : pos0)
         if (p > 32766) return 0;
     const size_t base = out.size();
-    out.resize(base + (size_t)8 * n_wide * 4);
+    out.resize(base + (size_t)8 * n_wide * 4 + (n_wide * 7 + 1) / 2);
+    // The compact image after the eight octant copies (k_megakernel stages it in LDS when it
+    // fits, cpt_path.hpp trace_wide): 7 x 16 B per node, one copy for every octant --
+    //   [min x][max x][min y][max y][min z][max z] of the four slots (octant 0's order), then
+    //   {refs of slots 0..3 as int16, perm}: perm byte o = octant o's near-first child order
+    //   as four 2-bit slot indices (nearest in bits 0-1).
+    // A lane reads its entry planes at min or max by the sign of its direction, so its slab
+    // distances are bit for bit those of its octant's copy.
+    uint32_t* compact = reinterpret_cast<uint32_t*>(&out[base + (size_t)8 * n_wide * 4]);
+    std::vector<std::vector<int>> ord0(n_wide);
     for (int o = 0; o < 8; ++o) {
         for (int id = 0; id < n_wide; ++id) {
             const std::vector<int>& ch = kids[id];
@@ -607,6 +617,37 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
                 rec(right_first ? n.left : n.right);
             };
             rec(wbin[id]);
+            if (o == 0) ord0[id] = ord;
+            {
+                const std::vector<int>& o0 = ord0[id];
+                uint32_t* q = compact + (size_t)id * 28;
+                if (o == 0) {
+                    for (int k = 0; k < 4; ++k) {
+                        F3 lo{1e30f, 1e30f, 1e30f}, hi{-1e30f, -1e30f, -1e30f};
+                        int32_t r = -1;
+                        if (k < (int)o0.size()) {
+                            const BNode& n = w.nodes[o0[k]];
+                            lo = n.bmin;
+                            hi = n.bmax;
+                            r = n.is_object ? ~pos0[o0[k]] : wide_of[o0[k]];
+                        }
+                        const float l3[3] = {lo.x, lo.y, lo.z}, h3[3] = {hi.x, hi.y, hi.z};
+                        for (int a = 0; a < 3; ++a) {
+                            std::memcpy(&q[(2 * a) * 4 + k], &l3[a], 4);
+                            std::memcpy(&q[(2 * a + 1) * 4 + k], &h3[a], 4);
+                        }
+                        q[24 + (k >> 1)] |= (uint32_t)(uint16_t)(int16_t)r << (16 * (k & 1));
+                    }
+                }
+                uint32_t perm = 0;
+                for (int k = 0; k < 4; ++k) {
+                    int slot = k;   // empty slots stay where they are (at the end of every order)
+                    if (k < (int)ord.size())
+                        slot = (int)(std::find(o0.begin(), o0.end(), ord[k]) - o0.begin());
+                    perm |= (uint32_t)slot << (2 * k);
+                }
+                q[26 + (o >> 2)] |= perm << (8 * (o & 3));
+            }
             float f[24];
             int32_t ref[4];
             for (int k = 0; k < 4; ++k) {
@@ -770,9 +811,10 @@ int cpt_create(int device, cpt_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_start);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_stop);
-    if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipEventCreate(&c->ev_main);
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 32 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_work, 64);
-    if (e == hipSuccess) e = hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(c->d_stats, 0, 32 * sizeof(unsigned long long));
     if (e == hipSuccess) {
         const std::vector<uint32_t>& J = jump_tables();
         e = hipMalloc((void**)&c->d_jumps, J.size() * sizeof(uint32_t));
@@ -804,6 +846,7 @@ int cpt_destroy(cpt_ctx* c) {
     (void)hipFree(c->d_work);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
+    if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
     return CPT_OK;
@@ -1133,6 +1176,7 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
         if (!p.accumulate && c->n_rows > 0)
             HIP_TRY(c, hipMemsetAsync(c->d_accum, 0, (size_t)c->n_rows * c->width * sizeof(float4), s));
         int launches = 0;
+        HIP_TRY(c, hipEventRecord(c->ev_main, s));
         HIP_TRY(c, cpt::launch_wavefront(p, c->wf, (flags & CPT_RENDER_STATS) != 0, aux, s, &launches));
         c->last_launches = launches;
     } else {
@@ -1153,8 +1197,8 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
             if ((rc = ensure(c, &c->d_tile_order, &c->cap_tile_order, n_tiles)) != CPT_OK) return rc;
             HIP_TRY(c, cpt::launch_tile_schedule(p, passes, c->d_sched, c->cap_sched, c->d_tile_order, s));
             p.tile_order = c->d_tile_order;
-            c->last_launches = 2;
         }
+        HIP_TRY(c, hipEventRecord(c->ev_main, s));
         HIP_TRY(c, cpt::launch_megakernel(p, (flags & CPT_RENDER_STATS) != 0, aux, s));
     }
     HIP_TRY(c, hipEventRecord(c->ev_stop, s));
@@ -1231,6 +1275,14 @@ int cpt_get_raw_counters(cpt_ctx* c, uint64_t* out8) {
     return CPT_OK;
 }
 
+int cpt_get_diag_counters(cpt_ctx* c, uint64_t* out16) {
+    if (!c || !out16) return CPT_ERR_INVALID_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    HIP_TRY(c, hipMemcpy(out16, c->d_stats + 16, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return CPT_OK;
+}
+
 int cpt_get_walk_info(cpt_ctx* c, int32_t* out4) {
     if (!c || !out4) return CPT_ERR_INVALID_ARG;
     out4[0] = c->n_bvh;
@@ -1243,7 +1295,7 @@ int cpt_get_walk_info(cpt_ctx* c, int32_t* out4) {
 int cpt_reset_stats(cpt_ctx* c) {
     if (!c) return CPT_ERR_INVALID_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, 8 * sizeof(unsigned long long), c->stream()));
+    HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, 32 * sizeof(unsigned long long), c->stream()));
     return CPT_OK;
 }
 
@@ -1262,6 +1314,7 @@ int cpt_last_kernel_stats(cpt_ctx* c, float* avg_ms, int* launches) {
     float ms = 0.f;
     int rc = cpt_last_render_ms(c, &ms);
     if (rc != CPT_OK) return rc;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_main, c->ev_stop));   // without the pilot
     *launches = c->last_launches;
     *avg_ms = c->last_launches > 0 ? ms / (float)c->last_launches : 0.f;
     return CPT_OK;

@@ -41,6 +41,7 @@ struct Lane {
     int x, y;
     size_t pix;
     uint32_t tile;
+    uint32_t rank;   // dequeue position of the pixel's tile (heaviest first under the cost schedule)
     Xorwow s;
     v3 sum;
     float passes;
@@ -60,9 +61,28 @@ __device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int&
 // Deferred sky fetches run when this many 64ths of the tracing lanes hold one.
 constexpr int DEFER_MISS_ROUND = 32;
 
-template <bool STATS, bool AUX, bool PROBE>
-__global__ void __launch_bounds__(256, CPT_WAVES_PER_SIMD) k_megakernel(const KParams p) {
+// LDST: the 4-wide walk tree's compact image (<= LDS_TREE_NODES nodes) is staged in LDS once
+// per workgroup, and the walk reads its nodes there instead of from the octant copies in HBM
+// (a lane's node loads become ds_read_b128s: LDS latency instead of L1/L2 latency on every
+// dependent step of the walk).  One 768-lane workgroup per CU shares the copy.
+// One LDS workgroup per CU: 16 waves, 4 per SIMD (the image, the 16-bit stacks and the pending
+// sky fetches take 156 KB of the CU's 160 KB), which caps the kernel at 128 VGPRs.
+#ifndef CPT_LDS_BLOCK
+#define CPT_LDS_BLOCK 1024
+#endif
+template <bool LDST> constexpr int mk_block() { return LDST ? CPT_LDS_BLOCK : 256; }
+template <bool LDST> constexpr int mk_waves() { return LDST ? CPT_LDS_BLOCK / 256 : CPT_WAVES_PER_SIMD; }
+
+template <bool STATS, bool AUX, bool PROBE, bool LDST>
+__global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakernel(const KParams p) {
     constexpr bool COUNT = STATS || PROBE;
+    constexpr int BLK = mk_block<LDST>();
+    __shared__ uint4 s_tree[LDST ? LDS_TREE_NODES * 7 : 1];
+    if (LDST) {
+        const uint4* src = reinterpret_cast<const uint4*>(p.nodes + p.n_nodes + 8 * p.n_walk + 32 * p.n_wide);
+        for (int i = threadIdx.x; i < 7 * p.n_wide; i += BLK) s_tree[i] = src[i];
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63;
     const size_t npix = (size_t)p.n_rows * p.width;
     const uint32_t n_work = (uint32_t)(((p.width + 7) >> 3) * ((p.n_rows + 7) >> 3)) * 64u;
@@ -81,13 +101,20 @@ __global__ void __launch_bounds__(256, CPT_WAVES_PER_SIMD) k_megakernel(const KP
     float dep_acc = 0.f, first_depth = 0.f;
 
     // a lane's pending sky fetch: direction, the pass's radiance and attenuation so far
-    __shared__ float pending_q[9 * 256];
+    __shared__ float pending_q[9 * BLK];
     float* const pq = pending_q + threadIdx.x;
     bool pend = false;
+    stamps::init();
     for (;;) {
+        stamps::lap(5);
+        stamps::count(8);
         // ---- refill idle lanes with new pixels (wave-aggregated dequeue) ----------------
         if (!exhausted) {
+#ifdef CPT_MAX_LANES
+            const uint64_t need = __ballot(!busy && lane < CPT_MAX_LANES);   // A/B: sparse waves
+#else
             const uint64_t need = __ballot(!busy);
+#endif
             if (need) {
                 const int leader = __ffsll((unsigned long long)need) - 1;
                 uint32_t base = 0;
@@ -100,6 +127,7 @@ __global__ void __launch_bounds__(256, CPT_WAVES_PER_SIMD) k_megakernel(const KP
                     const uint32_t id = base + rank;
                     int x, ri;
                     if (id < n_work && decode_pixel(p, id, x, ri, L.tile)) {
+                        L.rank = id >> 6;
                         L.x = x;
                         L.y = p.rows[ri];
                         L.pix = (size_t)ri * p.width + x;
@@ -136,8 +164,17 @@ __global__ void __launch_bounds__(256, CPT_WAVES_PER_SIMD) k_megakernel(const KP
                         }
                     }
                 }
+#ifdef CPT_PRIO_CUT
+                // A/B: waves holding one of the heaviest tiles issue first (s_setprio)
+                if (p.tile_order) {
+                    const uint32_t cut = (n_work >> 6) * (uint32_t)CPT_PRIO_CUT / 1024u;
+                    if (__any(busy && L.rank < cut)) __builtin_amdgcn_s_setprio(3);
+                    else __builtin_amdgcn_s_setprio(0);
+                }
+#endif
             }
         }
+        stamps::lap(0);
         if (!__any(busy)) break;
         if (busy && L.left > 0) {
             // ---- one path segment: TraceRay + ClosetHit/Miss (path_tracer.cu:141-169) ----
@@ -147,7 +184,8 @@ __global__ void __launch_bounds__(256, CPT_WAVES_PER_SIMD) k_megakernel(const KP
             const RayK rk = make_rayk(ray);
             const bool finite_ray = !(ray.o.x != ray.o.x || ray.o.y != ray.o.y || ray.o.z != ray.o.z ||
                                       ray.d.x != ray.d.x || ray.d.y != ray.d.y || ray.d.z != ray.d.z);
-            const bool hit = trace_segment<COUNT>(p, rk, finite_ray, h, code, cnt);
+            const bool hit = trace_segment<COUNT, BLK, LDST>(p, rk, finite_ray, h, code, cnt, s_tree);
+            stamps::lap(3);
             Shade sh;
             v3 attr_normal;
             if (hit) {
@@ -156,6 +194,7 @@ __global__ void __launch_bounds__(256, CPT_WAVES_PER_SIMD) k_megakernel(const KP
                 eval_material(m, h.normal, ray.d, L.s, sh);
                 attr_normal = h.normal;
                 ray.o = h.pos;                         // payload.hit_pos = position
+                stamps::lap(4);
             } else {
                 if (COUNT) cnt.misses++;
                 sh.attenuation = mk1(0.f);             // never read: the path ends here
@@ -176,18 +215,18 @@ __global__ void __launch_bounds__(256, CPT_WAVES_PER_SIMD) k_megakernel(const KP
                                    __popcll(__ballot(pend || !hit)) * 64 >= DEFER_MISS_ROUND * __popcll(__ballot(1));
                 if (flush) {
                     if (pend) {   // older pending fetches first (their pass came first)
-                        const v3 pd = mk(pq[0 * 256], pq[1 * 256], pq[2 * 256]);
+                        const v3 pd = mk(pq[0 * BLK], pq[1 * BLK], pq[2 * BLK]);
                         const v3 sky = miss_radiance(p, pd);
-                        const v3 pr = mk(pq[3 * 256], pq[4 * 256], pq[5 * 256]);
-                        const v3 pa = mk(pq[6 * 256], pq[7 * 256], pq[8 * 256]);
+                        const v3 pr = mk(pq[3 * BLK], pq[4 * BLK], pq[5 * BLK]);
+                        const v3 pa = mk(pq[6 * BLK], pq[7 * BLK], pq[8 * BLK]);
                         L.sum = L.sum + (pr + pa * sky);
                         pend = false;
                     }
                     if (!hit) sh.radiance = miss_radiance(p, ray.d);
                 } else if (!hit) {
-                    pq[0 * 256] = ray.d.x; pq[1 * 256] = ray.d.y; pq[2 * 256] = ray.d.z;
-                    pq[3 * 256] = rad.x; pq[4 * 256] = rad.y; pq[5 * 256] = rad.z;
-                    pq[6 * 256] = att.x; pq[7 * 256] = att.y; pq[8 * 256] = att.z;
+                    pq[0 * BLK] = ray.d.x; pq[1 * BLK] = ray.d.y; pq[2 * BLK] = ray.d.z;
+                    pq[3 * BLK] = rad.x; pq[4 * BLK] = rad.y; pq[5 * BLK] = rad.z;
+                    pq[6 * BLK] = att.x; pq[7 * BLK] = att.y; pq[8 * BLK] = att.z;
                     pend = true;
                     deferred = true;
                     sh.radiance = mk1(0.f);            // placeholder: this pass's sum waits
@@ -243,6 +282,7 @@ __global__ void __launch_bounds__(256, CPT_WAVES_PER_SIMD) k_megakernel(const KP
             busy = false;
         }
     }
+    stamps::flush(p.stats + 16);
     if (STATS && !PROBE) {
         uint64_t a = wave_sum(cnt.segments), b = wave_sum(cnt.nodes), c = wave_sum(cnt.prims);
         uint64_t d = wave_sum(cnt.hits), e = wave_sum(cnt.misses);
@@ -513,36 +553,54 @@ __global__ void k_math_batch(int op, const float* a, const float* b, float* out,
 // ======================================================================================
 // Host-side launchers (called from cpt_capi.cpp).
 // ======================================================================================
-template <bool S, bool A, bool P>
+template <bool S, bool A, bool P, bool T>
 static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
     static int blocks_per_cu = -1, cus = 0;
-    constexpr int block = 256;
+    constexpr int block = mk_block<T>();
     if (blocks_per_cu < 0) {
         int dev = 0;
         hipError_t e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_megakernel<S, A, P>, block, 0);
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_megakernel<S, A, P, T>, block, 0);
         if (e != hipSuccess) return e;
         if (blocks_per_cu < 1) blocks_per_cu = 1;
     }
     // persistent grid: every resident slot once; lanes pull pixels from p.work
     const long long tiles = (long long)((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
+#ifdef CPT_MAX_LANES
+    long long want = (tiles * 64 * (64 / CPT_MAX_LANES) + block - 1) / block;
+#else
     long long want = (tiles * 64 + block - 1) / block;
+#endif
     long long grid = std::min<long long>(want, (long long)blocks_per_cu * cus);
     if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL((k_megakernel<S, A, P>), dim3((unsigned)grid), dim3(block), 0, stream, p);
+    hipLaunchKernelGGL((k_megakernel<S, A, P, T>), dim3((unsigned)grid), dim3(block), 0, stream, p);
     return hipGetLastError();
+}
+
+// The LDS walk needs the wide tree (ordered walk) and an image that fits.
+static bool use_lds_tree(const KParams& p) {
+#ifdef CPT_NO_LDS_TREE
+    return false;
+#else
+    return p.ordered == 1 && p.n_wide > 0 && p.n_wide <= LDS_TREE_NODES;
+#endif
+}
+
+template <bool S, bool A, bool P>
+static hipError_t launch_mk_any(const KParams& p, hipStream_t stream) {
+    return use_lds_tree(p) ? launch_mk<S, A, P, true>(p, stream) : launch_mk<S, A, P, false>(p, stream);
 }
 
 hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t stream) {
     if (p.width <= 0 || p.n_rows <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(p.work, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    if (stats && aux) return launch_mk<true, true, false>(p, stream);
-    if (stats) return launch_mk<true, false, false>(p, stream);
-    if (aux) return launch_mk<false, true, false>(p, stream);
-    return launch_mk<false, false, false>(p, stream);
+    if (stats && aux) return launch_mk_any<true, true, false>(p, stream);
+    if (stats) return launch_mk_any<true, false, false>(p, stream);
+    if (aux) return launch_mk_any<false, true, false>(p, stream);
+    return launch_mk_any<false, false, false>(p, stream);
 }
 
 // ======================================================================================
@@ -581,7 +639,7 @@ hipError_t launch_tile_schedule(const KParams& p0, int passes, void* scratch, si
     p.tile_cost = cost;
     p.tile_order = nullptr;
     p.accumulate = 0;
-    e = launch_mk<false, false, true>(p, stream);
+    e = launch_mk_any<false, false, true>(p, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_iota, dim3((n + 255) / 256), dim3(256), 0, stream, ids, (uint32_t)n);
     e = hipGetLastError();

@@ -8,6 +8,7 @@
 
 #include "cpt_device.hpp"
 #include "cpt_internal.hpp"
+#include "cpt_stamps.hpp"
 
 namespace cpt {
 
@@ -402,8 +403,13 @@ struct BufSrc {
     }
 };
 
+// The wide tree's compact image (cpt_capi.cpp linearise_wide): 7 x 16 B per node, after the
+// eight octant copies; padded to whole 32-B Nodes.
+__host__ __device__ __forceinline__ int wide_compact_nodes(int n_wide) { return (7 * n_wide + 1) / 2; }
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(const KParams& p) {
-    const uint32_t bytes = (uint32_t)(p.n_nodes + 8 * p.n_walk + 32 * p.n_wide) * (uint32_t)sizeof(Node);
+    const uint32_t bytes = (uint32_t)(p.n_nodes + 8 * p.n_walk + 32 * p.n_wide + wide_compact_nodes(p.n_wide)) *
+                           (uint32_t)sizeof(Node);
     return __builtin_amdgcn_make_buffer_rsrc((void*)p.nodes, (short)0, (int)bytes, 0x00020000);
 }
 
@@ -567,7 +573,12 @@ constexpr int SPEC_LEAF_ROUND = 32;
 // tests, whose box passes the conservative test, is tested here too, under a limit that is
 // never below the final tmax; the rank rule and the certificate are unchanged.
 // ======================================================================================
-constexpr int WIDE_LANES = 256;   // block size of every kernel that walks (stack stride)
+constexpr int WIDE_LANES = 256;   // block size of the kernels that walk the octant copies in HBM
+
+typedef __attribute__((address_space(3))) int16_t lds_i16;
+
+// LDS image of the wide tree (k_megakernel<..., LDST>): up to this many nodes of 7 x 16 B.
+constexpr int LDS_TREE_NODES = 512;
 
 struct WideNode {
     f2v e[3][2], x[3][2];   // entry / exit planes per axis, children (0,1) and (2,3)
@@ -585,6 +596,27 @@ __device__ __forceinline__ WideNode load_wide(__amdgpu_buffer_rsrc_t rsrc, uint3
     }
     const v4u32 r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 96, 0, 0);
     n.ref[0] = (int)r.x; n.ref[1] = (int)r.y; n.ref[2] = (int)r.z; n.ref[3] = (int)r.w;
+    return n;
+}
+
+// A node of the LDS image for a ray whose direction signs are (sx, sy, sz): the entry planes
+// of an axis are the slots' max planes when the ray runs toward -axis, else the min planes
+// (exactly the octant copy's choice), so the slab decisions are those of load_wide on the
+// ray's octant copy.  Slots are in octant 0's order; `perm` gives the ray's near-first order.
+__device__ __forceinline__ WideNode load_wide_lds(const uint4* tree, int cur, int sx, int sy, int sz, int pshift,
+                                                  bool phi, uint32_t& perm) {
+    const uint4* q = tree + cur * 7;
+    WideNode n;
+    const uint4 ex = q[sx], xx = q[1 - sx], ey = q[2 + sy], xy = q[3 - sy], ez = q[4 + sz], xz = q[5 - sz];
+    const uint4 r = q[6];
+    auto lo = [](uint4 v) { return f2v{__uint_as_float(v.x), __uint_as_float(v.y)}; };
+    auto hi = [](uint4 v) { return f2v{__uint_as_float(v.z), __uint_as_float(v.w)}; };
+    n.e[0][0] = lo(ex); n.e[0][1] = hi(ex); n.x[0][0] = lo(xx); n.x[0][1] = hi(xx);
+    n.e[1][0] = lo(ey); n.e[1][1] = hi(ey); n.x[1][0] = lo(xy); n.x[1][1] = hi(xy);
+    n.e[2][0] = lo(ez); n.e[2][1] = hi(ez); n.x[2][0] = lo(xz); n.x[2][1] = hi(xz);
+    n.ref[0] = (int)(int16_t)(r.x & 0xffffu); n.ref[1] = (int)(int16_t)(r.x >> 16);
+    n.ref[2] = (int)(int16_t)(r.y & 0xffffu); n.ref[3] = (int)(int16_t)(r.y >> 16);
+    perm = ((phi ? r.w : r.z) >> pshift) & 0xffu;
     return n;
 }
 
@@ -610,17 +642,22 @@ __device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], co
 // Child refs (node words 24..27, cpt_capi.cpp linearise_wide): >= 0 a wide node of the same
 // octant, -1 none, <= -2 a leaf as ~k with k its position in the octant-0 binary order
 // (absolute Node index n_nodes + k).  The host keeps both ranges within 15 bits, so the LDS
-// stack holds 16-bit entries (16 KB per 256-lane block).
-template <bool STATS>
+// stack holds 16-bit entries (BLK lanes x CPT_WSTACK x 2 B per block).
+// LDST: the nodes come from the block's LDS image `tree` (k_megakernel stages it), else from
+// the ray's octant copy in HBM through `rsrc`.
+template <bool STATS, int BLK = WIDE_LANES, bool LDST = false>
 __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc_t rsrc, int oct, const RayK& ray,
-                                          Hit& h, int& code_out, Counters& cnt) {
-    __shared__ int16_t wstack[CPT_WSTACK * WIDE_LANES];
-    int16_t* const stk = wstack + threadIdx.x;
+                                          Hit& h, int& code_out, Counters& cnt, const uint4* tree) {
+    __shared__ int16_t wstack[CPT_WSTACK * BLK];
+    // an LDS-typed pointer: 32-bit ds_read/ds_write addressing (a generic pointer costs a
+    // 64-bit multiply-add per push and pop)
+    lds_i16* const stk = (lds_i16*)wstack + threadIdx.x;
     const BufSrc nodes{rsrc, 0u};   // leaves by absolute Node index
     constexpr int NONE = -1;
     float tmax = DEFAULT_RAY_TMAX;
     int best = -1, kind = 0;
     int best_rank = 0x7fffffff;
+    stamps::lap(6);
     // the platforms (every ray tests them) run first, by the whole wave at once, so the walk
     // starts with their tmax; same rank rule, so the order does not matter
     for (int k = 0; k < p.n_unb; ++k) {
@@ -633,30 +670,56 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         }
     }
     float limit = walk_limit(tmax);   // changes only in leaf rounds
+    stamps::lap(7);
     const uint32_t wbase = (uint32_t)(p.n_nodes + 8 * p.n_walk + 4 * oct * p.n_wide) * (uint32_t)sizeof(Node);
-    int sp = 0, cur = 0;   // the root
+    const int sx = oct & 1, sy = (oct >> 1) & 1, sz = oct >> 2, pshift = 8 * (oct & 3);
+    const bool phi = oct >= 4;
+    lds_i16* top = stk;    // the next free stack entry (entries are BLK apart)
+    int cur = 0;           // the root
     int parked = -1;       // absolute Node index of the parked leaf
-    auto pop = [&]() -> int { return sp > 0 ? (int)stk[--sp * WIDE_LANES] : NONE; };
+    auto pop = [&]() -> int {
+        if (top == stk) return NONE;
+        top -= BLK;
+        return (int)*top;
+    };
     for (;;) {
+        stamps::count(9);
         if (cur <= -2 && parked < 0) {
             parked = p.n_nodes + ~cur;
             cur = pop();
         }
         if (cur >= 0) {
             if (STATS) cnt.nodes++;
-            const WideNode n = load_wide(rsrc, wbase + (uint32_t)cur * 128u);
+            uint32_t perm = 0xE4u;   // slots 0..3 already near-first (octant copy)
+            const WideNode n = LDST ? load_wide_lds(tree, cur, sx, sy, sz, pshift, phi, perm)
+                                    : load_wide(rsrc, wbase + (uint32_t)cur * 128u);
             const f2v e01[3] = {n.e[0][0], n.e[1][0], n.e[2][0]}, x01[3] = {n.x[0][0], n.x[1][0], n.x[2][0]};
             const f2v e23[3] = {n.e[0][1], n.e[1][1], n.e[2][1]}, x23[3] = {n.x[0][1], n.x[1][1], n.x[2][1]};
             const uint32_t m = wide_pair(e01, x01, ray, limit) | (wide_pair(e23, x23, ray, limit) << 2);
-            int next = NONE;
+            // Children in the ray's near-first order (rank k = 0 nearest): hit bits hk and refs
+            // rk.  The nearest hit child is walked next; the other hits are pushed, far ones
+            // first, without branches: every candidate is written at the top and the top moves
+            // past it only when it is pushed (the host bounds the depth, so the write at an
+            // unmoved top stays inside the lane's stack).
+            uint32_t hk = 0;
+            int rk[4];
 #pragma unroll
-            for (int k = 3; k >= 0; --k) {
-                if ((m >> k) & 1u) {
-                    if (next != NONE) stk[sp++ * WIDE_LANES] = (int16_t)next;
-                    next = n.ref[k];
-                }
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t slot = LDST ? (perm >> (2 * k)) & 3u : (uint32_t)k;
+                hk |= ((m >> slot) & 1u) << k;
+                rk[k] = LDST ? (slot & 2u ? (slot & 1u ? n.ref[3] : n.ref[2]) : (slot & 1u ? n.ref[1] : n.ref[0]))
+                             : n.ref[k];
             }
-            if (next == NONE) next = pop();
+#pragma unroll
+            for (int k = 3; k >= 1; --k) {
+                const bool push = ((hk >> k) & 1u) && (hk & ((1u << k) - 1u));
+                *top = (int16_t)rk[k];
+                top += push ? BLK : 0;
+            }
+            const uint32_t first = __builtin_ctz(hk | 16u);   // 4: no child hit
+            const int n01 = (first & 1u) ? rk[1] : rk[0], n23 = (first & 1u) ? rk[3] : rk[2];
+            int next = (first & 2u) ? n23 : n01;
+            if (hk == 0) next = pop();
             cur = next;
             if (cur <= -2 && parked < 0) {   // park the nearest leaf at once
                 parked = p.n_nodes + ~cur;
@@ -666,8 +729,10 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         const bool working = parked >= 0 || cur != NONE;
         const bool stopped = parked >= 0 && (cur == NONE || cur <= -2);
         const uint64_t w = __ballot(working);
+        stamps::lap(1);
         if (!w) break;
         if (__popcll(__ballot(stopped)) * 64 >= SPEC_LEAF_ROUND * __popcll(w) && parked >= 0) {
+            stamps::count(10);
             if (STATS) cnt.prims++;
             const Node lf = nodes(parked);
             int k;
@@ -679,6 +744,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
             }
             parked = -1;
         }
+        stamps::lap(2);
     }
     if (best < 0) return 0;
     const Node wn = nodes(best);
@@ -694,15 +760,15 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
 // and the reference-order fallback (CPT_TRAVERSAL_ORDERED): the 4-wide walk with parked
 // leaves (ordered == 1 and a wide tree), else the binary octant orders testing each leaf
 // where the walk meets it.
-template <bool STATS>
+template <bool STATS, int BLK = WIDE_LANES, bool LDST = false>
 __device__ __forceinline__ bool trace_segment(const KParams& p, const RayK& rk, bool finite, Hit& h, int& code,
-                                              Counters& cnt) {
+                                              Counters& cnt, const uint4* tree = nullptr) {
     const __amdgpu_buffer_rsrc_t rsrc = node_rsrc(p);
     if (p.ordered && __builtin_expect(finite, 1)) {
         int n, r;
         if (p.ordered == 1 && p.n_wide > 0) {
             const int oct = (rk.d.x < 0.f ? 1 : 0) | (rk.d.y < 0.f ? 2 : 0) | (rk.d.z < 0.f ? 4 : 0);
-            r = trace_wide<STATS>(p, rsrc, oct, rk, h, code, cnt);
+            r = trace_wide<STATS, BLK, LDST>(p, rsrc, oct, rk, h, code, cnt, tree);
         } else {
             const BufSrc order{rsrc, walk_order(p, rk.d, n) * (uint32_t)sizeof(Node)};
             r = trace<STATS, true, true>(order, n, rk, h, code, cnt);

@@ -1,0 +1,51 @@
+// cpt_stamps.hpp — DIAGNOSTIC wave-time stamps of the megakernel (CPT_STAMPS builds only; a
+// stamped library is never the one bench.py times).  Every stamp is taken by the wave's first
+// active lane, so a wave's time is counted once wherever it is (also inside divergent code):
+// lap(i) adds the s_memtime cycles since the wave's previous lap to slot i; count(i) adds 1.
+// Slots (tools/stamps.py): 0 refill, 1 walk: node visits, 2 walk: leaf rounds, 3 certificate +
+// hit attributes, 4 hit shading, 5 rest of the loop (sky, pass bookkeeping, RayGen, write-back),
+// 6 ray setup, 7 platforms; counts: 8 outer rounds, 9 walk iterations, 10 leaf rounds.
+// The block's per-wave slots live in LDS; flush() adds them to out[0..15].
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cpt {
+namespace stamps {
+constexpr int N_SLOTS = 16;   // slot 15: the wave's last stamp
+
+#ifdef CPT_STAMPS
+__device__ __forceinline__ unsigned long long* wave_slots() {
+    __shared__ unsigned long long s[16 * N_SLOTS];   // up to 16 waves per block
+    return s + (threadIdx.x >> 6) * N_SLOTS;
+}
+__device__ __forceinline__ bool first_active() {
+    return (int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1;
+}
+__device__ __forceinline__ void init() {   // whole wave active
+    if ((threadIdx.x & 63) < N_SLOTS) wave_slots()[threadIdx.x & 63] = 0;
+    if ((threadIdx.x & 63) == 0) wave_slots()[N_SLOTS - 1] = __builtin_amdgcn_s_memtime();
+}
+__device__ __forceinline__ void lap(int i) {
+    if (first_active()) {
+        unsigned long long* s = wave_slots();
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        s[i] += t - s[N_SLOTS - 1];
+        s[N_SLOTS - 1] = t;
+    }
+}
+__device__ __forceinline__ void count(int i) {
+    if (first_active()) wave_slots()[i] += 1;
+}
+__device__ __forceinline__ void flush(unsigned long long* out) {   // whole wave active
+    if ((threadIdx.x & 63) < N_SLOTS - 1) atomicAdd(out + (threadIdx.x & 63), wave_slots()[threadIdx.x & 63]);
+}
+#else
+__device__ __forceinline__ void init() {}
+__device__ __forceinline__ void lap(int) {}
+__device__ __forceinline__ void count(int) {}
+__device__ __forceinline__ void flush(unsigned long long*) {}
+#endif
+}  // namespace stamps
+}  // namespace cpt

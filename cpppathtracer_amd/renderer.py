@@ -152,6 +152,13 @@ class Renderer:
         self._check(self._L.cpt_last_render_ms(self._ctx, ctypes.byref(ms)))
         return float(ms.value)
 
+    def last_kernel_stats(self):
+        """(average ms per launch, launches) of the last render's dominant kernel, without the
+        cost schedule's pilot (HIP events on the launch stream; waits for the render)."""
+        ms, n = ctypes.c_float(0), ctypes.c_int(0)
+        self._check(self._L.cpt_last_kernel_stats(self._ctx, ctypes.byref(ms), ctypes.byref(n)))
+        return float(ms.value), int(n.value)
+
     # -- readback --------------------------------------------------------------------
     @property
     def npix(self):
@@ -192,6 +199,12 @@ class Renderer:
     def raw_counters(self):
         out = np.zeros(8, dtype=np.uint64)
         self._check(self._L.cpt_get_raw_counters(self._ctx, _p(out)))
+        return [int(x) for x in out]
+
+    def diag_counters(self):
+        """DIAGNOSTIC: the 16 stamp slots of a CPT_STAMPS build (cpt_stamps.hpp)."""
+        out = np.zeros(16, dtype=np.uint64)
+        self._check(self._L.cpt_get_diag_counters(self._ctx, _p(out)))
         return [int(x) for x in out]
 
     def walk_info(self):

@@ -229,9 +229,11 @@ int cpt_copy_accum_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
 int cpt_get_stats(cpt_ctx* ctx, cpt_stats* out);
 int cpt_reset_stats(cpt_ctx* ctx);
 /* All 8 raw device counters (0-4 = cpt_stats; 5 = ordered-walk segments that failed the
- * winner certificate and took the reference walk (CPT_RENDER_STATS | CPT_TRAVERSAL_ORDERED);
- * 5-7 in a CPT_STAMPS diagnostic build: refill, traversal, shading cycle sums). */
+ * winner certificate and took the reference walk (CPT_RENDER_STATS | CPT_TRAVERSAL_ORDERED)). */
 int cpt_get_raw_counters(cpt_ctx* ctx, uint64_t* out8);
+/* DIAGNOSTIC: the 16 wave-time stamp slots of a CPT_STAMPS build (cpt_stamps.hpp; all zero in
+ * the shipped library), summed over the renders since the last cpt_reset_stats. */
+int cpt_get_diag_counters(cpt_ctx* ctx, uint64_t* out16);
 /* Node counts of the scene's walk structures (host-side, no GPU work): [0] the reference
  * order (bvh.cu's tree, 32-B nodes), [1] each octant order of the binary walk tree, [2] the
  * 4-wide walk tree's nodes per octant (128 B each; 0 = the ordered walk uses the binary
@@ -240,7 +242,9 @@ int cpt_get_raw_counters(cpt_ctx* ctx, uint64_t* out8);
 int cpt_get_walk_info(cpt_ctx* ctx, int32_t* out4);
 /* Device time of the last cpt_render (HIP events on the launch stream); waits for it. */
 int cpt_last_render_ms(cpt_ctx* ctx, float* ms);
-/* Average device time of one kernel launch of the last cpt_render's dominant kernel. */
+/* Average device time of one launch of the last cpt_render's dominant kernel: the megakernel
+ * (launches = 1; the cost schedule's pilot and sort are not included) or the wavefront's
+ * extend/shade launches (their total / launches).  Waits for the render. */
 int cpt_last_kernel_stats(cpt_ctx* ctx, float* avg_ms, int* launches);
 
 /* Display path (path_tracer.cu:177-254): 5x5 edge-aware denoise of the current 1-spp

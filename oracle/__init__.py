@@ -24,11 +24,23 @@ def build(force: bool = False) -> str:
     return LIB_PATH
 
 
+def use_library(path=None):
+    """DIAGNOSTIC: bind the module to another build of the oracle (e.g. the FMA-contraction
+    variant, `make -C oracle fma`); None returns to the default build."""
+    global _lib, _lib_path
+    _lib = None
+    _lib_path = path
+
+
+_lib_path = None
+
+
 def lib():
     global _lib
     if _lib is None:
-        build()
-        L = ctypes.CDLL(LIB_PATH)
+        if _lib_path is None:
+            build()
+        L = ctypes.CDLL(_lib_path or LIB_PATH)
         P = ctypes.c_void_p
         i32, u64, f32, f64 = ctypes.c_int, ctypes.c_uint64, ctypes.c_float, ctypes.c_double
         L.or_abi_version.restype = i32
@@ -77,6 +89,8 @@ def lib():
         L.or_clear_textures.restype = None
         L.or_last_fallbacks.argtypes = []
         L.or_last_fallbacks.restype = u64
+        L.or_set_pixel_segments.argtypes = [P]
+        L.or_set_pixel_segments.restype = None
         L.or_set_walk.argtypes = [i32]
         L.or_set_walk.restype = None
         _lib = L
@@ -178,6 +192,21 @@ def clear_textures():
 def last_fallbacks() -> int:
     """DIAGNOSTIC: certificate fallbacks of the last render() in the ordered walk."""
     return int(lib().or_last_fallbacks())
+
+
+def pixel_segments(objs, cam, env, rows, spp, max_depth, seed, threads=1):
+    """DIAGNOSTIC: each pixel's number of path segments over `spp` passes (the length of its
+    sequential chain) -> uint32 [n_rows * W]."""
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    W = int(np.asarray(cam["width"]).reshape(-1)[0])
+    out = np.zeros(rows.size * W, dtype=np.uint32)
+    rng = init_rng(seed, W, rows, threads=threads)
+    lib().or_set_pixel_segments(_ptr(out))
+    try:
+        render(objs, cam, env, rows, spp, max_depth, rng, threads=threads)
+    finally:
+        lib().or_set_pixel_segments(None)
+    return out
 
 
 def set_walk(ordered: bool):

@@ -1209,6 +1209,10 @@ struct RenderJob {
     int accumulate;
 };
 
+// DIAGNOSTIC (or_set_pixel_segments): per-pixel path segments of the next renders, i.e. the
+// length of each pixel's sequential chain (tools/chain_costs.py).
+uint32_t* g_pixel_segments = nullptr;
+
 void render_rows(const RenderJob& J, int thread, int nthreads, Stats& st) {
     const int W = J.cam.width;
     const size_t npix = (size_t)J.n_rows * W;
@@ -1223,12 +1227,14 @@ void render_rows(const RenderJob& J, int thread, int nthreads, Stats& st) {
             f3 sum = J.accumulate ? mk(a[0], a[1], a[2]) : mk1(0.0f);
             float cnt = J.accumulate ? a[3] : 0.0f;
             PassOut last{};
+            const uint64_t seg0 = st.segments;
             for (int sidx = 0; sidx < J.spp; ++sidx) {
                 last = sample_pixel(*J.bvh, J.env, J.cam, J.max_depth, x, y, s, st);
                 sum = add(sum, last.radiance);
                 cnt += 1.0f;
             }
             a[0] = sum.x; a[1] = sum.y; a[2] = sum.z; a[3] = cnt;
+            if (g_pixel_segments) g_pixel_segments[pix] += (uint32_t)(st.segments - seg0);
             if (J.normal && J.spp > 0) {
                 J.normal[pix * 3 + 0] = last.normal.x;
                 J.normal[pix * 3 + 1] = last.normal.y;
@@ -1249,6 +1255,10 @@ void render_rows(const RenderJob& J, int thread, int nthreads, Stats& st) {
 extern "C" {
 
 int or_abi_version(void) { return 1; }
+
+// DIAGNOSTIC: per-pixel segment counts of the following renders are ADDED to `out`
+// ([n_rows * W] of the render's frame); nullptr turns it off.
+void or_set_pixel_segments(uint32_t* out) { g_pixel_segments = out; }
 
 // Binds texels to a material texture handle (replaces an earlier binding of the handle).
 void or_bind_texture(uint64_t handle, const uint8_t* rgba, int w, int h, int valid_cols, int addr, int filter) {

@@ -1,50 +1,55 @@
-"""Per-phase cycle shares from CPT_STAMPS diagnostic builds (never timed).
-  CPT_STAMPS=1: megakernel refill / trace / shade;  CPT_STAMPS=2: BVH walk leaf / slab / whole iteration;
-  CPT_STAMPS=4: hit shading / miss shading / rest of the megakernel loop;
-  CPT_STAMPS=3: wave-level counts (walk iterations, iterations with a lane at a leaf / at an inner
-  node, segment rounds) for the lane-efficiency breakdown.
-Build a diagnostic library with build.build(out=..., defines={"CPT_STAMPS": m}) and point
-CPT_LIB_PATH at it."""
+"""Wave-time breakdown of the megakernel from a CPT_STAMPS diagnostic build (cpt_stamps.hpp;
+never the timed library).
+
+    python tools/stamps.py [config] [spp] [--rows a:b]      (CPT_LIB_PATH = the stamped build)
+
+Build the diagnostic library with
+    python -c "from cpppathtracer_amd import build as b; b.build(out='build/diag/stamps.so', defines={'CPT_STAMPS': 1})"
+Prints each section's share of the waves' time and the per-round / per-iteration cycles.
+"""
+import json
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
 import torch  # noqa: F401,E402
 from cpppathtracer_amd import Renderer, camera_get_copy, scenes, texture_io  # noqa: E402
 
-cfg = scenes.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "c4"]
-spp = int(sys.argv[2]) if len(sys.argv) > 2 else 8
-mode = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+NAMES = ["refill", "walk_nodes", "walk_leaf_rounds", "certificate_attrs", "hit_shading", "rest", "ray_setup",
+         "platforms"]
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+cfg = scenes.CONFIGS[args[0] if args else "c4"]
+spp = int(args[1]) if len(args) > 1 else 8
+rows = None
+for a in sys.argv[1:]:
+    if a.startswith("--rows="):
+        lo, hi = (int(x) for x in a[7:].split(":"))
+        rows = np.arange(lo, hi, dtype=np.int32)
 r = Renderer(0)
 r.set_scene(scenes.SCENES[cfg["scene"]]())
 r.set_env(texture_io.load_cptex())
-r.set_frame(cfg["width"], cfg["height"])
+r.set_frame(cfg["width"], cfg["height"], rows)
 r.init_rng(1234)
 cam = camera_get_copy(scenes.camera_for(cfg["width"], cfg["height"]))
+r.render(cam, 1, cfg["depth"], sync=True, ordered=True)   # warm-up
+r.init_rng(1234)
 r.reset_stats()
-r.render(cam, spp, cfg["depth"], stats=True, sync=True, ordered=os.environ.get("CPT_WALK", "ordered") == "ordered")
-c = r.raw_counters()
-print("counts", dict(zip(["segments", "nodes", "prims", "hits", "misses"], c[:5])))
-if mode == 1:
-    tot = sum(c[5:8])
-    print("refill %.1f%%  trace %.1f%%  shade+rest %.1f%%  (wave-cycles %d)" % (100 * c[5] / tot, 100 * c[6] / tot,
-                                                                              100 * c[7] / tot, tot))
-elif mode == 4:
-    tot = c[7]
-    print("hit shading %.1f%%  miss shading %.1f%%  rest %.1f%%  (wave-cycles %d)" % (
-        100 * c[5] / tot, 100 * c[6] / tot, 100 * (tot - c[5] - c[6]) / tot, tot))
-elif mode == 3:
-    seg, nodes, hits = c[0], c[1], c[3]
-    w_seg = c[4] - (seg - hits)          # stats[4] = misses + segment rounds
-    w_leaf, w_inner, w_it = c[5], c[6], c[7]
-    print("segment rounds %d: %.1f of 64 lanes trace per round" % (w_seg, seg / w_seg))
-    print("walk iterations %d: %.1f of 64 lanes step per iteration (%.1f walk iterations per round, "
-          "%.1f node visits per segment)" % (w_it, nodes / w_it, w_it / w_seg, nodes / seg))
-    print("iterations with a lane at a leaf %.1f%%, at an inner node %.1f%%, both %.1f%%" % (
-        100 * w_leaf / w_it, 100 * w_inner / w_it, 100 * (w_leaf + w_inner - w_it) / w_it))
-else:
-    # per-iteration wave-cycles, normalised by lane-level node visits / 64 (the ideal iteration count)
-    it = c[7]
-    print("walk iterations: leaf %.1f%%  slab %.1f%%  rest %.1f%%  (iteration wave-cycles %d)" % (
-        100 * c[5] / it, 100 * c[6] / it, 100 * (it - c[5] - c[6]) / it, it))
-    print("wave-cycles per lane node visit x64: %.1f" % (it / (c[1] / 64.0)))
+r.render(cam, spp, cfg["depth"], stats=True, sync=True, ordered=True, schedule="cost")
+c = r.diag_counters()
+st = dict(zip(["segments", "nodes", "prims", "hits", "misses"], r.raw_counters()[:5]))
+tot = sum(c[:8])
+rounds, iters, leaf_rounds = c[8], c[9], c[10]
+out = {
+    "config": cfg, "spp": spp, "counts": st,
+    "share": {n: round(c[i] / tot, 4) for i, n in enumerate(NAMES)},
+    "wave_cycles": tot, "wave_rounds": rounds, "walk_iterations": iters, "leaf_rounds": leaf_rounds,
+    "cycles_per_round": round(tot / max(1, rounds), 1),
+    "walk_iterations_per_round": round(iters / max(1, rounds), 2),
+    "leaf_rounds_per_round": round(leaf_rounds / max(1, rounds), 2),
+    "cycles_per_walk_iteration": round((c[1] + c[2]) / max(1, iters), 1),
+    "cycles_per_leaf_round": round(c[2] / max(1, leaf_rounds), 1),
+    "lanes_per_round": round(st["segments"] / max(1, rounds), 2),
+    "lanes_per_walk_iteration": round(st["nodes"] / max(1, iters), 2),
+}
+print(json.dumps(out))
