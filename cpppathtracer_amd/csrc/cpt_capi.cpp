@@ -599,10 +599,10 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
     // The compact image after the eight octant copies (k_megakernel stages it in LDS when it
     // fits, cpt_path.hpp trace_wide): 7 x 16 B per node, one copy for every octant --
     //   [min x][max x][min y][max y][min z][max z] of the four slots (octant 0's order), then
-    //   {refs of slots 0..3 as int16, perm}: perm byte o = octant o's near-first child order
-    //   as four 2-bit slot indices (nearest in bits 0-1).
+    //   {refs of slots 0..3 as int16, 8 B zero}.
     // A lane reads its entry planes at min or max by the sign of its direction, so its slab
-    // distances are bit for bit those of its octant's copy.
+    // distances are bit for bit those of its octant's copy; it orders the hit children by
+    // their entry distances.
     uint32_t* compact = reinterpret_cast<uint32_t*>(&out[base + (size_t)8 * n_wide * 4]);
     std::vector<std::vector<int>> ord0(n_wide);
     for (int o = 0; o < 8; ++o) {
@@ -639,14 +639,6 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
                         q[24 + (k >> 1)] |= (uint32_t)(uint16_t)(int16_t)r << (16 * (k & 1));
                     }
                 }
-                uint32_t perm = 0;
-                for (int k = 0; k < 4; ++k) {
-                    int slot = k;   // empty slots stay where they are (at the end of every order)
-                    if (k < (int)ord.size())
-                        slot = (int)(std::find(o0.begin(), o0.end(), ord[k]) - o0.begin());
-                    perm |= (uint32_t)slot << (2 * k);
-                }
-                q[26 + (o >> 2)] |= perm << (8 * (o & 3));
             }
             float f[24];
             int32_t ref[4];

@@ -41,7 +41,6 @@ struct Lane {
     int x, y;
     size_t pix;
     uint32_t tile;
-    uint32_t rank;   // dequeue position of the pixel's tile (heaviest first under the cost schedule)
     Xorwow s;
     v3 sum;
     float passes;
@@ -59,7 +58,10 @@ __device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int&
 }
 
 // Deferred sky fetches run when this many 64ths of the tracing lanes hold one.
-constexpr int DEFER_MISS_ROUND = 32;
+#ifndef CPT_DEFER_MISS_ROUND
+#define CPT_DEFER_MISS_ROUND 32
+#endif
+constexpr int DEFER_MISS_ROUND = CPT_DEFER_MISS_ROUND;
 
 // LDST: the 4-wide walk tree's compact image (<= LDS_TREE_NODES nodes) is staged in LDS once
 // per workgroup, and the walk reads its nodes there instead of from the octant copies in HBM
@@ -110,11 +112,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         stamps::count(8);
         // ---- refill idle lanes with new pixels (wave-aggregated dequeue) ----------------
         if (!exhausted) {
-#ifdef CPT_MAX_LANES
-            const uint64_t need = __ballot(!busy && lane < CPT_MAX_LANES);   // A/B: sparse waves
-#else
             const uint64_t need = __ballot(!busy);
-#endif
             if (need) {
                 const int leader = __ffsll((unsigned long long)need) - 1;
                 uint32_t base = 0;
@@ -127,7 +125,6 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                     const uint32_t id = base + rank;
                     int x, ri;
                     if (id < n_work && decode_pixel(p, id, x, ri, L.tile)) {
-                        L.rank = id >> 6;
                         L.x = x;
                         L.y = p.rows[ri];
                         L.pix = (size_t)ri * p.width + x;
@@ -164,14 +161,6 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                         }
                     }
                 }
-#ifdef CPT_PRIO_CUT
-                // A/B: waves holding one of the heaviest tiles issue first (s_setprio)
-                if (p.tile_order) {
-                    const uint32_t cut = (n_work >> 6) * (uint32_t)CPT_PRIO_CUT / 1024u;
-                    if (__any(busy && L.rank < cut)) __builtin_amdgcn_s_setprio(3);
-                    else __builtin_amdgcn_s_setprio(0);
-                }
-#endif
             }
         }
         stamps::lap(0);
@@ -568,11 +557,7 @@ static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
     }
     // persistent grid: every resident slot once; lanes pull pixels from p.work
     const long long tiles = (long long)((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
-#ifdef CPT_MAX_LANES
-    long long want = (tiles * 64 * (64 / CPT_MAX_LANES) + block - 1) / block;
-#else
     long long want = (tiles * 64 + block - 1) / block;
-#endif
     long long grid = std::min<long long>(want, (long long)blocks_per_cu * cus);
     if (grid < 1) return hipSuccess;
     hipLaunchKernelGGL((k_megakernel<S, A, P, T>), dim3((unsigned)grid), dim3(block), 0, stream, p);

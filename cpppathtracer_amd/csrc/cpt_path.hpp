@@ -559,7 +559,10 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
 
 // Leaf rounds of the wide walk run when this many 64ths of the wave's working lanes are
 // stopped at a parked leaf.
-constexpr int SPEC_LEAF_ROUND = 32;
+#ifndef CPT_SPEC_LEAF_ROUND
+#define CPT_SPEC_LEAF_ROUND 32
+#endif
+constexpr int SPEC_LEAF_ROUND = CPT_SPEC_LEAF_ROUND;
 
 // ======================================================================================
 // The ordered walk on the 4-wide walk tree (DESIGN.md §Wide walk).  One iteration loads a
@@ -602,9 +605,8 @@ __device__ __forceinline__ WideNode load_wide(__amdgpu_buffer_rsrc_t rsrc, uint3
 // A node of the LDS image for a ray whose direction signs are (sx, sy, sz): the entry planes
 // of an axis are the slots' max planes when the ray runs toward -axis, else the min planes
 // (exactly the octant copy's choice), so the slab decisions are those of load_wide on the
-// ray's octant copy.  Slots are in octant 0's order; `perm` gives the ray's near-first order.
-__device__ __forceinline__ WideNode load_wide_lds(const uint4* tree, int cur, int sx, int sy, int sz, int pshift,
-                                                  bool phi, uint32_t& perm) {
+// ray's octant copy.
+__device__ __forceinline__ WideNode load_wide_lds(const uint4* tree, int cur, int sx, int sy, int sz) {
     const uint4* q = tree + cur * 7;
     WideNode n;
     const uint4 ex = q[sx], xx = q[1 - sx], ey = q[2 + sy], xy = q[3 - sy], ez = q[4 + sz], xz = q[5 - sz];
@@ -616,12 +618,12 @@ __device__ __forceinline__ WideNode load_wide_lds(const uint4* tree, int cur, in
     n.e[2][0] = lo(ez); n.e[2][1] = hi(ez); n.x[2][0] = lo(xz); n.x[2][1] = hi(xz);
     n.ref[0] = (int)(int16_t)(r.x & 0xffffu); n.ref[1] = (int)(int16_t)(r.x >> 16);
     n.ref[2] = (int)(int16_t)(r.y & 0xffffu); n.ref[3] = (int)(int16_t)(r.y >> 16);
-    perm = ((phi ? r.w : r.z) >> pshift) & 0xffu;
     return n;
 }
 
 // Hit mask of the four children: slab_reject_octant for each, two children per packed op.
-__device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], const RayK& ray, float limit) {
+__device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], const RayK& ray, float limit,
+                                              float& lo_a, float& lo_b) {
     const f2v ox = {ray.o.x, ray.o.x}, oy = {ray.o.y, ray.o.y}, oz = {ray.o.z, ray.o.z};
     const f2v ix = {ray.ix, ray.ix}, iy = {ray.iy, ray.iy}, iz = {ray.iz, ray.iz};
     const f2v bx = {ray.bx, ray.bx}, by = {ray.by, ray.by}, bz = {ray.bz, ray.bz};
@@ -636,6 +638,8 @@ __device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], co
     const float m1 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo1) + __builtin_fabsf(hi1), 2.0f * WALK_MARGIN_ABS);
     const bool rej0 = lo0 - hi0 > m0 || lo0 > limit || hi0 < ray.t3;
     const bool rej1 = lo1 - hi1 > m1 || lo1 > limit || hi1 < ray.t3;
+    lo_a = lo0;
+    lo_b = lo1;
     return (rej0 ? 0u : 1u) | (rej1 ? 0u : 2u);
 }
 
@@ -672,8 +676,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     float limit = walk_limit(tmax);   // changes only in leaf rounds
     stamps::lap(7);
     const uint32_t wbase = (uint32_t)(p.n_nodes + 8 * p.n_walk + 4 * oct * p.n_wide) * (uint32_t)sizeof(Node);
-    const int sx = oct & 1, sy = (oct >> 1) & 1, sz = oct >> 2, pshift = 8 * (oct & 3);
-    const bool phi = oct >= 4;
+    const int sx = oct & 1, sy = (oct >> 1) & 1, sz = oct >> 2;
     lds_i16* top = stk;    // the next free stack entry (entries are BLK apart)
     int cur = 0;           // the root
     int parked = -1;       // absolute Node index of the parked leaf
@@ -690,37 +693,40 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         }
         if (cur >= 0) {
             if (STATS) cnt.nodes++;
-            uint32_t perm = 0xE4u;   // slots 0..3 already near-first (octant copy)
-            const WideNode n = LDST ? load_wide_lds(tree, cur, sx, sy, sz, pshift, phi, perm)
-                                    : load_wide(rsrc, wbase + (uint32_t)cur * 128u);
+            const WideNode n = LDST ? load_wide_lds(tree, cur, sx, sy, sz) : load_wide(rsrc, wbase + (uint32_t)cur * 128u);
             const f2v e01[3] = {n.e[0][0], n.e[1][0], n.e[2][0]}, x01[3] = {n.x[0][0], n.x[1][0], n.x[2][0]};
             const f2v e23[3] = {n.e[0][1], n.e[1][1], n.e[2][1]}, x23[3] = {n.x[0][1], n.x[1][1], n.x[2][1]};
-            const uint32_t m = wide_pair(e01, x01, ray, limit) | (wide_pair(e23, x23, ray, limit) << 2);
-            // Children in the ray's near-first order (rank k = 0 nearest): hit bits hk and refs
-            // rk.  The nearest hit child is walked next; the other hits are pushed, far ones
-            // first, without branches: every candidate is written at the top and the top moves
-            // past it only when it is pushed (the host bounds the depth, so the write at an
-            // unmoved top stays inside the lane's stack).
-            uint32_t hk = 0;
-            int rk[4];
+            float lo[4];
+            const uint32_t m = wide_pair(e01, x01, ray, limit, lo[0], lo[1]) |
+                               (wide_pair(e23, x23, ray, limit, lo[2], lo[3]) << 2);
+            // The hit child walked next: on the LDS image the one with the nearest entry
+            // distance (first slot on ties), on an octant copy the first in its near-first
+            // slot order.  The other hits are pushed (slot 3 first) without branches: every
+            // slot is written at the top, and the top moves past it only when it is pushed
+            // (the host bounds the depth, so a write at an unmoved top stays inside the
+            // lane's stack).
+            int bk;
+            if (LDST) {
+                bk = 0;
+                float bd = (m & 1u) ? lo[0] : __builtin_inff();
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t slot = LDST ? (perm >> (2 * k)) & 3u : (uint32_t)k;
-                hk |= ((m >> slot) & 1u) << k;
-                rk[k] = LDST ? (slot & 2u ? (slot & 1u ? n.ref[3] : n.ref[2]) : (slot & 1u ? n.ref[1] : n.ref[0]))
-                             : n.ref[k];
+                for (int k = 1; k < 4; ++k) {
+                    const float d = ((m >> k) & 1u) ? lo[k] : __builtin_inff();
+                    const bool closer = d < bd;
+                    bd = closer ? d : bd;
+                    bk = closer ? k : bk;
+                }
+                if (bd == __builtin_inff()) bk = __builtin_ctz(m | 16u);   // no finite distance
+            } else {
+                bk = __builtin_ctz(m | 16u);
             }
 #pragma unroll
-            for (int k = 3; k >= 1; --k) {
-                const bool push = ((hk >> k) & 1u) && (hk & ((1u << k) - 1u));
-                *top = (int16_t)rk[k];
-                top += push ? BLK : 0;
+            for (int k = 3; k >= 0; --k) {
+                *top = (int16_t)n.ref[k];
+                top += (((m >> k) & 1u) && k != bk) ? BLK : 0;
             }
-            const uint32_t first = __builtin_ctz(hk | 16u);   // 4: no child hit
-            const int n01 = (first & 1u) ? rk[1] : rk[0], n23 = (first & 1u) ? rk[3] : rk[2];
-            int next = (first & 2u) ? n23 : n01;
-            if (hk == 0) next = pop();
-            cur = next;
+            const int n01 = (bk & 1) ? n.ref[1] : n.ref[0], n23 = (bk & 1) ? n.ref[3] : n.ref[2];
+            cur = m == 0 ? pop() : ((bk & 2) ? n23 : n01);
             if (cur <= -2 && parked < 0) {   // park the nearest leaf at once
                 parked = p.n_nodes + ~cur;
                 cur = pop();
