@@ -1028,6 +1028,9 @@ int cpt_bind_texture(cpt_ctx* c, uint64_t handle, const uint8_t* rgba, int logic
 int cpt_set_frame(cpt_ctx* c, int width, int height, const int32_t* rows, int n_rows) {
     if (!c) return CPT_ERR_INVALID_ARG;
     if (width <= 0 || height <= 0) return fail(c, CPT_ERR_INVALID_ARG, "cpt_set_frame: %dx%d", width, height);
+    // the megakernel keeps a lane's pixel as 16-bit x / y and a 32-bit index
+    if (width > 65535 || height > 65535)
+        return fail(c, CPT_ERR_INVALID_ARG, "cpt_set_frame: %dx%d exceeds 65535 pixels per axis", width, height);
     std::vector<int32_t> r;
     if (rows) {
         if (n_rows < 0) return fail(c, CPT_ERR_INVALID_ARG, "cpt_set_frame: n_rows %d", n_rows);

@@ -38,8 +38,8 @@ namespace cpt {
 // primitive tests) added to its tile's cost.
 // ======================================================================================
 struct Lane {
-    int x, y;
-    size_t pix;
+    uint32_t xy;     // x | y << 16 (frames are < 65536 pixels wide and high)
+    uint32_t pix;    // context pixel index (frames are < 2^32 pixels)
     uint32_t tile;
     Xorwow s;
     v3 sum;
@@ -56,6 +56,13 @@ __device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int&
     ri = (int)(tile / tiles_x) * 8 + (int)(k >> 3);
     return x < p.width && ri < p.n_rows;
 }
+
+// LDST: a round's walks are suspended once at most this many lanes of the wave still walk
+// (cpt_path.hpp trace_wide).
+#ifndef CPT_SUSPEND_AT
+#define CPT_SUSPEND_AT 8
+#endif
+constexpr int SUSPEND_AT = CPT_SUSPEND_AT;
 
 // Deferred sky fetches run when this many 64ths of the tracing lanes hold one.
 #ifndef CPT_DEFER_MISS_ROUND
@@ -106,6 +113,8 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     __shared__ float pending_q[9 * BLK];
     float* const pq = pending_q + threadIdx.x;
     bool pend = false;
+    WalkState ws;          // the lane's suspended walk, if any
+    ws.active = false;
     stamps::init();
     for (;;) {
         stamps::lap(5);
@@ -125,15 +134,14 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                     const uint32_t id = base + rank;
                     int x, ri;
                     if (id < n_work && decode_pixel(p, id, x, ri, L.tile)) {
-                        L.x = x;
-                        L.y = p.rows[ri];
-                        L.pix = (size_t)ri * p.width + x;
+                        L.xy = (uint32_t)x | ((uint32_t)p.rows[ri] << 16);
+                        L.pix = (uint32_t)ri * (uint32_t)p.width + (uint32_t)x;
                         L.s.v0 = p.rng[L.pix];
                         L.s.v1 = p.rng[npix + L.pix];
-                        L.s.v2 = p.rng[2 * npix + L.pix];
-                        L.s.v3 = p.rng[3 * npix + L.pix];
-                        L.s.v4 = p.rng[4 * npix + L.pix];
-                        L.s.d = p.rng[5 * npix + L.pix];
+                        L.s.v2 = p.rng[2 * npix + (size_t)L.pix];
+                        L.s.v3 = p.rng[3 * npix + (size_t)L.pix];
+                        L.s.v4 = p.rng[4 * npix + (size_t)L.pix];
+                        L.s.d = p.rng[5 * npix + (size_t)L.pix];
                         float4 acc = (p.accumulate && !PROBE) ? p.accum[L.pix] : make_float4(0.f, 0.f, 0.f, 0.f);
                         L.sum = mk(acc.x, acc.y, acc.z);
                         L.passes = acc.w;
@@ -144,14 +152,14 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                         if (max_depth == 0) {
                             // while (0 < 0) never runs: each pass is RayGen's draws and zero radiance
                             for (; L.left > 0; --L.left) {
-                                (void)ray_gen(p, L.x, L.y, L.s);
+                                (void)ray_gen(p, (int)(L.xy & 0xffffu), (int)(L.xy >> 16), L.s);
                                 L.sum = L.sum + mk1(0.f);
                                 L.passes += 1.0f;
                             }
                         }
                         busy = true;
                         if (L.left > 0) {
-                            ray = ray_gen(p, L.x, L.y, L.s);
+                            ray = ray_gen(p, (int)(L.xy & 0xffffu), (int)(L.xy >> 16), L.s);
                             att = mk1(1.f);
                             rad = mk1(0.f);
                             depth = 0;
@@ -165,16 +173,22 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         }
         stamps::lap(0);
         if (!__any(busy)) break;
+        Hit h;
+        int code = -1;
+        int tr = 2;
         if (busy && L.left > 0) {
-            // ---- one path segment: TraceRay + ClosetHit/Miss (path_tracer.cu:141-169) ----
-            Hit h;
-            int code = -1;
-            if (COUNT) cnt.segments++;
+            // ---- one path segment: TraceRay (path_tracer.cu:141-158); a walk suspended in an
+            // earlier round resumes here (LDST: trace_wide's suspension) -------------------
+            if (COUNT && !ws.active) cnt.segments++;
             const RayK rk = make_rayk(ray);
             const bool finite_ray = !(ray.o.x != ray.o.x || ray.o.y != ray.o.y || ray.o.z != ray.o.z ||
                                       ray.d.x != ray.d.x || ray.d.y != ray.d.y || ray.d.z != ray.d.z);
-            const bool hit = trace_segment<COUNT, BLK, LDST>(p, rk, finite_ray, h, code, cnt, s_tree);
-            stamps::lap(3);
+            tr = trace_segment<COUNT, BLK, LDST>(p, rk, finite_ray, h, code, cnt, s_tree, ws, LDST ? SUSPEND_AT : 0);
+        }
+        stamps::lap(3);
+        if (busy && L.left > 0 && tr != 2) {
+            // ---- ClosetHit / Miss and the path bookkeeping (path_tracer.cu:159-169) --------
+            const bool hit = tr == 1;
             Shade sh;
             v3 attr_normal;
             if (hit) {
@@ -238,7 +252,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 L.passes += 1.0f;
                 if (AUX) { first_normal = nrm_acc; first_depth = dep_acc; }
                 if (--L.left > 0) {
-                    ray = ray_gen(p, L.x, L.y, L.s);
+                    ray = ray_gen(p, (int)(L.xy & 0xffffu), (int)(L.xy >> 16), L.s);
                     att = mk1(1.f);
                     rad = mk1(0.f);
                     depth = 0;
@@ -256,17 +270,17 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 // ---- pixel finished: write back (path_tracer.cu:172-174) -----------------
                 p.accum[L.pix] = make_float4(L.sum.x, L.sum.y, L.sum.z, L.passes);
                 if (AUX && p.spp > 0) {
-                    p.normal[3 * L.pix + 0] = first_normal.x;
-                    p.normal[3 * L.pix + 1] = first_normal.y;
-                    p.normal[3 * L.pix + 2] = first_normal.z;
+                    p.normal[3 * (size_t)L.pix + 0] = first_normal.x;
+                    p.normal[3 * (size_t)L.pix + 1] = first_normal.y;
+                    p.normal[3 * (size_t)L.pix + 2] = first_normal.z;
                     p.depth[L.pix] = first_depth;
                 }
                 p.rng[L.pix] = L.s.v0;
                 p.rng[npix + L.pix] = L.s.v1;
-                p.rng[2 * npix + L.pix] = L.s.v2;
-                p.rng[3 * npix + L.pix] = L.s.v3;
-                p.rng[4 * npix + L.pix] = L.s.v4;
-                p.rng[5 * npix + L.pix] = L.s.d;
+                p.rng[2 * npix + (size_t)L.pix] = L.s.v2;
+                p.rng[3 * npix + (size_t)L.pix] = L.s.v3;
+                p.rng[4 * npix + (size_t)L.pix] = L.s.v4;
+                p.rng[5 * npix + (size_t)L.pix] = L.s.d;
             }
             busy = false;
         }

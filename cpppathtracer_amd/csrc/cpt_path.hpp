@@ -106,7 +106,8 @@ __device__ inline v3 tex2d(const KParams& p, float u, float v) {
 struct RayK {
     v3 o, d;
     float tmin;
-    double yx, yy, yz;   // 1/d.x, 1/d.y, 1/d.z   (slab planes; d.y also for caps / platform)
+    double yx, yy, yz;   // 1/d.x, 1/d.y, 1/d.z   (exact slab planes; d.y also for caps / platform);
+                         // yx and yz are filled by with_slab() where an exact slab test runs
     double ya;           // 1/dot(d,d)            (sphere roots, object.cu:15-20)
     double yc;           // 1/(dx*dx + dz*dz)     (cylinder side roots, object.cu:69-79)
     float ix, iy, iz;    // f32 1/d per axis for the ordered walk's conservative slabs; 0 = the
@@ -120,9 +121,9 @@ __device__ __forceinline__ RayK make_rayk(const Ray& r) {
     k.o = r.o;
     k.d = r.d;
     k.tmin = r.tmin;
-    k.yx = rcp_d(r.d.x);
+    k.yx = 0.0;   // with_slab()
     k.yy = rcp_d(r.d.y);
-    k.yz = rcp_d(r.d.z);
+    k.yz = 0.0;
     k.ya = rcp_d(dot(r.d, r.d));
     k.yc = rcp_d(r.d.x * r.d.x + r.d.z * r.d.z);
     k.ix = __builtin_fabsf(r.d.x) >= 1e-30f ? 1.0f / r.d.x : 0.0f;
@@ -132,6 +133,15 @@ __device__ __forceinline__ RayK make_rayk(const Ray& r) {
     k.by = k.iy != 0.0f ? 0.0f : DEFAULT_RAY_TMAX * 2;
     k.bz = k.iz != 0.0f ? 0.0f : DEFAULT_RAY_TMAX * 2;
     k.t3 = (r.tmin - 1e-4f) * (1.0f + 2e-3f);
+    return k;
+}
+
+// The exact slab test's reciprocals, computed where one runs (the winner certificate and the
+// reference walk), so the ordered walk does not carry them.
+__device__ __forceinline__ RayK with_slab(const RayK& k0) {
+    RayK k = k0;
+    k.yx = rcp_d(k0.d.x);
+    k.yz = rcp_d(k0.d.z);
     return k;
 }
 
@@ -550,7 +560,7 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
         // with every primitive it tests also tested here, it keeps the same one.
         Node box;
         leaf_aabb(w, box);
-        if (slab_reject<FAST>(box, ray, tmax)) return -1;
+        if (slab_reject<FAST>(box, with_slab(ray), tmax)) return -1;
     }
     h = hit_attributes(w, ray, tmax, kind);
     code_out = w.code;
@@ -649,43 +659,75 @@ __device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], co
 // stack holds 16-bit entries (BLK lanes x CPT_WSTACK x 2 B per block).
 // LDST: the nodes come from the block's LDS image `tree` (k_megakernel stages it), else from
 // the ray's octant copy in HBM through `rsrc`.
+// A lane's wide walk in progress, kept across rounds of the megakernel when the walk is
+// suspended (trace_wide's `suspend_at`): the stack itself stays in LDS.
+struct WalkState {
+    lds_i16* top;
+    int cur, parked, best, kind, best_rank;
+    float tmax, limit;
+    bool active;   // a walk is in progress (suspended in an earlier round)
+};
+
+// Suspension (the megakernel): once at most `suspend_at` lanes of the wave still walk and at
+// least SUSPEND_MIN_DONE lanes of this call have finished theirs, the call returns 2 for the
+// lanes still walking (their state in `ws`) and the finished lanes go on to shade and start
+// their next segment; the suspended lanes resume in the next round, beside them.  The walk's
+// tail -- iterations with a few working lanes -- then overlaps other lanes' work.  At least
+// one iteration runs per call, so every walk progresses.  The result does not depend on
+// where a walk is suspended: it is the closest hit over a superset of the primitives the
+// reference tests, whatever the culling limit was at each node (DESIGN.md §Ordered walk).
+#ifndef CPT_SUSPEND_MIN_DONE
+#define CPT_SUSPEND_MIN_DONE 32
+#endif
+constexpr int SUSPEND_MIN_DONE = CPT_SUSPEND_MIN_DONE;
+
 template <bool STATS, int BLK = WIDE_LANES, bool LDST = false>
 __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc_t rsrc, int oct, const RayK& ray,
-                                          Hit& h, int& code_out, Counters& cnt, const uint4* tree) {
+                                          Hit& h, int& code_out, Counters& cnt, const uint4* tree, WalkState& ws,
+                                          int suspend_at) {
     __shared__ int16_t wstack[CPT_WSTACK * BLK];
     // an LDS-typed pointer: 32-bit ds_read/ds_write addressing (a generic pointer costs a
     // 64-bit multiply-add per push and pop)
     lds_i16* const stk = (lds_i16*)wstack + threadIdx.x;
     const BufSrc nodes{rsrc, 0u};   // leaves by absolute Node index
     constexpr int NONE = -1;
-    float tmax = DEFAULT_RAY_TMAX;
-    int best = -1, kind = 0;
-    int best_rank = 0x7fffffff;
+    const uint64_t participants = __ballot(1);
     stamps::lap(6);
-    // the platforms (every ray tests them) run first, by the whole wave at once, so the walk
-    // starts with their tmax; same rank rule, so the order does not matter
-    for (int k = 0; k < p.n_unb; ++k) {
-        if (STATS) cnt.prims++;
-        const Node pl = nodes(p.n_nodes + k);
-        int kk;
-        if (ranked_leaf_test<true, true, false>(pl, ray, tmax, kk, best_rank)) {
-            best = p.n_nodes + k;
-            kind = kk;
+    if (!ws.active) {
+        // a new walk: the platforms (every ray tests them) first, by the whole wave at once,
+        // so the walk starts with their tmax; same rank rule, so the order does not matter
+        ws.tmax = DEFAULT_RAY_TMAX;
+        ws.best = -1;
+        ws.kind = 0;
+        ws.best_rank = 0x7fffffff;
+        for (int k = 0; k < p.n_unb; ++k) {
+            if (STATS) cnt.prims++;
+            const Node pl = nodes(p.n_nodes + k);
+            int kk;
+            if (ranked_leaf_test<true, true, false>(pl, ray, ws.tmax, kk, ws.best_rank)) {
+                ws.best = p.n_nodes + k;
+                ws.kind = kk;
+            }
         }
+        ws.limit = walk_limit(ws.tmax);   // changes only in leaf rounds
+        ws.top = stk;
+        ws.cur = 0;        // the root
+        ws.parked = -1;    // absolute Node index of the parked leaf
     }
-    float limit = walk_limit(tmax);   // changes only in leaf rounds
     stamps::lap(7);
+    float tmax = ws.tmax, limit = ws.limit;
+    int best = ws.best, kind = ws.kind, best_rank = ws.best_rank;
+    lds_i16* top = ws.top;   // the next free stack entry (entries are BLK apart)
+    int cur = ws.cur, parked = ws.parked;
     const uint32_t wbase = (uint32_t)(p.n_nodes + 8 * p.n_walk + 4 * oct * p.n_wide) * (uint32_t)sizeof(Node);
     const int sx = oct & 1, sy = (oct >> 1) & 1, sz = oct >> 2;
-    lds_i16* top = stk;    // the next free stack entry (entries are BLK apart)
-    int cur = 0;           // the root
-    int parked = -1;       // absolute Node index of the parked leaf
     auto pop = [&]() -> int {
         if (top == stk) return NONE;
         top -= BLK;
         return (int)*top;
     };
-    for (;;) {
+    bool working = true;
+    for (int it = 0;; ++it) {
         stamps::count(9);
         if (cur <= -2 && parked < 0) {
             parked = p.n_nodes + ~cur;
@@ -732,11 +774,14 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
                 cur = pop();
             }
         }
-        const bool working = parked >= 0 || cur != NONE;
+        working = parked >= 0 || cur != NONE;
         const bool stopped = parked >= 0 && (cur == NONE || cur <= -2);
         const uint64_t w = __ballot(working);
-        stamps::lap(1);
+        const bool tail = __popcll(w) <= 8;   // stamps only: the walk's tail (few lanes left)
+        stamps::lap(tail ? 11 : 1);
+        if (tail) stamps::count(13);
         if (!w) break;
+        if (__popcll(w) <= suspend_at && __popcll(participants & ~w) >= SUSPEND_MIN_DONE && it > 0) break;
         if (__popcll(__ballot(stopped)) * 64 >= SPEC_LEAF_ROUND * __popcll(w) && parked >= 0) {
             stamps::count(10);
             if (STATS) cnt.prims++;
@@ -750,13 +795,19 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
             }
             parked = -1;
         }
-        stamps::lap(2);
+        stamps::lap(tail ? 12 : 2);
+    }
+    ws.active = working;
+    if (working) {   // suspended
+        ws.tmax = tmax; ws.limit = limit; ws.best = best; ws.kind = kind; ws.best_rank = best_rank;
+        ws.top = top; ws.cur = cur; ws.parked = parked;
+        return 2;
     }
     if (best < 0) return 0;
     const Node wn = nodes(best);
     Node box;
     leaf_aabb(wn, box);
-    if (slab_reject<true>(box, ray, tmax)) return -1;
+    if (slab_reject<true>(box, with_slab(ray), tmax)) return -1;
     h = hit_attributes(wn, ray, tmax, kind);
     code_out = wn.code;
     return 1;
@@ -766,25 +817,37 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
 // and the reference-order fallback (CPT_TRAVERSAL_ORDERED): the 4-wide walk with parked
 // leaves (ordered == 1 and a wide tree), else the binary octant orders testing each leaf
 // where the walk meets it.
+// Returns 1 hit, 0 miss, or 2 when the walk was suspended (only with suspend_at > 0; the
+// lane calls again in a later round with the same ray and `ws`).
 template <bool STATS, int BLK = WIDE_LANES, bool LDST = false>
-__device__ __forceinline__ bool trace_segment(const KParams& p, const RayK& rk, bool finite, Hit& h, int& code,
-                                              Counters& cnt, const uint4* tree = nullptr) {
+__device__ __forceinline__ int trace_segment(const KParams& p, const RayK& rk, bool finite, Hit& h, int& code,
+                                             Counters& cnt, const uint4* tree, WalkState& ws, int suspend_at) {
     const __amdgpu_buffer_rsrc_t rsrc = node_rsrc(p);
     if (p.ordered && __builtin_expect(finite, 1)) {
         int n, r;
         if (p.ordered == 1 && p.n_wide > 0) {
             const int oct = (rk.d.x < 0.f ? 1 : 0) | (rk.d.y < 0.f ? 2 : 0) | (rk.d.z < 0.f ? 4 : 0);
-            r = trace_wide<STATS, BLK, LDST>(p, rsrc, oct, rk, h, code, cnt, tree);
+            r = trace_wide<STATS, BLK, LDST>(p, rsrc, oct, rk, h, code, cnt, tree, ws, suspend_at);
         } else {
             const BufSrc order{rsrc, walk_order(p, rk.d, n) * (uint32_t)sizeof(Node)};
             r = trace<STATS, true, true>(order, n, rk, h, code, cnt);
         }
-        if (__builtin_expect(r >= 0, 1)) return r > 0;
+        if (__builtin_expect(r >= 0, 1)) return r;
         if (STATS) cnt.fallbacks++;
     }
     const BufSrc ref{rsrc, 0u};
-    if (__builtin_expect(finite, 1)) return trace<STATS, true>(ref, p.n_nodes, rk, h, code, cnt) > 0;
-    return trace<STATS, false>(ref, p.n_nodes, rk, h, code, cnt) > 0;
+    const RayK rs = with_slab(rk);
+    if (__builtin_expect(finite, 1)) return trace<STATS, true>(ref, p.n_nodes, rs, h, code, cnt) > 0 ? 1 : 0;
+    return trace<STATS, false>(ref, p.n_nodes, rs, h, code, cnt) > 0 ? 1 : 0;
+}
+
+// The same without suspension (a walk always completes).
+template <bool STATS, int BLK = WIDE_LANES, bool LDST = false>
+__device__ __forceinline__ bool trace_segment(const KParams& p, const RayK& rk, bool finite, Hit& h, int& code,
+                                              Counters& cnt, const uint4* tree = nullptr) {
+    WalkState ws;
+    ws.active = false;
+    return trace_segment<STATS, BLK, LDST>(p, rk, finite, h, code, cnt, tree, ws, 0) == 1;
 }
 
 // ======================================================================================

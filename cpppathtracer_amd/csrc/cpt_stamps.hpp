@@ -4,7 +4,8 @@
 // lap(i) adds the s_memtime cycles since the wave's previous lap to slot i; count(i) adds 1.
 // Slots (tools/stamps.py): 0 refill, 1 walk: node visits, 2 walk: leaf rounds, 3 certificate +
 // hit attributes, 4 hit shading, 5 rest of the loop (sky, pass bookkeeping, RayGen, write-back),
-// 6 ray setup, 7 platforms; counts: 8 outer rounds, 9 walk iterations, 10 leaf rounds.
+// 6 ray setup, 7 platforms; counts: 8 outer rounds, 9 walk iterations, 10 leaf rounds;
+// 11 / 12: slots 1 / 2 in walk iterations with <= 8 working lanes (the tail), 13 their count.
 // The block's per-wave slots live in LDS; flush() adds them to out[0..15].
 #pragma once
 

@@ -38,7 +38,7 @@ r.reset_stats()
 r.render(cam, spp, cfg["depth"], stats=True, sync=True, ordered=True, schedule="cost")
 c = r.diag_counters()
 st = dict(zip(["segments", "nodes", "prims", "hits", "misses"], r.raw_counters()[:5]))
-tot = sum(c[:8])
+tot = sum(c[:8]) + c[11] + c[12]
 rounds, iters, leaf_rounds = c[8], c[9], c[10]
 out = {
     "config": cfg, "spp": spp, "counts": st,
@@ -47,8 +47,10 @@ out = {
     "cycles_per_round": round(tot / max(1, rounds), 1),
     "walk_iterations_per_round": round(iters / max(1, rounds), 2),
     "leaf_rounds_per_round": round(leaf_rounds / max(1, rounds), 2),
-    "cycles_per_walk_iteration": round((c[1] + c[2]) / max(1, iters), 1),
-    "cycles_per_leaf_round": round(c[2] / max(1, leaf_rounds), 1),
+    "cycles_per_walk_iteration": round((c[1] + c[2] + c[11] + c[12]) / max(1, iters), 1),
+    "cycles_per_leaf_round": round((c[2] + c[12]) / max(1, leaf_rounds), 1),
+    "tail_share": round((c[11] + c[12]) / tot, 4),
+    "tail_iterations_per_round": round(c[13] / max(1, rounds), 2),
     "lanes_per_round": round(st["segments"] / max(1, rounds), 2),
     "lanes_per_walk_iteration": round(st["nodes"] / max(1, iters), 2),
 }
