@@ -35,6 +35,7 @@ sys.path.insert(0, REPO)
 METRIC = "Mpaths/sec (pixels×spp/s) at 1920×1080; achieved HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 WIDE_NODE_BYTES = 112   # a 4-wide walk node visit loads 7 x dwordx4 (cpt_path.hpp load_wide)
+LDS_TREE_NODES = 512    # k_megakernel stages the wide tree in LDS up to this size (cpt_path.hpp)
 
 
 def parse_args(argv=None):
@@ -184,7 +185,7 @@ def run(args):
     import torch
     import torch.distributed as dist
 
-    from cpppathtracer_amd import Renderer, camera_get_copy, scenes, texture_io, tiling
+    from cpppathtracer_amd import Renderer, camera_get_copy, multigpu, scenes, texture_io, tiling
 
     world = check_world(args, os.environ)
     rank = int(os.environ.get("RANK", "0"))
@@ -245,10 +246,7 @@ def run(args):
     t_init = time.perf_counter() - t_init
 
     npix_local = rows.size * W
-    max_rows = tiling.max_rows(H, world)
-    send = torch.zeros((max_rows * W, 4), dtype=torch.float32, device=dev)
-    gathered = torch.zeros((world * max_rows * W, 4), dtype=torch.float32, device=dev) if world > 1 else None
-    stitch_idx = torch.from_numpy(tiling.stitch_index(H, W, world)).to(dev) if world > 1 else None
+    gather = multigpu.TileGather(W, H, world, rank, dev, backend) if world > 1 else None
     kernel_events = []
     ordered = args.walk == "ordered"
     schedule = args.schedule if args.path == "megakernel" else "tiles"
@@ -262,14 +260,7 @@ def run(args):
         if world > 1:
             # all-gather of the fp32 tiles (RCCL over xGMI), then the on-device stitch into the
             # full framebuffer (every rank holds a copy after the all-gather)
-            r.copy_accum_device(send.data_ptr(), npix_local * 16)
-            if backend == "nccl":
-                dist.all_gather_into_tensor(gathered, send)
-            else:
-                g_host = gathered.cpu()
-                dist.all_gather_into_tensor(g_host, send.cpu())
-                gathered.copy_(g_host)
-            return gathered.view(world * max_rows, W, 4).index_select(0, stitch_idx)
+            return gather(r)
         return None
 
     # Counting passes (same pixels, same seed; not timed) for the algorithmic byte model: the
@@ -291,7 +282,11 @@ def run(args):
     walk_info = r.walk_info()
     hbm_ceiling = r.measure_read_bandwidth(4 << 30, 10) if not args.no_hbm_probe else None
     wide = ordered and walk_info["n_wide"] > 0
-    walk_node_bytes = WIDE_NODE_BYTES if wide else 32
+    # Global-memory bytes per node visit of the executed walk: the 4-wide nodes come from the
+    # workgroup's LDS image when it fits (loaded once per workgroup per launch, priced below), so
+    # a visit moves no global-memory bytes; otherwise 112 B per wide visit, 32 B per binary one.
+    lds_image = wide and args.path == "megakernel" and walk_info["n_wide"] <= LDS_TREE_NODES
+    walk_node_bytes = 0 if lds_image else (WIDE_NODE_BYTES if wide else 32)
     st = walk_counts = walk_diff = None
     if not args.no_count:
         st = count_pass(False)
@@ -370,6 +365,9 @@ def run(args):
             # over the max-over-ranks render time.
             share = npix_local / float(W * H)
             bytes_launch = byte_model(walk_counts, paths_total, walk_node_bytes) * share
+            if lds_image:   # every workgroup stages the image once (one workgroup per CU)
+                bytes_launch += walk_info["n_wide"] * WIDE_NODE_BYTES * torch.cuda.get_device_properties(
+                    dev).multi_processor_count
             bytes_ref = byte_model(st, paths_total) * share
             kms = avg_kernel_ms_max if world > 1 else avg_kernel_ms
             t_render = kms * max(1, launches) / 1e3   # the byte counts cover every launch of the render
@@ -389,8 +387,12 @@ def run(args):
                 "kernel_avg_ms": round(kms, 3),
                 "launches_per_step": launches,
                 "bytes_per_launch": int(bytes_launch),
-                "byte_model": f"SURVEY.md 8(d): 76 S + {walk_node_bytes} nodes + 32 prims + 40 hits + 16 misses + 16 P "
-                              f"on the executed walk's counts ({'4-wide walk tree: 7 x 16 B loaded per node visit' if wide else 'binary nodes'})",
+                "byte_model": (f"SURVEY.md 8(d): 76 S + {walk_node_bytes} nodes + 32 prims + 40 hits + 16 misses + 16 P "
+                               "on the executed walk's counts" +
+                               (" (4-wide nodes read from the workgroup's LDS image: no global-memory bytes per "
+                                "visit, + the image's 112 B x n_wide once per workgroup)" if lds_image else
+                                " (4-wide walk tree: 7 x 16 B loaded per node visit)" if wide else " (binary nodes)")),
+                "lds_node_bytes_per_launch": int(walk_counts["nodes"] * WIDE_NODE_BYTES * share) if lds_image else 0,
                 "walk_info": walk_info,
                 "walk_counts": walk_counts,
                 "reference_counts": st,

@@ -631,19 +631,21 @@ __device__ __forceinline__ WideNode load_wide_lds(const uint4* tree, int cur, in
     return n;
 }
 
-// Hit mask of the four children: slab_reject_octant for each, two children per packed op.
+// Hit mask of children (a, b) of a pair: slab_reject_octant for each, in scalar f32 ops (the
+// packed v_pk_add/v_pk_fma form needs the ray's o, 1/d and bias as register pairs: 9 more
+// VGPRs, spilled, and measured 0.7% slower).
 __device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], const RayK& ray, float limit,
                                               float& lo_a, float& lo_b) {
-    const f2v ox = {ray.o.x, ray.o.x}, oy = {ray.o.y, ray.o.y}, oz = {ray.o.z, ray.o.z};
-    const f2v ix = {ray.ix, ray.ix}, iy = {ray.iy, ray.iy}, iz = {ray.iz, ray.iz};
-    const f2v bx = {ray.bx, ray.bx}, by = {ray.by, ray.by}, bz = {ray.bz, ray.bz};
-    const f2v tnx = __builtin_elementwise_fma(e[0] - ox, ix, -bx), tfx = __builtin_elementwise_fma(x[0] - ox, ix, bx);
-    const f2v tny = __builtin_elementwise_fma(e[1] - oy, iy, -by), tfy = __builtin_elementwise_fma(x[1] - oy, iy, by);
-    const f2v tnz = __builtin_elementwise_fma(e[2] - oz, iz, -bz), tfz = __builtin_elementwise_fma(x[2] - oz, iz, bz);
-    const float lo0 = __builtin_fmaxf(__builtin_fmaxf(tnx.x, tny.x), tnz.x);
-    const float hi0 = __builtin_fminf(__builtin_fminf(tfx.x, tfy.x), tfz.x);
-    const float lo1 = __builtin_fmaxf(__builtin_fmaxf(tnx.y, tny.y), tnz.y);
-    const float hi1 = __builtin_fminf(__builtin_fminf(tfx.y, tfy.y), tfz.y);
+    auto near = [&](float pl, float o, float i, float b) { return __builtin_fmaf(pl - o, i, -b); };
+    auto far = [&](float pl, float o, float i, float b) { return __builtin_fmaf(pl - o, i, b); };
+    const float lo0 = __builtin_fmaxf(__builtin_fmaxf(near(e[0].x, ray.o.x, ray.ix, ray.bx), near(e[1].x, ray.o.y, ray.iy, ray.by)),
+                                      near(e[2].x, ray.o.z, ray.iz, ray.bz));
+    const float hi0 = __builtin_fminf(__builtin_fminf(far(x[0].x, ray.o.x, ray.ix, ray.bx), far(x[1].x, ray.o.y, ray.iy, ray.by)),
+                                      far(x[2].x, ray.o.z, ray.iz, ray.bz));
+    const float lo1 = __builtin_fmaxf(__builtin_fmaxf(near(e[0].y, ray.o.x, ray.ix, ray.bx), near(e[1].y, ray.o.y, ray.iy, ray.by)),
+                                      near(e[2].y, ray.o.z, ray.iz, ray.bz));
+    const float hi1 = __builtin_fminf(__builtin_fminf(far(x[0].y, ray.o.x, ray.ix, ray.bx), far(x[1].y, ray.o.y, ray.iy, ray.by)),
+                                      far(x[2].y, ray.o.z, ray.iz, ray.bz));
     const float m0 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo0) + __builtin_fabsf(hi0), 2.0f * WALK_MARGIN_ABS);
     const float m1 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo1) + __builtin_fabsf(hi1), 2.0f * WALK_MARGIN_ABS);
     const bool rej0 = lo0 - hi0 > m0 || lo0 > limit || hi0 < ray.t3;
@@ -715,10 +717,15 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         ws.parked = -1;    // absolute Node index of the parked leaf
     }
     stamps::lap(7);
-    float tmax = ws.tmax, limit = ws.limit;
-    int best = ws.best, kind = ws.kind, best_rank = ws.best_rank;
-    lds_i16* top = ws.top;   // the next free stack entry (entries are BLK apart)
-    int cur = ws.cur, parked = ws.parked;
+    // the walk runs on the lane's WalkState itself (one copy of it lives across the round)
+    float& tmax = ws.tmax;
+    float& limit = ws.limit;
+    int& best = ws.best;
+    int& kind = ws.kind;
+    int& best_rank = ws.best_rank;
+    lds_i16*& top = ws.top;   // the next free stack entry (entries are BLK apart)
+    int& cur = ws.cur;
+    int& parked = ws.parked;
     const uint32_t wbase = (uint32_t)(p.n_nodes + 8 * p.n_walk + 4 * oct * p.n_wide) * (uint32_t)sizeof(Node);
     const int sx = oct & 1, sy = (oct >> 1) & 1, sz = oct >> 2;
     auto pop = [&]() -> int {
@@ -798,11 +805,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         stamps::lap(tail ? 12 : 2);
     }
     ws.active = working;
-    if (working) {   // suspended
-        ws.tmax = tmax; ws.limit = limit; ws.best = best; ws.kind = kind; ws.best_rank = best_rank;
-        ws.top = top; ws.cur = cur; ws.parked = parked;
-        return 2;
-    }
+    if (working) return 2;   // suspended
     if (best < 0) return 0;
     const Node wn = nodes(best);
     Node box;

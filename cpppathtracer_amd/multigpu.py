@@ -1,0 +1,40 @@
+"""Row-tiled multi-GPU frame assembly: one process per GPU renders the rows
+of its interleaved 8-row blocks (tiling.partition_rows), then one all-gather of the fp32
+accumulator tiles (RCCL over xGMI; gloo host copies for CPU/shared-GPU rehearsals) and an
+on-device row stitch give every rank the full framebuffer.  bench.py's N > 1 step.
+
+A pixel's stream depends only on (seed, x, y) (path_tracer.cu:36-42), so the stitched frame is
+bit-identical to a monolithic render (tests/test_multi_gpu_cpu.py on the oracle,
+tests/test_gpu_multirank.py through libcpt.so).
+"""
+import torch
+import torch.distributed as dist
+
+from . import tiling
+
+
+class TileGather:
+    """Buffers and the collective for one rank's share of a row-tiled frame."""
+
+    def __init__(self, width, height, world, rank, device, backend="nccl"):
+        self.width, self.height, self.world, self.rank = width, height, world, rank
+        self.backend = backend
+        self.rows = tiling.partition_rows(height, world, rank)
+        self.max_rows = tiling.max_rows(height, world)
+        self.send = torch.zeros((self.max_rows * width, 4), dtype=torch.float32, device=device)
+        self.gathered = torch.zeros((world * self.max_rows * width, 4), dtype=torch.float32, device=device)
+        self.stitch_idx = torch.from_numpy(tiling.stitch_index(height, width, world)).to(device)
+
+    def __call__(self, renderer):
+        """The full (height, width, 4) fp32 framebuffer (rgb sums + pass count) after this
+        rank's render: device copy of the local tile, all-gather, row stitch."""
+        renderer.copy_accum_device(self.send.data_ptr(), self.rows.size * self.width * 16)
+        if self.world == 1:
+            return self.send.view(self.max_rows, self.width, 4)[: self.height]
+        if self.backend == "nccl":
+            dist.all_gather_into_tensor(self.gathered, self.send)
+        else:   # gloo: host copies (rehearsal with ranks sharing a GPU)
+            g_host = self.gathered.cpu()
+            dist.all_gather_into_tensor(g_host, self.send.cpu())
+            self.gathered.copy_(g_host)
+        return self.gathered.view(self.world * self.max_rows, self.width, 4).index_select(0, self.stitch_idx)

@@ -2,7 +2,7 @@
 into the JSON bench.py reads (profiles/rocprof_<config>_<path>_<walk>.json).
 
     python tools/rocprof_summary.py <prof dir> <config> <n_rows> <spp> <path> <walk> <schedule> <out.json>
-                                    [kernel substring, default "k_megakernel<false, false, false>"]
+                                    [kernel substring, default "k_megakernel<false, false, false" (the timed instantiation)]
 
 Per launch of the kernel (averaged over the profiled launches):
   * duration from the kernel trace (trace_kernel_stats.csv);
@@ -74,7 +74,7 @@ def summarise(d, kname):
 
 if __name__ == "__main__":
     d, config, n_rows, spp, path, walk, schedule, out = sys.argv[1:9]
-    kname = sys.argv[9] if len(sys.argv) > 9 else "k_megakernel<false, false, false>"
+    kname = sys.argv[9] if len(sys.argv) > 9 else "k_megakernel<false, false, false"
     res = {"config": config, "n_rows": int(n_rows), "spp": int(spp), "path": path, "walk": walk,
            "schedule": schedule, "source": os.path.relpath(d, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))}
     res.update(summarise(d, kname))
