@@ -304,6 +304,7 @@ struct cpt_ctx {
     int n_walk = 0;                    // nodes of each octant order (walk tree + unbounded leaves)
     int n_wide = 0;                    // 4-wide walk-tree nodes per octant (0: none, binary walk)
     int n_unb = 0;                     // unbounded (platform) leaves at the head of each octant order
+    int n_leaves = 0;                  // the wide tree's leaf array (after its compact image)
     std::vector<Mat> mats_h;           // deduplicated materials (host-staged, see Mat)
     std::vector<int> mat_have_tex;     // per material slot: textured?
     std::vector<uint64_t> mat_tex;     // per material slot: texture handle (textured slots)
@@ -555,7 +556,7 @@ int build(HostBvh& t, const std::vector<cpt_object>& O, std::vector<int>& idx, i
 constexpr int WIDE_STACK = CPT_WSTACK;
 
 int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int n_bvh, int n_unb,
-                   std::vector<Node>& out) {
+                   std::vector<Node>& out, int* n_leaves_out) {
     std::vector<int> wbin;                      // binary node of each wide node
     std::vector<std::vector<int>> kids;         // its children (binary node ids)
     std::vector<int> wide_of(w.nodes.size(), -1);
@@ -594,8 +595,25 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
     if (n_wide > 32767) return 0;
     for (int p : pos0)
         if (p > 32766) return 0;
+    // The leaf array after the compact image (staged in LDS with it when it fits): the
+    // platforms (the head of every octant order), then the walk tree's leaves in the order the
+    // wide nodes first reference them; Node copies of octant 0's inline leaves.  The compact
+    // image refers to leaf i as ~(i + 1) (<= -2, apart from the empty slot's -1).
+    std::vector<int> li_of(w.nodes.size(), -1), leaf_pos;
+    for (int k = 0; k < n_unb; ++k) leaf_pos.push_back(k);
+    for (int id = 0; id < n_wide; ++id)
+        for (int x : kids[id])
+            if (w.nodes[x].is_object && li_of[x] < 0) {
+                li_of[x] = (int)leaf_pos.size();
+                leaf_pos.push_back(pos0[x]);
+            }
+    if ((int)leaf_pos.size() > 32765) return 0;
     const size_t base = out.size();
-    out.resize(base + (size_t)8 * n_wide * 4 + (n_wide * 7 + 1) / 2);
+    const size_t n_compact = (size_t)(n_wide * 7 + 1) / 2;
+    out.resize(base + (size_t)8 * n_wide * 4 + n_compact + leaf_pos.size());
+    for (size_t i = 0; i < leaf_pos.size(); ++i)
+        out[base + (size_t)8 * n_wide * 4 + n_compact + i] = out[(size_t)n_bvh + leaf_pos[i]];
+    *n_leaves_out = (int)leaf_pos.size();
     // The compact image after the eight octant copies (k_megakernel stages it in LDS when it
     // fits, cpt_path.hpp trace_wide): 7 x 16 B per node, one copy for every octant --
     //   [min x][max x][min y][max y][min z][max z] of the four slots (octant 0's order), then
@@ -629,7 +647,7 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
                             const BNode& n = w.nodes[o0[k]];
                             lo = n.bmin;
                             hi = n.bmax;
-                            r = n.is_object ? ~pos0[o0[k]] : wide_of[o0[k]];
+                            r = n.is_object ? ~(li_of[o0[k]] + 1) : wide_of[o0[k]];
                         }
                         const float l3[3] = {lo.x, lo.y, lo.z}, h3[3] = {hi.x, hi.y, hi.z};
                         for (int a = 0; a < 3; ++a) {
@@ -691,7 +709,9 @@ void linearise_all(cpt_ctx* c) {
     }
     c->n_walk = (int)(c->lin.size() - c->n_bvh) / 8;
     c->n_unb = (int)unbounded.size();
-    if (root >= 0 && !w.nodes[root].is_object) c->n_wide = linearise_wide(w, root, pos0, c->n_bvh, c->n_unb, c->lin);
+    c->n_leaves = 0;
+    if (root >= 0 && !w.nodes[root].is_object)
+        c->n_wide = linearise_wide(w, root, pos0, c->n_bvh, c->n_unb, c->lin, &c->n_leaves);
 }
 
 int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, std::vector<int>& rank) {
@@ -1126,6 +1146,7 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     p.n_walk = c->n_walk;
     p.n_wide = c->n_wide;
     p.n_unb = c->n_unb;
+    p.n_leaves = c->n_wide > 0 ? c->n_leaves : 0;
     p.ordered = (flags & CPT_TRAVERSAL_ORDERED) ? ((flags & CPT_TRAVERSAL_PLAIN_LEAVES) ? 2 : 1) : 0;
     p.env = c->d_env;
     p.env_w = c->env_w;

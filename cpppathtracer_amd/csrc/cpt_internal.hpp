@@ -32,6 +32,7 @@ struct KParams {
     int n_wide;             // 4-wide walk-tree nodes per octant, after the eight octant orders
                             // (0: the ordered walk uses the binary octant orders)
     int n_unb;              // unbounded leaves at the head of every octant order
+    int n_leaves;           // the wide tree's leaf array (platforms first), after its compact image
     int ordered;            // CPT_TRAVERSAL_ORDERED: walk the ray's octant order (2: plain leaves)
     const uint32_t* env;    // packed RGBA8, env_cols x env_h
     int env_w, env_h, env_cols;

@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     float dep_acc = 0.f, first_depth = 0.f;
 
     // a lane's pending sky fetch: direction, the pass's radiance and attenuation so far
-    __shared__ float pending_q[9 * BLK];
+    __shared__ float pending_q[DEFER_MISS_ROUND > 0 ? 9 * BLK : 1];
     float* const pq = pending_q + threadIdx.x;
     bool pend = false;
     WalkState ws;          // the lane's suspended walk, if any
@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             {
                 const bool ends = !hit || !(depth + 1 < max_depth);
                 const bool need_now = (pend && ends) || (!hit && L.left == 1);
-                const bool flush = __ballot(need_now) != 0 ||
+                const bool flush = DEFER_MISS_ROUND == 0 || __ballot(need_now) != 0 ||
                                    __popcll(__ballot(pend || !hit)) * 64 >= DEFER_MISS_ROUND * __popcll(__ballot(1));
                 if (flush) {
                     if (pend) {   // older pending fetches first (their pass came first)

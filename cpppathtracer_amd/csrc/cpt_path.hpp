@@ -416,10 +416,14 @@ struct BufSrc {
 // The wide tree's compact image (cpt_capi.cpp linearise_wide): 7 x 16 B per node, after the
 // eight octant copies; padded to whole 32-B Nodes.
 __host__ __device__ __forceinline__ int wide_compact_nodes(int n_wide) { return (7 * n_wide + 1) / 2; }
+// Node index of the wide tree's leaf array (the compact image's leaf refs index it).
+__host__ __device__ __forceinline__ int wide_leaves_base(const KParams& p) {
+    return p.n_nodes + 8 * p.n_walk + 32 * p.n_wide + wide_compact_nodes(p.n_wide);
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(const KParams& p) {
-    const uint32_t bytes = (uint32_t)(p.n_nodes + 8 * p.n_walk + 32 * p.n_wide + wide_compact_nodes(p.n_wide)) *
-                           (uint32_t)sizeof(Node);
+    const uint32_t bytes = (uint32_t)(p.n_nodes + 8 * p.n_walk + 32 * p.n_wide + wide_compact_nodes(p.n_wide) +
+                                      p.n_leaves) * (uint32_t)sizeof(Node);
     return __builtin_amdgcn_make_buffer_rsrc((void*)p.nodes, (short)0, (int)bytes, 0x00020000);
 }
 
@@ -656,9 +660,10 @@ __device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], co
 }
 
 // Child refs (node words 24..27, cpt_capi.cpp linearise_wide): >= 0 a wide node of the same
-// octant, -1 none, <= -2 a leaf as ~k with k its position in the octant-0 binary order
-// (absolute Node index n_nodes + k).  The host keeps both ranges within 15 bits, so the LDS
-// stack holds 16-bit entries (BLK lanes x CPT_WSTACK x 2 B per block).
+// octant, -1 none, <= -2 a leaf: on an octant copy ~k with k its position in the octant-0
+// binary order (absolute Node index n_nodes + k), on the LDS image ~(i + 1) with i its index in
+// the leaf array.  The host keeps the ranges within 15 bits, so the LDS stack holds 16-bit
+// entries (BLK lanes x CPT_WSTACK x 2 B per block).
 // LDST: the nodes come from the block's LDS image `tree` (k_megakernel stages it), else from
 // the ray's octant copy in HBM through `rsrc`.
 // A lane's wide walk in progress, kept across rounds of the megakernel when the walk is
@@ -691,7 +696,16 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     // an LDS-typed pointer: 32-bit ds_read/ds_write addressing (a generic pointer costs a
     // 64-bit multiply-add per push and pop)
     lds_i16* const stk = (lds_i16*)wstack + threadIdx.x;
-    const BufSrc nodes{rsrc, 0u};   // leaves by absolute Node index
+    // Leaves: on the octant copies by absolute Node index (the platforms at n_nodes + k); on the
+    // LDS image by index into the wide tree's leaf array (platforms first, 32 B each, contiguous
+    // in HBM; staging it in LDS as well needs the pending sky fetches' LDS and measured 1.5%
+    // slower than keeping those).
+    const int leaf0 = LDST ? 0 : p.n_nodes;
+    // the leaf a ref <= -2 names: Node n_nodes + ~ref on the octant copies, leaf ~ref - 1 of
+    // the leaf array on the LDS image
+    auto leaf_of = [&](int ref) { return LDST ? ~ref - 1 : p.n_nodes + ~ref; };
+    const BufSrc leaf_src{rsrc, LDST ? (uint32_t)wide_leaves_base(p) * (uint32_t)sizeof(Node) : 0u};
+    auto leaf = [&](int i) -> Node { return leaf_src(i); };
     constexpr int NONE = -1;
     const uint64_t participants = __ballot(1);
     stamps::lap(6);
@@ -704,10 +718,10 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         ws.best_rank = 0x7fffffff;
         for (int k = 0; k < p.n_unb; ++k) {
             if (STATS) cnt.prims++;
-            const Node pl = nodes(p.n_nodes + k);
+            const Node pl = leaf(leaf0 + k);
             int kk;
             if (ranked_leaf_test<true, true, false>(pl, ray, ws.tmax, kk, ws.best_rank)) {
-                ws.best = p.n_nodes + k;
+                ws.best = leaf0 + k;
                 ws.kind = kk;
             }
         }
@@ -737,7 +751,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     for (int it = 0;; ++it) {
         stamps::count(9);
         if (cur <= -2 && parked < 0) {
-            parked = p.n_nodes + ~cur;
+            parked = leaf_of(cur);
             cur = pop();
         }
         if (cur >= 0) {
@@ -777,7 +791,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
             const int n01 = (bk & 1) ? n.ref[1] : n.ref[0], n23 = (bk & 1) ? n.ref[3] : n.ref[2];
             cur = m == 0 ? pop() : ((bk & 2) ? n23 : n01);
             if (cur <= -2 && parked < 0) {   // park the nearest leaf at once
-                parked = p.n_nodes + ~cur;
+                parked = leaf_of(cur);
                 cur = pop();
             }
         }
@@ -792,7 +806,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         if (__popcll(__ballot(stopped)) * 64 >= SPEC_LEAF_ROUND * __popcll(w) && parked >= 0) {
             stamps::count(10);
             if (STATS) cnt.prims++;
-            const Node lf = nodes(parked);
+            const Node lf = leaf(parked);
             int k;
             // no pretest: the parent's slab test already tested this leaf's own box
             if (ranked_leaf_test<true, true, false>(lf, ray, tmax, k, best_rank)) {
@@ -807,7 +821,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     ws.active = working;
     if (working) return 2;   // suspended
     if (best < 0) return 0;
-    const Node wn = nodes(best);
+    const Node wn = leaf(best);
     Node box;
     leaf_aabb(wn, box);
     if (slab_reject<true>(box, with_slab(ray), tmax)) return -1;
