@@ -67,6 +67,8 @@ CPT_PATH_WAVEFRONT = 0x100
 CPT_TRAVERSAL_ORDERED = 0x200
 CPT_TRAVERSAL_PLAIN_LEAVES = 0x400
 CPT_SCHEDULE_COST = 0x800
+CPT_SCHEDULE_CONSOLIDATE = 0x1000
+CPT_SCHEDULE_NO_CONSOLIDATE = 0x2000
 
 
 class CptError(RuntimeError):

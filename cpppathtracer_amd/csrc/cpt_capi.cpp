@@ -347,6 +347,8 @@ struct cpt_ctx {
     size_t cap_sched = 0;
     uint32_t* d_tile_order = nullptr;
     size_t cap_tile_order = 0;
+    uint4* d_resume = nullptr;          // tail consolidation: handed-over chains (5 x uint4 each)
+    size_t cap_resume = 0;
     cpt::WfState wf{};           // wavefront path state (allocated on first use)
     bool wf_ready = false;
     float* d_mix = nullptr;      // display running mean (Mix), rgb per pixel of the display band
@@ -856,6 +858,7 @@ int cpt_destroy(cpt_ctx* c) {
     (void)hipFree(c->d_jumps);
     (void)hipFree(c->d_stats);
     (void)hipFree(c->d_work);
+    (void)hipFree(c->d_resume);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
@@ -1175,6 +1178,8 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     p.spp = spp;
     p.max_depth = max_depth;
     p.accumulate = (flags & CPT_RENDER_ACCUMULATE) ? 1 : 0;
+    p.lanes = 64;
+    if (const char* e = getenv("CPT_LANES_PER_WAVE")) p.lanes = std::max(1, std::min(64, atoi(e)));   // DIAGNOSTIC
     const bool wavefront = (flags & CPT_PATH_WAVEFRONT) != 0;
     if (wavefront && !c->wf_ready && c->n_rows > 0) {
         const size_t npix = (size_t)c->n_rows * c->width;
@@ -1213,6 +1218,23 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
             if ((rc = ensure(c, &c->d_tile_order, &c->cap_tile_order, n_tiles)) != CPT_OK) return rc;
             HIP_TRY(c, cpt::launch_tile_schedule(p, passes, c->d_sched, c->cap_sched, c->d_tile_order, s));
             p.tile_order = c->d_tile_order;
+        }
+        // Tail consolidation (cpt_kernels.hip): one slab of hand-over slots per workgroup of the
+        // persistent grid (one LDS workgroup of 1024 lanes per CU), 3 x 256 chains each.  By
+        // default for frames of at most 3 pixels per lane: with more, the tail is a small part
+        // of the render and the plain kernel's tighter code wins.
+        int cus = 0;
+        HIP_TRY(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+        cus = std::max(cus, 1);
+        const bool cons = (flags & CPT_SCHEDULE_CONSOLIDATE) ||
+                          (!(flags & CPT_SCHEDULE_NO_CONSOLIDATE) &&
+                           (size_t)c->n_rows * c->width <= 3u * 1024u * (size_t)cus);
+        if (cons && spp > 1) {
+            const size_t cap = 3u * 256u * (size_t)cus;
+            int rc;
+            if ((rc = ensure(c, &c->d_resume, &c->cap_resume, 5 * cap)) != CPT_OK) return rc;
+            p.resume = c->d_resume;
+            p.resume_cap = cap;
         }
         HIP_TRY(c, hipEventRecord(c->ev_main, s));
         HIP_TRY(c, cpt::launch_megakernel(p, (flags & CPT_RENDER_STATS) != 0, aux, s));

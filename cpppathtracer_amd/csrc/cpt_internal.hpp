@@ -48,6 +48,11 @@ struct KParams {
     const uint32_t* tile_order;  // megakernel dequeue order of the 8x8 tiles (nullptr: row-major)
     uint32_t* tile_cost;    // pilot launch only: per-tile work (cost schedule)
     int spp, max_depth, accumulate;
+    int lanes;              // lanes per wave that take pixels (64; fewer: DIAGNOSTIC CPT_LANES_PER_WAVE)
+    // Tail consolidation (LDS walk only; nullptr: off): slabs of chains handed over at a pass
+    // boundary by retiring waves, 5 x uint4 per chain, ho_slots chains per workgroup.
+    uint4* resume;
+    size_t resume_cap;      // chains (all workgroups)
 };
 
 // Cost schedule (cpt_kernels.hip, DESIGN.md §Cost schedule): a `passes`-pass pilot of the

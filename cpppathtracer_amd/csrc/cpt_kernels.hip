@@ -37,6 +37,37 @@ namespace cpt {
 // RNG states, but nothing is written back except each pixel's work (segments + node visits +
 // primitive tests) added to its tile's cost.
 // ======================================================================================
+// TAIL CONSOLIDATION (LDS walk, p.resume != nullptr).  Once the pixel
+// queue is drained, chains finish and the waves thin out, but every wave keeps its SIMD slot
+// until its last lane is done: in the tail of a frame (and for all of it when a rank holds
+// about one pixel per lane) a few live lanes in each of four waves per SIMD share the SIMD,
+// and a chain's segment takes ~30 us instead of the ~17 us of a wave alone on its SIMD.  So
+// the block's 16 waves are ranked in four levels of four (one wave per SIMD each, by wave
+// index); when the chains still live fit into the waves of the levels below l, the waves of
+// level l retire: each lane, at the end of its current pass, hands its chain over (RNG state,
+// running sum, passes left: the pass boundary needs no path state) through a queue, and the
+// waves of the lower levels take those chains into their idle lanes.  Level 0 never retires
+// and takes hand-overs until no chain of its workgroup is live.  A chain's passes run in the
+// same order from the same state wherever they run, so the image is unchanged.
+// Everything is per workgroup (one per CU): the live count and the queue's head, tail and
+// publication flags are LDS words, the payloads a per-workgroup slab in HBM, so the waves of a
+// CU consolidate among themselves without device-wide traffic (a device-wide queue measured
+// 20-40% slower at 1-4 pixels per lane from its polling and contended CAS).  Payloads are
+// coherent (sc1) loads and stores, ordered before the flag by waiting for the stores.
+__device__ __forceinline__ uint32_t ld_coherent(const uint32_t* a) {
+    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_coherent(uint32_t* a, uint32_t v) {
+    __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Hand-over slots per workgroup: each of the waves of levels 1.. retires once and hands over
+// at most its 64 chains, so (levels - 1) x 256 slots always suffice.
+template <int BLK> constexpr int ho_slots() { return (BLK / 256 - 1) * 256; }
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {   // set lanes of `mask` below this one
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
 struct Lane {
     uint32_t xy;     // x | y << 16 (frames are < 65536 pixels wide and high)
     uint32_t pix;    // context pixel index (frames are < 2^32 pixels)
@@ -82,7 +113,7 @@ constexpr int DEFER_MISS_ROUND = CPT_DEFER_MISS_ROUND;
 template <bool LDST> constexpr int mk_block() { return LDST ? CPT_LDS_BLOCK : 256; }
 template <bool LDST> constexpr int mk_waves() { return LDST ? CPT_LDS_BLOCK / 256 : CPT_WAVES_PER_SIMD; }
 
-template <bool STATS, bool AUX, bool PROBE, bool LDST>
+template <bool STATS, bool AUX, bool PROBE, bool LDST, bool CONS>
 __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakernel(const KParams p) {
     constexpr bool COUNT = STATS || PROBE;
     constexpr int BLK = mk_block<LDST>();
@@ -115,22 +146,96 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     bool pend = false;
     WalkState ws;          // the lane's suspended walk, if any
     ws.active = false;
+    // tail consolidation (see above): this wave's level, the lanes one level holds over the grid
+    static_assert(!CONS || (LDST && !PROBE && ho_slots<BLK>() > 0), "consolidation needs the LDS walk");
+    constexpr int QS = CONS ? ho_slots<BLK>() : 1;
+    __shared__ uint32_t s_q[CONS ? 3 : 1];   // hand-over queue head, tail; the workgroup's live chains
+    __shared__ uint8_t s_qflag[QS];          // slot published
+    const bool cons = CONS && (size_t)(blockIdx.x + 1) * QS <= p.resume_cap;
+    uint4* const qslab = cons ? p.resume + 5 * (size_t)blockIdx.x * QS : nullptr;
+    volatile uint32_t* const vq = s_q;
+    const uint32_t level = __builtin_amdgcn_readfirstlane((uint32_t)(threadIdx.x >> 8));
+    bool retiring = false;       // wave-uniform: hand every chain over at its next pass end
+    uint32_t idle_spins = 0;
+    if (cons) {
+        if (threadIdx.x < 3) s_q[threadIdx.x] = 0u;
+        for (int i = threadIdx.x; i < QS; i += BLK) s_qflag[i] = 0;
+        __syncthreads();
+    }
+    // a chain's next pass (RayGen, path_tracer.cu:134)
+    auto start_pass = [&]() {
+        ray = ray_gen(p, (int)(L.xy & 0xffffu), (int)(L.xy >> 16), L.s);
+        att = mk1(1.f);
+        rad = mk1(0.f);
+        depth = 0;
+        first = true;
+        nrm_acc = mk1(0.f);
+        dep_acc = 0.f;
+    };
     stamps::init();
     for (;;) {
         stamps::lap(5);
         stamps::count(8);
+        if (cons && !retiring && level > 0 && exhausted && vq[2] <= level * 256u) retiring = true;
+        bool begin = false;   // a lane took a chain: start its next pass
+        // ---- take handed-over chains into idle lanes (consolidation) ---------------------
+        if (cons && !retiring && exhausted) {
+            const uint64_t need = __ballot(!busy && lane < p.lanes);
+            if (need && vq[1] != vq[0]) {
+                const int leader = __ffsll((unsigned long long)need) - 1;
+                uint32_t h = 0, n = 0;
+                if (lane == leader) {
+                    for (int tries = 0; tries < 16; ++tries) {
+                        h = vq[0];
+                        uint32_t t = vq[1];
+                        t = t < (uint32_t)QS ? t : (uint32_t)QS;   // slots past the cap are never written
+                        const uint32_t want = (uint32_t)__popcll(need);
+                        n = t > h ? (t - h < want ? t - h : want) : 0u;
+                        if (n == 0 || atomicCAS(&s_q[0], h, h + n) == h) break;
+                        n = 0;
+                    }
+                }
+                h = __shfl(h, leader);
+                n = __shfl(n, leader);
+                const uint32_t rank = lane_rank(need);
+                if (((need >> lane) & 1ull) && rank < n) {
+                    const uint32_t slot = h + rank;
+                    // the slot was allocated before it was written: wait for its publication
+                    const volatile uint8_t* fl = s_qflag + slot;
+                    for (uint32_t w = 0; *fl == 0 && w < (1u << 22); ++w) __builtin_amdgcn_s_sleep(1);
+                    const uint32_t* e = reinterpret_cast<const uint32_t*>(qslab + 5 * (size_t)slot);
+                    auto ld4 = [&](int q) {
+                        return make_uint4(ld_coherent(e + 4 * q), ld_coherent(e + 4 * q + 1), ld_coherent(e + 4 * q + 2),
+                                          ld_coherent(e + 4 * q + 3));
+                    };
+                    const uint4 e0 = ld4(0), e1 = ld4(1), e2 = ld4(2), e3 = AUX ? ld4(3) : make_uint4(0u, 0u, 0u, 0u);
+                    const uint32_t left = ld_coherent(e + 16);
+                    L.pix = e0.x; L.xy = e0.y; L.s.v0 = e0.z; L.s.v1 = e0.w;
+                    L.s.v2 = e1.x; L.s.v3 = e1.y; L.s.v4 = e1.z; L.s.d = e1.w;
+                    L.sum = mk(__uint_as_float(e2.x), __uint_as_float(e2.y), __uint_as_float(e2.z));
+                    L.passes = __uint_as_float(e2.w);
+                    if (AUX) {
+                        first_normal = mk(__uint_as_float(e3.x), __uint_as_float(e3.y), __uint_as_float(e3.z));
+                        first_depth = __uint_as_float(e3.w);
+                    }
+                    L.left = (int)left;
+                    busy = true;
+                    begin = true;
+                }
+            }
+        }
         // ---- refill idle lanes with new pixels (wave-aggregated dequeue) ----------------
-        if (!exhausted) {
-            const uint64_t need = __ballot(!busy);
+        if (!exhausted && !retiring) {
+            const uint64_t need = __ballot(!busy && lane < p.lanes);
             if (need) {
                 const int leader = __ffsll((unsigned long long)need) - 1;
                 uint32_t base = 0;
                 if (lane == leader) base = atomicAdd(p.work, (uint32_t)__popcll(need));
                 base = __shfl(base, leader);
                 if (base + (uint32_t)__popcll(need) >= n_work) exhausted = true;
-                if (!busy) {
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                bool took = false;
+                if ((need >> lane) & 1ull) {
+                    const uint32_t rank = lane_rank(need);
                     const uint32_t id = base + rank;
                     int x, ri;
                     if (id < n_work && decode_pixel(p, id, x, ri, L.tile)) {
@@ -158,24 +263,33 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                             }
                         }
                         busy = true;
-                        if (L.left > 0) {
-                            ray = ray_gen(p, (int)(L.xy & 0xffffu), (int)(L.xy >> 16), L.s);
-                            att = mk1(1.f);
-                            rad = mk1(0.f);
-                            depth = 0;
-                            first = true;
-                            nrm_acc = mk1(0.f);
-                            dep_acc = 0.f;
-                        }
+                        took = true;
+                        begin = L.left > 0;
                     }
+                }
+                if (cons) {   // live chains (taken, not finished): the consolidation's measure
+                    const uint64_t t = __ballot(took);
+                    if (t && lane == leader) atomicAdd(&s_q[2], (uint32_t)__popcll(t));
                 }
             }
         }
+        if (begin) start_pass();
         stamps::lap(0);
-        if (!__any(busy)) break;
+        if (!__any(busy)) {
+            if (!cons || retiring) break;
+            if (exhausted) {
+                // a keeper with nothing to do: wait for hand-overs while any chain is live (a
+                // chain in flight is never more than a pass away from its hand-over or its end)
+                if (vq[2] == 0u) break;
+                if (++idle_spins > (1u << 26)) break;   // never hang the device on a lost count
+                __builtin_amdgcn_s_sleep(16);
+            }
+            continue;   // taken ids past the frame's rows: take again
+        }
         Hit h;
         int code = -1;
         int tr = 2;
+        bool hand_over = false;
         if (busy && L.left > 0) {
             // ---- one path segment: TraceRay (path_tracer.cu:141-158); a walk suspended in an
             // earlier round resumes here (LDST: trace_wide's suspension) -------------------
@@ -214,7 +328,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             {
                 const bool ends = !hit || !(depth + 1 < max_depth);
                 const bool need_now = (pend && ends) || (!hit && L.left == 1);
-                const bool flush = DEFER_MISS_ROUND == 0 || __ballot(need_now) != 0 ||
+                const bool flush = DEFER_MISS_ROUND == 0 || retiring || __ballot(need_now) != 0 ||
                                    __popcll(__ballot(pend || !hit)) * 64 >= DEFER_MISS_ROUND * __popcll(__ballot(1));
                 if (flush) {
                     if (pend) {   // older pending fetches first (their pass came first)
@@ -252,16 +366,40 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 L.passes += 1.0f;
                 if (AUX) { first_normal = nrm_acc; first_depth = dep_acc; }
                 if (--L.left > 0) {
-                    ray = ray_gen(p, (int)(L.xy & 0xffffu), (int)(L.xy >> 16), L.s);
-                    att = mk1(1.f);
-                    rad = mk1(0.f);
-                    depth = 0;
-                    first = true;
-                    nrm_acc = mk1(0.f);
-                    dep_acc = 0.f;
+                    if (retiring) hand_over = true;   // the next pass runs in a keeper wave
+                    else start_pass();
                 }
             }
         }
+        if (cons) {
+            // ---- hand chains over at their pass boundary (retiring waves) ---------------
+            const uint64_t ho = __ballot(hand_over);
+            if (ho) {
+                const int leader = __ffsll((unsigned long long)ho) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&s_q[1], (uint32_t)__popcll(ho));
+                base = __shfl(base, leader);
+                if (hand_over) {
+                    const uint32_t slot = base + lane_rank(ho);
+                    {   // slot < QS (ho_slots)
+                        uint32_t* e = reinterpret_cast<uint32_t*>(qslab + 5 * (size_t)slot);
+                        const uint32_t w[20] = {L.pix, L.xy, L.s.v0, L.s.v1, L.s.v2, L.s.v3, L.s.v4, L.s.d,
+                                                __float_as_uint(L.sum.x), __float_as_uint(L.sum.y), __float_as_uint(L.sum.z),
+                                                __float_as_uint(L.passes), __float_as_uint(first_normal.x),
+                                                __float_as_uint(first_normal.y), __float_as_uint(first_normal.z),
+                                                __float_as_uint(first_depth), (uint32_t)L.left, 0u, 0u, 0u};
+#pragma unroll
+                        for (int k = 0; k < 17; ++k)
+                            if (AUX || k < 12 || k == 16) st_coherent(e + k, w[k]);
+                        wait_stores();   // the payload is in memory before the flag
+                        *(volatile uint8_t*)(s_qflag + slot) = 1;
+                        busy = false;
+                    }
+                    hand_over = false;
+                }
+            }
+        }
+        bool finished = false;
         if (busy && L.left == 0) {
             if (PROBE) {
                 // ---- pilot: the pixel's work goes to its tile's cost ----------------------
@@ -283,6 +421,11 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 p.rng[5 * npix + (size_t)L.pix] = L.s.d;
             }
             busy = false;
+            finished = true;
+        }
+        if (cons) {
+            const uint64_t f = __ballot(finished);
+            if (f && lane == __ffsll((unsigned long long)f) - 1) atomicSub(&s_q[2], (uint32_t)__popcll(f));
         }
     }
     stamps::flush(p.stats + 16);
@@ -556,7 +699,7 @@ __global__ void k_math_batch(int op, const float* a, const float* b, float* out,
 // ======================================================================================
 // Host-side launchers (called from cpt_capi.cpp).
 // ======================================================================================
-template <bool S, bool A, bool P, bool T>
+template <bool S, bool A, bool P, bool T, bool C = false>
 static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
     static int blocks_per_cu = -1, cus = 0;
     constexpr int block = mk_block<T>();
@@ -565,16 +708,16 @@ static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
         hipError_t e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_megakernel<S, A, P, T>, block, 0);
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_megakernel<S, A, P, T, C>, block, 0);
         if (e != hipSuccess) return e;
         if (blocks_per_cu < 1) blocks_per_cu = 1;
     }
     // persistent grid: every resident slot once; lanes pull pixels from p.work
     const long long tiles = (long long)((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
-    long long want = (tiles * 64 + block - 1) / block;
+    long long want = (tiles * 64 * ((64 + p.lanes - 1) / p.lanes) + block - 1) / block;
     long long grid = std::min<long long>(want, (long long)blocks_per_cu * cus);
     if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL((k_megakernel<S, A, P, T>), dim3((unsigned)grid), dim3(block), 0, stream, p);
+    hipLaunchKernelGGL((k_megakernel<S, A, P, T, C>), dim3((unsigned)grid), dim3(block), 0, stream, p);
     return hipGetLastError();
 }
 
@@ -589,7 +732,11 @@ static bool use_lds_tree(const KParams& p) {
 
 template <bool S, bool A, bool P>
 static hipError_t launch_mk_any(const KParams& p, hipStream_t stream) {
-    return use_lds_tree(p) ? launch_mk<S, A, P, true>(p, stream) : launch_mk<S, A, P, false>(p, stream);
+    if (!use_lds_tree(p)) return launch_mk<S, A, P, false>(p, stream);
+    if constexpr (!P) {
+        if (p.resume) return launch_mk<S, A, P, true, true>(p, stream);   // tail consolidation
+    }
+    return launch_mk<S, A, P, true>(p, stream);
 }
 
 hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t stream) {

@@ -10,7 +10,8 @@ import numpy as np
 
 from . import _lib
 from ._lib import (CPT_PATH_WAVEFRONT, CPT_RENDER_ACCUMULATE, CPT_RENDER_AUX, CPT_RENDER_STATS, CPT_RENDER_SYNC,
-                   CPT_SCHEDULE_COST, CPT_TRAVERSAL_ORDERED, CPT_TRAVERSAL_PLAIN_LEAVES, CptError, check)
+                   CPT_SCHEDULE_CONSOLIDATE, CPT_SCHEDULE_COST, CPT_SCHEDULE_NO_CONSOLIDATE, CPT_TRAVERSAL_ORDERED,
+                   CPT_TRAVERSAL_PLAIN_LEAVES, CptError, check)
 
 PATHS = ("megakernel", "wavefront")
 from .types import CAMERA_DTYPE, OBJECT_DTYPE
@@ -119,7 +120,7 @@ class Renderer:
 
     # -- render ----------------------------------------------------------------------
     def render(self, cam, spp, max_depth, accumulate=False, aux=False, stats=False, sync=False, flags=0,
-               path="megakernel", ordered=False, schedule="tiles"):
+               path="megakernel", ordered=False, schedule="tiles", consolidate=None):
         """path: "megakernel" (per-lane regeneration, state in VGPRs) or "wavefront" (SoA state in
         HBM, extend/shade kernels with ballot compaction).  Both give identical results.
         ordered: near-first BVH walk per direction octant (CPT_TRAVERSAL_ORDERED); same closest
@@ -128,7 +129,9 @@ class Renderer:
         counts, CPT_TRAVERSAL_PLAIN_LEAVES) instead of parking leaves for wave-wide rounds.
         schedule: "tiles" (8x8 tiles dequeued in row-major order) or "cost" (CPT_SCHEDULE_COST: a
         short pilot render measures each tile's work and the megakernel dequeues the tiles
-        heaviest first; same results, DESIGN.md §Cost schedule)."""
+        heaviest first; same results, DESIGN.md §Cost schedule).
+        consolidate: None (the library's default: on for frames of <= 3 pixels per lane), True or
+        False (CPT_SCHEDULE_[NO_]CONSOLIDATE): the megakernel's tail consolidation, same results."""
         if path not in PATHS:
             raise ValueError(f"path must be one of {PATHS}")
         if schedule not in ("tiles", "cost"):
@@ -142,6 +145,8 @@ class Renderer:
         f |= CPT_RENDER_STATS if stats else 0
         f |= CPT_RENDER_SYNC if sync else 0
         f |= CPT_SCHEDULE_COST if schedule == "cost" else 0
+        if consolidate is not None:
+            f |= CPT_SCHEDULE_CONSOLIDATE if consolidate else CPT_SCHEDULE_NO_CONSOLIDATE
         self._check(self._L.cpt_render(self._ctx, _p(c), spp, max_depth, f))
 
     def synchronize(self):

@@ -91,6 +91,8 @@ def lib():
         L.or_last_fallbacks.restype = u64
         L.or_set_pixel_segments.argtypes = [P]
         L.or_set_pixel_segments.restype = None
+        L.or_set_pass_trace.argtypes = [P, P]
+        L.or_set_pass_trace.restype = None
         L.or_set_walk.argtypes = [i32]
         L.or_set_walk.restype = None
         _lib = L
@@ -207,6 +209,22 @@ def pixel_segments(objs, cam, env, rows, spp, max_depth, seed, threads=1):
     finally:
         lib().or_set_pixel_segments(None)
     return out
+
+
+def pass_trace(objs, cam, env, rows, spp, max_depth, seed, threads=1):
+    """DIAGNOSTIC: per pixel and pass, the pass's RNG draws and path segments -> two uint8
+    arrays [n_rows * W, spp]."""
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    W = int(np.asarray(cam["width"]).reshape(-1)[0])
+    draws = np.zeros((rows.size * W, spp), dtype=np.uint8)
+    segs = np.zeros((rows.size * W, spp), dtype=np.uint8)
+    rng = init_rng(seed, W, rows, threads=threads)
+    lib().or_set_pass_trace(_ptr(draws), _ptr(segs))
+    try:
+        render(objs, cam, env, rows, spp, max_depth, rng, threads=threads)
+    finally:
+        lib().or_set_pass_trace(None, None)
+    return draws, segs
 
 
 def set_walk(ordered: bool):

@@ -1212,6 +1212,10 @@ struct RenderJob {
 // DIAGNOSTIC (or_set_pixel_segments): per-pixel path segments of the next renders, i.e. the
 // length of each pixel's sequential chain (tools/chain_costs.py).
 uint32_t* g_pixel_segments = nullptr;
+// DIAGNOSTIC (or_set_pass_trace): per pixel and pass, the RNG draws and path segments of the
+// pass ([n_rows * W][spp] bytes each; tools/pass_trace.py).
+uint8_t* g_pass_draws = nullptr;
+uint8_t* g_pass_segs = nullptr;
 
 void render_rows(const RenderJob& J, int thread, int nthreads, Stats& st) {
     const int W = J.cam.width;
@@ -1229,7 +1233,16 @@ void render_rows(const RenderJob& J, int thread, int nthreads, Stats& st) {
             PassOut last{};
             const uint64_t seg0 = st.segments;
             for (int sidx = 0; sidx < J.spp; ++sidx) {
+                const uint32_t d0 = s.d;
+                const uint64_t sg0 = st.segments;
                 last = sample_pixel(*J.bvh, J.env, J.cam, J.max_depth, x, y, s, st);
+                if (g_pass_draws) {
+                    // draws = (d1 - d0) / 362437 mod 2^32 (each draw adds the odd Weyl constant)
+                    uint32_t inv = 362437u;
+                    for (int i = 0; i < 5; ++i) inv *= 2u - 362437u * inv;
+                    g_pass_draws[pix * J.spp + sidx] = (uint8_t)((s.d - d0) * inv);
+                    g_pass_segs[pix * J.spp + sidx] = (uint8_t)(st.segments - sg0);
+                }
                 sum = add(sum, last.radiance);
                 cnt += 1.0f;
             }
@@ -1259,6 +1272,10 @@ int or_abi_version(void) { return 1; }
 // DIAGNOSTIC: per-pixel segment counts of the following renders are ADDED to `out`
 // ([n_rows * W] of the render's frame); nullptr turns it off.
 void or_set_pixel_segments(uint32_t* out) { g_pixel_segments = out; }
+
+// DIAGNOSTIC: per-pass draws and segments of the following renders ([n_rows * W][spp] each);
+// nullptr turns it off.
+void or_set_pass_trace(uint8_t* draws, uint8_t* segs) { g_pass_draws = draws; g_pass_segs = segs; }
 
 // Binds texels to a material texture handle (replaces an earlier binding of the handle).
 void or_bind_texture(uint64_t handle, const uint8_t* rgba, int w, int h, int valid_cols, int addr, int filter) {

@@ -113,18 +113,22 @@ def _run_both(gpu, oracle_mod, sky, objs, W, H, spp, depth, rows=None, seed=1234
 
 
 def _kw(path):
-    path, _, timed = path.partition("+")
+    path, *opts = path.split("+")
     base, _, mode = path.partition(":")
     kw = dict(path=base, ordered={"": False, "ordered": True, "plain": "plain"}[mode])
-    if timed:
+    if "timed" in opts:
         kw["schedule"] = "cost" if base == "megakernel" else "tiles"
+    if "nocons" in opts:
+        kw["consolidate"] = False
     return kw
 
 
 def _timed(path):
     """"<path>+timed": the instantiation bench.py times — no STATS counters, and for the
-    megakernel the cost schedule (pilot pass + heaviest-tiles-first order)."""
-    return path.endswith("+timed")
+    megakernel the cost schedule (pilot pass + heaviest-tiles-first order).  These small frames
+    run the tail-consolidating megakernel by default (<= 3 pixels per lane); "+nocons" selects
+    the plain one, which the N = 1 bench times on the full frame."""
+    return "+timed" in path
 
 
 CASES = [
@@ -144,12 +148,14 @@ CASES = [
 # of segments whose winner certificate failed (reference-walk fallback).  The default
 # ordered walk runs on 4-wide nodes and parks leaves for wave-wide rounds.
 PATHS = ["megakernel", "wavefront", "megakernel:ordered", "wavefront:ordered", "megakernel:plain",
-         "wavefront:plain", "megakernel+timed", "megakernel:ordered+timed", "wavefront:ordered+timed"]
+         "wavefront:plain", "megakernel+timed", "megakernel:ordered+timed", "wavefront:ordered+timed",
+         "megakernel:ordered+nocons", "megakernel:ordered+timed+nocons"]
 
 
 def _check_stats(gs, os_, path):
     if gs is None:   # "+timed": images and RNG states only
         return
+    path = path.split("+")[0]
     if path.endswith(":plain"):
         for k in ("segments", "hits", "misses"):
             assert gs[k] == os_[k], k
@@ -243,7 +249,8 @@ def test_empty_scene_and_no_env(gpu, oracle_mod, sky, path):
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
 
 
-@pytest.mark.parametrize("path", ["megakernel", "megakernel:ordered", "megakernel:plain", "megakernel:ordered+timed"])
+@pytest.mark.parametrize("path", ["megakernel", "megakernel:ordered", "megakernel:plain", "megakernel:ordered+timed",
+                                  "megakernel:ordered+timed+nocons"])
 def test_single_object_and_cylinders(gpu, oracle_mod, sky, path):
     objs = scenes.scene_s1000(n=3)
     for sl in (slice(0, 1), slice(1, 2), slice(0, 4)):

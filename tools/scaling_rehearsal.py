@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--block", type=int, default=None)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=1)
+    ap.add_argument("--consolidate", default="auto", choices=["auto", "on", "off"],
+                    help="megakernel tail consolidation (default: the library's rule)")
     a = ap.parse_args()
     import torch
     from cpppathtracer_amd import Renderer, camera_get_copy, scenes, texture_io, tiling
@@ -44,7 +46,8 @@ def main():
                     r.init_rng(1234)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(stream)
-                    r.render(cam, a.spp, depth, ordered=True, schedule=a.schedule)
+                    r.render(cam, a.spp, depth, ordered=True, schedule=a.schedule,
+                             consolidate={"auto": None, "on": True, "off": False}[a.consolidate])
                     e1.record(stream)
                     torch.cuda.synchronize()
                     ms = e0.elapsed_time(e1)
@@ -55,7 +58,8 @@ def main():
     t1 = res[min(res)]["max_rank_ms"]
     for n, v in res.items():
         v["projected_efficiency"] = round(t1 / (n * v["max_rank_ms"]), 4)
-    print(json.dumps({"config": a.config, "spp": a.spp, "block_rows": block, "schedule": a.schedule, "results": res}),
+    print(json.dumps({"config": a.config, "spp": a.spp, "block_rows": block, "schedule": a.schedule,
+                      "consolidate": a.consolidate, "results": res}),
           flush=True)
 
 

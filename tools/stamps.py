@@ -1,7 +1,7 @@
 """Wave-time breakdown of the megakernel from a CPT_STAMPS diagnostic build (cpt_stamps.hpp;
 never the timed library).
 
-    python tools/stamps.py [config] [spp] [--rows a:b]      (CPT_LIB_PATH = the stamped build)
+    python tools/stamps.py [config] [spp] [--rows=a:b] [--width=W]   (CPT_LIB_PATH = the stamped build)
 
 Build the diagnostic library with
     python -c "from cpppathtracer_amd import build as b; b.build(out='build/diag/stamps.so', defines={'CPT_STAMPS': 1})"
@@ -22,16 +22,19 @@ args = [a for a in sys.argv[1:] if not a.startswith("--")]
 cfg = scenes.CONFIGS[args[0] if args else "c4"]
 spp = int(args[1]) if len(args) > 1 else 8
 rows = None
+width = cfg["width"]
 for a in sys.argv[1:]:
+    if a.startswith("--width="):
+        width = int(a[8:])
     if a.startswith("--rows="):
         lo, hi = (int(x) for x in a[7:].split(":"))
         rows = np.arange(lo, hi, dtype=np.int32)
 r = Renderer(0)
 r.set_scene(scenes.SCENES[cfg["scene"]]())
 r.set_env(texture_io.load_cptex())
-r.set_frame(cfg["width"], cfg["height"], rows)
+r.set_frame(width, cfg["height"], rows)
 r.init_rng(1234)
-cam = camera_get_copy(scenes.camera_for(cfg["width"], cfg["height"]))
+cam = camera_get_copy(scenes.camera_for(width, cfg["height"]))
 r.render(cam, 1, cfg["depth"], sync=True, ordered=True)   # warm-up
 r.init_rng(1234)
 r.reset_stats()
