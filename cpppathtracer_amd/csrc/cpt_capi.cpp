@@ -1221,14 +1221,14 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
         }
         // Tail consolidation (cpt_kernels.hip): one slab of hand-over slots per workgroup of the
         // persistent grid (one LDS workgroup of 1024 lanes per CU), 3 x 256 chains each.  By
-        // default for frames of at most 3 pixels per lane: with more, the tail is a small part
+        // default for frames of at most 4 pixels per lane: with more, the tail is a small part
         // of the render and the plain kernel's tighter code wins.
         int cus = 0;
         HIP_TRY(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         cus = std::max(cus, 1);
         const bool cons = (flags & CPT_SCHEDULE_CONSOLIDATE) ||
                           (!(flags & CPT_SCHEDULE_NO_CONSOLIDATE) &&
-                           (size_t)c->n_rows * c->width <= 3u * 1024u * (size_t)cus);
+                           (size_t)c->n_rows * c->width <= 4u * 1024u * (size_t)cus);
         if (cons && spp > 1) {
             const size_t cap = 3u * 256u * (size_t)cus;
             int rc;

@@ -733,7 +733,7 @@ static bool use_lds_tree(const KParams& p) {
 template <bool S, bool A, bool P>
 static hipError_t launch_mk_any(const KParams& p, hipStream_t stream) {
     if (!use_lds_tree(p)) return launch_mk<S, A, P, false>(p, stream);
-    if constexpr (!P) {
+    if constexpr (!P && ho_slots<mk_block<true>()>() > 0) {
         if (p.resume) return launch_mk<S, A, P, true, true>(p, stream);   // tail consolidation
     }
     return launch_mk<S, A, P, true>(p, stream);

@@ -126,7 +126,7 @@ def _kw(path):
 def _timed(path):
     """"<path>+timed": the instantiation bench.py times — no STATS counters, and for the
     megakernel the cost schedule (pilot pass + heaviest-tiles-first order).  These small frames
-    run the tail-consolidating megakernel by default (<= 3 pixels per lane); "+nocons" selects
+    run the tail-consolidating megakernel by default (<= 4 pixels per lane); "+nocons" selects
     the plain one, which the N = 1 bench times on the full frame."""
     return "+timed" in path
 
