@@ -447,7 +447,9 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
 // ======================================================================================
 // Self-test of qdiv against the hardware IEEE divide on hashed bit patterns.
 // which = 0: all 2^32 x 2^32 patterns (NaN/inf/subnormal included); 1: a = box-plane
-// differences (|a| < 2^20), d = unit-vector components; 2: a, d in [2^-30, 2^30].
+// differences (|a| < 2^20), d = unit-vector components; 2: a, d in [2^-30, 2^30]; 3: rcp_d(d)
+// itself against 1.0 / (double)d for d = float bit pattern i; 4: rcp_f(d) against 1.0f / d on
+// its domain and rcp_f(sqrtf(d)) against 1.0f / sqrtf(d) for every pattern.
 // ======================================================================================
 __device__ __forceinline__ uint32_t hash32(uint64_t x) {
     x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
@@ -470,9 +472,26 @@ __global__ void k_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned l
             a = __uint_as_float((ua & 0x807fffffu) | ((97u + (ua >> 23) % 60u) << 23));
             d = __uint_as_float((ud & 0x807fffffu) | ((97u + (ud >> 23) % 60u) << 23));
         }
-        float q_ref = a / d;
-        float q = qdiv(a, d, rcp_d(d));
-        bool same = (__float_as_uint(q_ref) == __float_as_uint(q)) || (q_ref != q_ref && q != q);
+        bool same;
+        if (which == 3) {   // rcp_d over the float bit patterns 0 .. n-1
+            a = 1.0f;
+            d = __uint_as_float((uint32_t)i);
+            const double r_ref = 1.0 / (double)d, r = rcp_d(d);
+            same = __double_as_longlong(r_ref) == __double_as_longlong(r) || (r_ref != r_ref && r != r);
+        } else if (which == 4) {   // rcp_f over its domain, and over sqrtf of every pattern
+            a = 1.0f;
+            d = __uint_as_float((uint32_t)i);
+            const uint32_t ex = ((uint32_t)i >> 23) & 0xffu;
+            const bool dom = (ex >= 1u && ex <= 252u) || d == 0.0f || ex == 255u;
+            const float r_ref = 1.0f / d, r = rcp_f(d);
+            const float s = __builtin_sqrtf(d), rs_ref = 1.0f / s, rs = rcp_f(s);
+            same = (!dom || __float_as_uint(r_ref) == __float_as_uint(r) || (r_ref != r_ref && r != r)) &&
+                   (__float_as_uint(rs_ref) == __float_as_uint(rs) || (rs_ref != rs_ref && rs != rs));
+        } else {
+            const float q_ref = a / d;
+            const float q = qdiv(a, d, rcp_d(d));
+            same = (__float_as_uint(q_ref) == __float_as_uint(q)) || (q_ref != q_ref && q != q);
+        }
         if (!same) {
             unsigned long long k = atomicAdd(&out[0], 1ull);
             if ((long long)k + 1 < out_len) out[k + 1] = ((unsigned long long)__float_as_uint(a) << 32) | __float_as_uint(d);

@@ -126,9 +126,9 @@ __device__ __forceinline__ RayK make_rayk(const Ray& r) {
     k.yz = 0.0;
     k.ya = rcp_d(dot(r.d, r.d));
     k.yc = rcp_d(r.d.x * r.d.x + r.d.z * r.d.z);
-    k.ix = __builtin_fabsf(r.d.x) >= 1e-30f ? 1.0f / r.d.x : 0.0f;
-    k.iy = __builtin_fabsf(r.d.y) >= 1e-30f ? 1.0f / r.d.y : 0.0f;
-    k.iz = __builtin_fabsf(r.d.z) >= 1e-30f ? 1.0f / r.d.z : 0.0f;
+    k.ix = __builtin_fabsf(r.d.x) >= 1e-30f ? rcp_f(r.d.x) : 0.0f;
+    k.iy = __builtin_fabsf(r.d.y) >= 1e-30f ? rcp_f(r.d.y) : 0.0f;
+    k.iz = __builtin_fabsf(r.d.z) >= 1e-30f ? rcp_f(r.d.z) : 0.0f;
     k.bx = k.ix != 0.0f ? 0.0f : DEFAULT_RAY_TMAX * 2;
     k.by = k.iy != 0.0f ? 0.0f : DEFAULT_RAY_TMAX * 2;
     k.bz = k.iz != 0.0f ? 0.0f : DEFAULT_RAY_TMAX * 2;
@@ -876,10 +876,10 @@ struct Shade { v3 radiance, attenuation, bounce; };
 __device__ __forceinline__ v3 to_world(v3 a, v3 N) {
     v3 B, C;
     if (__builtin_fabsf(N.x) > __builtin_fabsf(N.y)) {
-        float invLen = 1.0f / __builtin_sqrtf(N.x * N.x + N.z * N.z);
+        float invLen = rcp_f(__builtin_sqrtf(N.x * N.x + N.z * N.z));
         C = mk(N.z * invLen, 0.0f, -N.x * invLen);
     } else {
-        float invLen = 1.0f / __builtin_sqrtf(N.y * N.y + N.z * N.z);
+        float invLen = rcp_f(__builtin_sqrtf(N.y * N.y + N.z * N.z));
         C = mk(0.f, N.z * invLen, -N.y * invLen);
     }
     B = cross(C, N);

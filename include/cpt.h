@@ -283,6 +283,9 @@ int cpt_measure_read_bandwidth(cpt_ctx* ctx, size_t bytes, int iters, float* gbp
 int cpt_math_batch(cpt_ctx* ctx, int op, const float* a, const float* b, float* out, size_t n);
 /* Device self-test of the exact-quotient kernel helper against the hardware IEEE f32 divide
  * over n hashed operand pairs (which: 0 all bit patterns, 1 slab-like ranges, 2 mid ranges).
+ * which = 3: the f64 reciprocal helper rcp_d(d) against the IEEE 1.0 / (double)d for the first
+ * n float bit patterns d (n = 2^32: all of them); which = 4: the f32 reciprocal helper rcp_f on
+ * its domain (2^-126 <= |d| < 2^126, 0, inf, NaN) and rcp_f(sqrtf(d)) for every pattern.
  * out[0] receives the mismatch count (0 expected), out[1..out_len) up to out_len-1 failing
  * pairs as (a bits << 32 | d bits). */
 int cpt_selftest_qdiv(cpt_ctx* ctx, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len);

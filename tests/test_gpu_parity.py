@@ -65,6 +65,21 @@ def test_exact_quotient_selftest(gpu, which, n):
     assert cnt == 0, [(float(a), float(d), float(a) / float(d)) for a, d in pairs]
 
 
+def test_rcp_d_exhaustive(gpu):
+    """rcp_d (v_rcp_f64 + two Newton steps, cpt_device.hpp) == the IEEE 1.0 / (double)d for
+    every one of the 2^32 float bit patterns d (+-0, +-inf, NaN and subnormals included)."""
+    cnt, pairs = gpu.selftest_qdiv(3, 1 << 32)
+    assert cnt == 0, [float(d) for _, d in pairs]
+
+
+def test_rcp_exhaustive(gpu):
+    """rcp_f (v_rcp_f32 + one Newton step, cpt_device.hpp) == the IEEE 1.0f / d for every
+    float pattern d with 2^-126 <= |d| < 2^126 (and 0, inf, NaN), and rcp_f(sqrtf(d)) ==
+    1.0f / sqrtf(d) for all 2^32 patterns (normalize and to_world take that form)."""
+    cnt, pairs = gpu.selftest_qdiv(4, 1 << 32)
+    assert cnt == 0, [float(d) for _, d in pairs]
+
+
 # ------------------------------------------------------------------------------- rng
 @pytest.mark.parametrize("w,rows", [(64, list(range(64))), (3840, [0, 1, 7, 1079, 2159]),
                                     (333, [5, 3, 200, 3])])
