@@ -1,7 +1,7 @@
 """Benchmark of the integrator hot path on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c5|...] [--spp S]
-                    [--scaling strong|weak] [--schedule cost|tiles]
+                    [--scaling strong|weak] [--schedule cost|tiles] [--consolidate auto|on|off]
 
 One step = one full render of the configured workload (all `spp` SamplePixel passes for
 every pixel of the image; each pass continues the pixel's XORWOW stream, exactly like the
@@ -53,6 +53,8 @@ def parse_args(argv=None):
     ap.add_argument("--walk", default="ordered", choices=["reference", "ordered"],
                     help="BVH node order: the reference's right-first DFS, or near-first per ray octant "
                          "(CPT_TRAVERSAL_ORDERED, same closest hits; DESIGN.md §Ordered walk)")
+    ap.add_argument("--consolidate", default="auto", choices=["auto", "on", "off"],
+                    help="megakernel tail consolidation (auto: on for ranks of <= 4 pixels per lane, spp >= 512)")
     ap.add_argument("--schedule", default="cost", choices=["cost", "tiles"],
                     help="megakernel pixel dequeue order: 8x8 tiles heaviest first from a pilot pass "
                          "(CPT_SCHEDULE_COST), or tiles in row-major order")
@@ -250,9 +252,16 @@ def run(args):
     kernel_events = []
     ordered = args.walk == "ordered"
     schedule = args.schedule if args.path == "megakernel" else "tiles"
+    consolidate = {"auto": None, "on": True, "off": False}[args.consolidate]
+    # the library's rule (cpt_capi.cpp): the LDS-walk megakernel consolidates its tail when the
+    # rank holds at most 4 pixels per lane of the persistent grid (1024 lanes per CU) and the
+    # chains have at least 512 passes
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    consolidating = (args.path == "megakernel" and ordered and spp > 1 and
+                     (consolidate if consolidate is not None else spp >= 512 and npix_local <= 4 * 1024 * cus))
 
     def step(timed=False):
-        r.render(cam, spp, depth, path=args.path, ordered=ordered, schedule=schedule)
+        r.render(cam, spp, depth, path=args.path, ordered=ordered, schedule=schedule, consolidate=consolidate)
         if timed:
             # the dominant kernel's device time: HIP events the context records on its launch
             # stream around the megakernel (after the cost schedule's pilot); waits for it
@@ -354,6 +363,7 @@ def run(args):
                 "workload": f"{args.config}: {cfg['scene']} {W}x{H} {spp}spp depth {depth}",
                 "width": W, "height": H, "spp": spp, "max_depth": depth, "seed": cfg["seed"],
                 "rows_rendered": H, "path": args.path, "walk": args.walk, "schedule": schedule,
+                "tail_consolidation": bool(consolidating),
                 "parallelism": f"row-tiled x{world} (interleaved {tiling.BLOCK_ROWS}-row blocks){collective}",
             },
             "rng_init_ms": round(t_init * 1e3, 2),

@@ -1221,13 +1221,15 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
         }
         // Tail consolidation (cpt_kernels.hip): one slab of hand-over slots per workgroup of the
         // persistent grid (one LDS workgroup of 1024 lanes per CU), 3 x 256 chains each.  By
-        // default for frames of at most 4 pixels per lane: with more, the tail is a small part
-        // of the render and the plain kernel's tighter code wins.
+        // default for frames of at most 4 pixels per lane and chains of at least 512 passes:
+        // with more pixels the tail is a small part of the render, with short chains the
+        // hand-overs do not pay, and the plain kernel's tighter code wins (DESIGN.md §Multi-GPU;
+        // C2 at 0.9 pixels per lane and 256 spp: 23.2 vs 21.9 Gpaths/s without).
         int cus = 0;
         HIP_TRY(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         cus = std::max(cus, 1);
         const bool cons = (flags & CPT_SCHEDULE_CONSOLIDATE) ||
-                          (!(flags & CPT_SCHEDULE_NO_CONSOLIDATE) &&
+                          (!(flags & CPT_SCHEDULE_NO_CONSOLIDATE) && spp >= 512 &&
                            (size_t)c->n_rows * c->width <= 4u * 1024u * (size_t)cus);
         if (cons && spp > 1) {
             const size_t cap = 3u * 256u * (size_t)cus;

@@ -130,7 +130,8 @@ class Renderer:
         schedule: "tiles" (8x8 tiles dequeued in row-major order) or "cost" (CPT_SCHEDULE_COST: a
         short pilot render measures each tile's work and the megakernel dequeues the tiles
         heaviest first; same results, DESIGN.md §Cost schedule).
-        consolidate: None (the library's default: on for frames of <= 4 pixels per lane), True or
+        consolidate: None (the library's default: on for frames of <= 4 pixels per lane and
+        spp >= 512), True or
         False (CPT_SCHEDULE_[NO_]CONSOLIDATE): the megakernel's tail consolidation, same results."""
         if path not in PATHS:
             raise ValueError(f"path must be one of {PATHS}")

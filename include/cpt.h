@@ -153,9 +153,9 @@ typedef struct cpt_ctx cpt_ctx;
 #define CPT_SCHEDULE_COST 0x800u
 /* Megakernel tail consolidation: once the pixel queue is drained, the
  * waves of a workgroup hand their chains over at pass boundaries so that each SIMD runs fewer,
- * fuller waves while chains finish.  Identical results.  By default it runs when spp > 1 and the
- * frame holds at most 4 pixels per lane of the persistent grid (a strong-scaled row tile);
- * these flags force it on or off.  Only the walk on the LDS tree image consolidates
+ * fuller waves while chains finish.  Identical results.  By default it runs when spp >= 512 and
+ * the frame holds at most 4 pixels per lane of the persistent grid (a strong-scaled row tile);
+ * these flags force it on or off (on needs spp > 1).  Only the walk on the LDS tree image consolidates
  * (CPT_TRAVERSAL_ORDERED, trees of up to 512 4-wide nodes). */
 #define CPT_SCHEDULE_CONSOLIDATE    0x1000u
 #define CPT_SCHEDULE_NO_CONSOLIDATE 0x2000u

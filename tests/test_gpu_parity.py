@@ -133,16 +133,17 @@ def _kw(path):
     kw = dict(path=base, ordered={"": False, "ordered": True, "plain": "plain"}[mode])
     if "timed" in opts:
         kw["schedule"] = "cost" if base == "megakernel" else "tiles"
-    if "nocons" in opts:
-        kw["consolidate"] = False
+    if "cons" in opts:
+        kw["consolidate"] = True
     return kw
 
 
 def _timed(path):
     """"<path>+timed": the instantiation bench.py times — no STATS counters, and for the
-    megakernel the cost schedule (pilot pass + heaviest-tiles-first order).  These small frames
-    run the tail-consolidating megakernel by default (<= 4 pixels per lane); "+nocons" selects
-    the plain one, which the N = 1 bench times on the full frame."""
+    megakernel the cost schedule (pilot pass + heaviest-tiles-first order).  "+cons" forces the
+    tail-consolidating megakernel, which the library picks by itself for ranks of <= 4 pixels per
+    lane at >= 512 spp (strong-scaled row tiles); these small test renders would otherwise run
+    the plain one, the kernel the N = 1 bench times."""
     return "+timed" in path
 
 
@@ -164,7 +165,7 @@ CASES = [
 # ordered walk runs on 4-wide nodes and parks leaves for wave-wide rounds.
 PATHS = ["megakernel", "wavefront", "megakernel:ordered", "wavefront:ordered", "megakernel:plain",
          "wavefront:plain", "megakernel+timed", "megakernel:ordered+timed", "wavefront:ordered+timed",
-         "megakernel:ordered+nocons", "megakernel:ordered+timed+nocons"]
+         "megakernel:ordered+cons", "megakernel:ordered+timed+cons"]
 
 
 def _check_stats(gs, os_, path):
@@ -265,7 +266,7 @@ def test_empty_scene_and_no_env(gpu, oracle_mod, sky, path):
 
 
 @pytest.mark.parametrize("path", ["megakernel", "megakernel:ordered", "megakernel:plain", "megakernel:ordered+timed",
-                                  "megakernel:ordered+timed+nocons"])
+                                  "megakernel:ordered+timed+cons"])
 def test_single_object_and_cylinders(gpu, oracle_mod, sky, path):
     objs = scenes.scene_s1000(n=3)
     for sl in (slice(0, 1), slice(1, 2), slice(0, 4)):
