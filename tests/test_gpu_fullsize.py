@@ -81,3 +81,21 @@ def test_fullsize_wavefront_equals_megakernel(gpu, sky):
     wf, wf_rng = _render(gpu, cam, 1, 16, ordered=True, path="wavefront")
     np.testing.assert_array_equal(wf.view(np.uint32), mk.view(np.uint32))
     np.testing.assert_array_equal(wf_rng, mk_rng)
+
+
+@pytest.mark.parametrize("config,spp", [("c2", 8), ("c3", 8), ("c4", 8)])
+def test_fullsize_configs_timed_kernel_rows_match_oracle(gpu, oracle_mod, sky, config, spp):
+    """BASELINE.json's C2 / C3 / C4 at full size through the instantiation bench.py times
+    (ordered walk, cost schedule, no counters), 8 passes: six evenly spaced rows and their
+    XORWOW end states equal the oracle's bit for bit."""
+    cfg = scenes.CONFIGS[config]
+    W, H, depth = cfg["width"], cfg["height"], cfg["depth"]
+    objs = scenes.SCENES[cfg["scene"]]()
+    cam = _frame(gpu, sky, objs, W, H)
+    acc, rng_end = _render(gpu, cam, spp, depth, ordered=True, schedule="cost")
+    rows = np.linspace(0, H - 1, 6).astype(np.int32)
+    rng = oracle_mod.init_rng(1234, W, rows, threads=16)
+    o_acc, _, _, _ = oracle_mod.render(objs, cam, sky, rows, spp, depth, rng, threads=16)
+    got = acc.reshape(H, W, 4)[rows].reshape(-1, 4)
+    np.testing.assert_array_equal(got.view(np.uint32), o_acc.view(np.uint32))
+    np.testing.assert_array_equal(rng_end.reshape(6, H, W)[:, rows].reshape(6, -1), rng)
