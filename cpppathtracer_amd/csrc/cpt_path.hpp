@@ -975,8 +975,7 @@ __device__ __forceinline__ v3 miss_radiance(const KParams& p, v3 dir) {
 }
 
 // MotionalCamera::RayGen (motional_camera.cu:202-213)
-__device__ __forceinline__ Ray ray_gen(const KParams& p, int x, int y, Xorwow& rng) {
-    const CamK& c = p.cam;
+__device__ __forceinline__ Ray ray_gen(const CamK& c, int x, int y, Xorwow& rng) {
     float r1 = uniform(rng), r2 = uniform(rng), r3 = uniform(rng);
     v3 rd = c.lens_radius * mk(r1, r2, r3);
     v3 u = mk(c.u[0], c.u[1], c.u[2]), v = mk(c.v[0], c.v[1], c.v[2]);
@@ -993,6 +992,25 @@ __device__ __forceinline__ Ray ray_gen(const KParams& p, int x, int y, Xorwow& r
     ray.tmin = 0.f;
     ray.tmax = DEFAULT_RAY_TMAX;
     return ray;
+}
+__device__ __forceinline__ Ray ray_gen(const KParams& p, int x, int y, Xorwow& rng) { return ray_gen(p.cam, x, y, rng); }
+
+// A kernel-argument field read where it is used: a scalar load from the kernarg segment through
+// a pointer the compiler cannot hoist (the empty asm redefines it), instead of a value held in
+// SGPRs across a persistent kernel's whole loop (whose SGPR spills to VGPR lanes cost v_readlane
+// / v_writelane pairs inside the hot loop).  Only for kernels whose single argument is KParams.
+__device__ __forceinline__ const KParams& kernarg_params() {
+    typedef __attribute__((address_space(4))) const KParams kparams4;
+    kparams4* base = (kparams4*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(base));
+    return *(const KParams*)base;
+}
+template <typename T>
+__device__ __forceinline__ T kernarg_field(size_t offset) {
+    typedef __attribute__((address_space(4))) const char kchar;
+    kchar* base = (kchar*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(base));
+    return *(const T*)(base + offset);   // a generic pointer: the AS4 origin is inferred
 }
 
 __device__ __forceinline__ uint64_t wave_sum(uint32_t v) {
