@@ -95,6 +95,11 @@ __device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int&
 #endif
 constexpr int SUSPEND_AT = CPT_SUSPEND_AT;
 
+#ifndef CPT_STATIC_FIRST
+#define CPT_STATIC_FIRST 1
+#endif
+constexpr bool STATIC_FIRST = CPT_STATIC_FIRST != 0;
+
 // Deferred sky fetches run when this many 64ths of the tracing lanes hold one.
 #ifndef CPT_DEFER_MISS_ROUND
 #define CPT_DEFER_MISS_ROUND 32
@@ -172,6 +177,11 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         nrm_acc = mk1(0.f);
         dep_acc = 0.f;
     };
+    // STATIC_FIRST (LDS walk): each wave's first tile is placed by level (see the refill); the
+    // counter then hands out the tiles after the first gridDim.x * BLK pixels
+    const bool stat = STATIC_FIRST && LDST && !PROBE && p.lanes == 64 && p.tile_order != nullptr;
+    const uint32_t n_static = gridDim.x * (uint32_t)BLK;
+    bool first_take = true;
     stamps::init();
     for (;;) {
         stamps::lap(5);
@@ -233,9 +243,18 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             if (need) {
                 const int leader = __ffsll((unsigned long long)need) - 1;
                 uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(p.work, (uint32_t)__popcll(need));
-                base = __shfl(base, leader);
-                if (base + (uint32_t)__popcll(need) >= n_work) exhausted = true;
+                if (stat && first_take) {
+                    // the wave's first tile by level: the heaviest tiles (cost order) go to the
+                    // level-0 waves (one per SIMD), the lightest to level 3, so every SIMD holds
+                    // one heavy wave that runs alone once its lighter neighbours finish
+                    base = (level * (gridDim.x * 4u) + blockIdx.x * 4u + ((threadIdx.x >> 6) & 3u)) * 64u;
+                    if (n_static >= n_work) exhausted = true;
+                } else {
+                    if (lane == leader) base = atomicAdd(p.work, (uint32_t)__popcll(need));
+                    base = __shfl(base, leader) + (stat ? n_static : 0u);
+                    if (base + (uint32_t)__popcll(need) >= n_work) exhausted = true;
+                }
+                first_take = false;
                 bool took = false;
                 if ((need >> lane) & 1ull) {
                     const uint32_t rank = lane_rank(need);
