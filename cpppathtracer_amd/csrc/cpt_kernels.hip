@@ -102,7 +102,7 @@ constexpr bool STATIC_FIRST = CPT_STATIC_FIRST != 0;
 
 // Deferred sky fetches run when this many 64ths of the tracing lanes hold one.
 #ifndef CPT_DEFER_MISS_ROUND
-#define CPT_DEFER_MISS_ROUND 32
+#define CPT_DEFER_MISS_ROUND 40
 #endif
 constexpr int DEFER_MISS_ROUND = CPT_DEFER_MISS_ROUND;
 

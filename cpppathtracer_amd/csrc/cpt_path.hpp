@@ -574,7 +574,7 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
 // Leaf rounds of the wide walk run when this many 64ths of the wave's working lanes are
 // stopped at a parked leaf.
 #ifndef CPT_SPEC_LEAF_ROUND
-#define CPT_SPEC_LEAF_ROUND 32
+#define CPT_SPEC_LEAF_ROUND 28
 #endif
 constexpr int SPEC_LEAF_ROUND = CPT_SPEC_LEAF_ROUND;
 
@@ -684,7 +684,7 @@ struct WalkState {
 // where a walk is suspended: it is the closest hit over a superset of the primitives the
 // reference tests, whatever the culling limit was at each node (DESIGN.md §Ordered walk).
 #ifndef CPT_SUSPEND_MIN_DONE
-#define CPT_SUSPEND_MIN_DONE 32
+#define CPT_SUSPEND_MIN_DONE 40
 #endif
 constexpr int SUSPEND_MIN_DONE = CPT_SUSPEND_MIN_DONE;
 

@@ -4,6 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 args="${AB_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-hbm-probe --no-count}"
 for lib in cpppathtracer_amd/libcpt.so build/ab/*.so; do
+    [ -e "$lib" ] || continue
     echo "### $lib"
     if [ -z "${AB_NOTEST:-}" ]; then
         CPT_LIB_PATH=$PWD/$lib timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -m gpu -x \
