@@ -89,10 +89,24 @@ __global__ void __launch_bounds__(256) k_wf_raygen(const KParams p, WfState w) {
     }
 }
 
-template <bool STATS>
-__global__ void __launch_bounds__(256) k_wf_extend(const KParams p, WfState w, const int32_t* __restrict__ qin,
-                                                  const uint32_t* __restrict__ nin) {
+// LDST: the megakernel's wide walk on the workgroup's LDS image of the tree (1024-lane blocks,
+// one per CU; the image is staged only by blocks that have rays), else the octant copies in HBM.
+constexpr int WF_LDS_BLOCK = 1024;
+template <bool LDST> constexpr int wf_extend_block() { return LDST ? WF_LDS_BLOCK : 256; }
+
+template <bool STATS, bool LDST>
+__global__ void __launch_bounds__(wf_extend_block<LDST>()) k_wf_extend(const KParams p, WfState w,
+                                                                       const int32_t* __restrict__ qin,
+                                                                       const uint32_t* __restrict__ nin) {
+    constexpr int BLK = wf_extend_block<LDST>();
     const uint32_t n = *nin;
+    __shared__ uint4 s_tree[LDST ? LDS_TREE_NODES * 7 : 1];
+    if (LDST) {
+        if ((uint32_t)blockIdx.x * BLK >= n) return;   // no ray for this block in this bounce
+        const uint4* src = reinterpret_cast<const uint4*>(p.nodes + p.n_nodes + 8 * p.n_walk + 32 * p.n_wide);
+        for (int i = threadIdx.x; i < 7 * p.n_wide; i += BLK) s_tree[i] = src[i];
+        __syncthreads();
+    }
     Counters cnt{};
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -110,7 +124,8 @@ __global__ void __launch_bounds__(256) k_wf_extend(const KParams p, WfState w, c
         int code = -1;
         if (STATS) cnt.segments++;
         bool hit;
-        hit = trace_segment<STATS>(p, rk, finite, h, code, cnt);
+        if (LDST) hit = trace_segment<STATS, BLK, true>(p, rk, finite, h, code, cnt, s_tree);
+        else hit = trace_segment<STATS>(p, rk, finite, h, code, cnt);
         w.hit_p[pix] = make_float4(h.pos.x, h.pos.y, h.pos.z, __int_as_float(hit ? code : -1));
         if (hit) w.hit_n[pix] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.f);
     }
@@ -257,11 +272,12 @@ hipError_t wavefront_build_ident(const KParams& p, WfState& w, hipStream_t strea
     return hipGetLastError();
 }
 
-template <bool S, bool A>
+template <bool S, bool A, bool T>
 static hipError_t wf_render_t(const KParams& p, WfState& w, hipStream_t stream, int* launches) {
     const size_t npix = (size_t)p.n_rows * p.width;
+    constexpr int eb = wf_extend_block<T>();
     const int gr = persistent_grid((const void*)k_wf_raygen<A>, 256, npix);
-    const int ge = persistent_grid((const void*)k_wf_extend<S>, 256, npix);
+    const int ge = persistent_grid((const void*)k_wf_extend<S, T>, eb, npix);
     const int gs = persistent_grid((const void*)k_wf_shade<S, A>, 256, npix);
     hipError_t e = hipSuccess;
     int n = 0;
@@ -275,7 +291,7 @@ static hipError_t wf_render_t(const KParams& p, WfState& w, hipStream_t stream, 
             uint32_t* nxt_n = w.counts + (b & 1);
             e = hipMemsetAsync(nxt_n, 0, sizeof(uint32_t), stream);
             if (e != hipSuccess) break;
-            hipLaunchKernelGGL(k_wf_extend<S>, dim3(ge), dim3(256), 0, stream, p, w, cur, cur_n);
+            hipLaunchKernelGGL((k_wf_extend<S, T>), dim3(ge), dim3(eb), 0, stream, p, w, cur, cur_n);
             hipLaunchKernelGGL((k_wf_shade<S, A>), dim3(gs), dim3(256), 0, stream, p, w, cur, cur_n, nxt, nxt_n);
             n += 2;
             cur = nxt;
@@ -287,12 +303,20 @@ static hipError_t wf_render_t(const KParams& p, WfState& w, hipStream_t stream, 
     return e;
 }
 
+template <bool T>
+static hipError_t wf_render_any(const KParams& p, WfState& w, bool stats, bool aux, hipStream_t stream, int* launches) {
+    if (stats && aux) return wf_render_t<true, true, T>(p, w, stream, launches);
+    if (stats) return wf_render_t<true, false, T>(p, w, stream, launches);
+    if (aux) return wf_render_t<false, true, T>(p, w, stream, launches);
+    return wf_render_t<false, false, T>(p, w, stream, launches);
+}
+
 hipError_t launch_wavefront(const KParams& p, WfState& w, bool stats, bool aux, hipStream_t stream, int* launches) {
     if (p.width <= 0 || p.n_rows <= 0) return hipSuccess;
-    if (stats && aux) return wf_render_t<true, true>(p, w, stream, launches);
-    if (stats) return wf_render_t<true, false>(p, w, stream, launches);
-    if (aux) return wf_render_t<false, true>(p, w, stream, launches);
-    return wf_render_t<false, false>(p, w, stream, launches);
+    // the wide walk's LDS image when it fits (as in the megakernel, cpt_kernels.hip use_lds_tree)
+    const bool lds = p.ordered == 1 && p.n_wide > 0 && p.n_wide <= LDS_TREE_NODES;
+    return lds ? wf_render_any<true>(p, w, stats, aux, stream, launches)
+               : wf_render_any<false>(p, w, stats, aux, stream, launches);
 }
 
 }  // namespace cpt
