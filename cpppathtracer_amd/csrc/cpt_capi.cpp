@@ -398,7 +398,8 @@ void free_frame(cpt_ctx* c) {
     (void)hipFree(c->d_normal); c->d_normal = nullptr;
     (void)hipFree(c->d_depth); c->d_depth = nullptr;
     (void)hipFree(c->d_mix); c->d_mix = nullptr;
-    for (float4** a : {&c->wf.ray_o, &c->wf.ray_d, &c->wf.att, &c->wf.rad, &c->wf.hit_p, &c->wf.hit_n, &c->wf.aux}) {
+    for (float4** a : {&c->wf.ray_o[0], &c->wf.ray_d[0], &c->wf.att[0], &c->wf.rad[0], &c->wf.aux[0], &c->wf.ray_o[1],
+                       &c->wf.ray_d[1], &c->wf.att[1], &c->wf.rad[1], &c->wf.aux[1], &c->wf.hit_p, &c->wf.hit_n}) {
         (void)hipFree(*a);
         *a = nullptr;
     }
@@ -1183,7 +1184,9 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     const bool wavefront = (flags & CPT_PATH_WAVEFRONT) != 0;
     if (wavefront && !c->wf_ready && c->n_rows > 0) {
         const size_t npix = (size_t)c->n_rows * c->width;
-        for (float4** a : {&c->wf.ray_o, &c->wf.ray_d, &c->wf.att, &c->wf.rad, &c->wf.hit_p, &c->wf.hit_n, &c->wf.aux})
+        for (float4** a : {&c->wf.ray_o[0], &c->wf.ray_d[0], &c->wf.att[0], &c->wf.rad[0], &c->wf.aux[0],
+                           &c->wf.ray_o[1], &c->wf.ray_d[1], &c->wf.att[1], &c->wf.rad[1], &c->wf.aux[1], &c->wf.hit_p,
+                           &c->wf.hit_n})
             HIP_TRY(c, hipMalloc((void**)a, npix * sizeof(float4)));
         HIP_TRY(c, hipMalloc((void**)&c->wf.queue[0], npix * sizeof(int32_t)));
         HIP_TRY(c, hipMalloc((void**)&c->wf.queue[1], npix * sizeof(int32_t)));

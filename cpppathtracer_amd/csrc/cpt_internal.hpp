@@ -62,9 +62,13 @@ size_t tile_schedule_scratch_bytes(int width, int n_rows);
 hipError_t launch_tile_schedule(const KParams& p, int passes, void* scratch, size_t scratch_bytes, uint32_t* order,
                                 hipStream_t stream);
 
-// Wavefront path state (cpt_wavefront.hip): SoA float4 arrays indexed by pixel + queues.
+// Wavefront path state (cpt_wavefront.hip): SoA float4 arrays indexed by QUEUE SLOT + queues.
+// The carried state is double-buffered: bounce b reads buffer b & 1 at its queue slot and shade
+// writes each surviving path into buffer (b + 1) & 1 at the slot the compaction gave it, so
+// every state access is coalesced.  Hit records are per slot of the current bounce.
 struct WfState {
-    float4 *ray_o, *ray_d, *att, *rad, *hit_p, *hit_n, *aux;
+    float4 *ray_o[2], *ray_d[2], *att[2], *rad[2], *aux[2];
+    float4 *hit_p, *hit_n;
     int32_t* queue[2];
     int32_t* ident;       // tile-ordered identity queue (first bounce)
     uint32_t* counts;     // [0], [1]: queue sizes; [3]: ident size

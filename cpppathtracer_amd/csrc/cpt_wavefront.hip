@@ -9,8 +9,10 @@
 //                 re-compacted into the next queue with a wave64 ballot + mbcnt prefix and ONE
 //                 atomic per wave; finished paths add their radiance to the pixel accumulator
 //
-// Path state lives in HBM as SoA float4 arrays indexed by pixel (coalesced for the tile-
-// ordered first bounce, L2-gathered afterwards); queues hold pixel indices.  A pixel's
+// Path state lives in HBM as SoA float4 arrays indexed by queue slot, double-buffered across
+// bounces: shade writes a surviving path at the slot the compaction gives it, so extend and the
+// next shade read it coalesced.  Queues map slot -> pixel, for the per-pixel XORWOW state and
+// the accumulator only.  A pixel's
 // passes run in order (pass p for all pixels, then p+1), so every pixel consumes its XORWOW
 // stream exactly as in the megakernel and the results are bit-identical to it.
 #include <hip/hip_runtime.h>
@@ -22,7 +24,7 @@
 
 namespace cpt {
 
-// Packed per-pixel path state (all float4, 16-B aligned, SoA).
+// Packed per-slot path state (all float4, 16-B aligned, SoA).
 //   ray_o  = (o.xyz, tmin)         ray_d = (d.xyz, depth as uint bits)
 //   att    = (attenuation.xyz, first-segment flag bits)
 //   rad    = (radiance.xyz, unused)
@@ -58,13 +60,15 @@ __device__ __forceinline__ void store_rng(const KParams& p, size_t npix, size_t 
     p.rng[5 * npix + pix] = s.d;
 }
 
-// Pass start.  The first queue is the tile-ordered identity (k_wf_ident), so nothing is
-// appended here.  max_depth == 0: the pass is RayGen's draws and a zero radiance.
+// Pass start.  The first queue is the tile-ordered identity (k_wf_ident, exactly npix
+// entries), so nothing is appended here: slot i of state buffer 0 is the path of pixel
+// ident[i].  max_depth == 0: the pass is RayGen's draws and a zero radiance.
 template <bool AUX>
 __global__ void __launch_bounds__(256) k_wf_raygen(const KParams p, WfState w) {
     const size_t npix = (size_t)p.n_rows * p.width;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t pix = (size_t)blockIdx.x * blockDim.x + threadIdx.x; pix < npix; pix += stride) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < npix; i += stride) {
+        const size_t pix = (size_t)w.ident[i];
         const int x = (int)(pix % p.width), ri = (int)(pix / p.width);
         Xorwow s;
         load_rng(p, npix, pix, s);
@@ -81,11 +85,11 @@ __global__ void __launch_bounds__(256) k_wf_raygen(const KParams p, WfState w) {
             }
             continue;
         }
-        w.ray_o[pix] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.tmin);
-        w.ray_d[pix] = make_float4(ray.d.x, ray.d.y, ray.d.z, __uint_as_float(0u));
-        w.att[pix] = make_float4(1.f, 1.f, 1.f, __uint_as_float(1u));
-        w.rad[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (AUX) w.aux[pix] = make_float4(0.f, 0.f, 0.f, 0.f);
+        w.ray_o[0][i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.tmin);
+        w.ray_d[0][i] = make_float4(ray.d.x, ray.d.y, ray.d.z, __uint_as_float(0u));
+        w.att[0][i] = make_float4(1.f, 1.f, 1.f, __uint_as_float(1u));
+        w.rad[0][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (AUX) w.aux[0][i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
 
@@ -96,8 +100,8 @@ template <bool LDST> constexpr int wf_extend_block() { return LDST ? WF_LDS_BLOC
 
 template <bool STATS, bool LDST>
 __global__ void __launch_bounds__(wf_extend_block<LDST>()) k_wf_extend(const KParams p, WfState w,
-                                                                       const int32_t* __restrict__ qin,
-                                                                       const uint32_t* __restrict__ nin) {
+                                                                       const uint32_t* __restrict__ nin,
+                                                                       const int sb) {
     constexpr int BLK = wf_extend_block<LDST>();
     const uint32_t n = *nin;
     __shared__ uint4 s_tree[LDST ? LDS_TREE_NODES * 7 : 1];
@@ -110,8 +114,7 @@ __global__ void __launch_bounds__(wf_extend_block<LDST>()) k_wf_extend(const KPa
     Counters cnt{};
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const int pix = qin[i];
-        const float4 o = w.ray_o[pix], d = w.ray_d[pix];
+        const float4 o = w.ray_o[sb][i], d = w.ray_d[sb][i];
         Ray ray;
         ray.o = mk(o.x, o.y, o.z);
         ray.d = mk(d.x, d.y, d.z);
@@ -126,8 +129,8 @@ __global__ void __launch_bounds__(wf_extend_block<LDST>()) k_wf_extend(const KPa
         bool hit;
         if (LDST) hit = trace_segment<STATS, BLK, true>(p, rk, finite, h, code, cnt, s_tree);
         else hit = trace_segment<STATS>(p, rk, finite, h, code, cnt);
-        w.hit_p[pix] = make_float4(h.pos.x, h.pos.y, h.pos.z, __int_as_float(hit ? code : -1));
-        if (hit) w.hit_n[pix] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.f);
+        w.hit_p[i] = make_float4(h.pos.x, h.pos.y, h.pos.z, __int_as_float(hit ? code : -1));
+        if (hit) w.hit_n[i] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.f);
     }
     if (STATS) {
         const uint64_t a = wave_sum(cnt.segments), b = wave_sum(cnt.nodes), c = wave_sum(cnt.prims);
@@ -144,7 +147,7 @@ __global__ void __launch_bounds__(wf_extend_block<LDST>()) k_wf_extend(const KPa
 template <bool STATS, bool AUX>
 __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, const int32_t* __restrict__ qin,
                                                  const uint32_t* __restrict__ nin, int32_t* __restrict__ qout,
-                                                 uint32_t* __restrict__ nout) {
+                                                 uint32_t* __restrict__ nout, const int sb) {
     const uint32_t n = *nin;
     const size_t npix = (size_t)p.n_rows * p.width;
     const uint32_t max_depth = (uint32_t)p.max_depth;
@@ -155,12 +158,13 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
     for (uint32_t t = 0, i = blockIdx.x * blockDim.x + threadIdx.x; t < trips; ++t, i += stride) {
         bool alive = false;
         int pix = 0;
+        float4 no4, nd4, na4, nr4, nx4;   // the surviving path's state for buffer sb ^ 1
         if (i < n) {
             pix = qin[i];
             Xorwow s;
             load_rng(p, npix, pix, s);
-            const float4 o4 = w.ray_o[pix], d4 = w.ray_d[pix], a4 = w.att[pix], r4 = w.rad[pix];
-            const float4 hp = w.hit_p[pix];
+            const float4 o4 = w.ray_o[sb][i], d4 = w.ray_d[sb][i], a4 = w.att[sb][i], r4 = w.rad[sb][i];
+            const float4 hp = w.hit_p[i];
             v3 dir = mk(d4.x, d4.y, d4.z);
             v3 att = mk(a4.x, a4.y, a4.z), rad = mk(r4.x, r4.y, r4.z);
             uint32_t depth = __float_as_uint(d4.w);
@@ -171,7 +175,7 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
             v3 org = mk(o4.x, o4.y, o4.z);
             if (code >= 0) {
                 hits++;
-                const float4 hn = w.hit_n[pix];
+                const float4 hn = w.hit_n[i];
                 const v3 normal = mk(hn.x, hn.y, hn.z);
                 const Mat m = p.mats[code >> 2];
                 eval_material(m, normal, dir, s, sh);
@@ -189,7 +193,7 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
             att = att * sh.attenuation;
             float4 aux4 = make_float4(0.f, 0.f, 0.f, 0.f);
             if (AUX) {
-                aux4 = w.aux[pix];
+                aux4 = w.aux[sb][i];
                 if (first) {
                     const v3 nn = mk(aux4.x, aux4.y, aux4.z) + attr_normal;
                     aux4 = make_float4(nn.x, nn.y, nn.z, aux4.w + DEFAULT_RAY_TMAX);
@@ -209,16 +213,24 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
                 }
             } else {
                 alive = true;
-                w.ray_o[pix] = make_float4(org.x, org.y, org.z, BOUNCE_RAY_TMIN);
-                w.ray_d[pix] = make_float4(dir.x, dir.y, dir.z, __uint_as_float(depth));
-                w.att[pix] = make_float4(att.x, att.y, att.z, __uint_as_float(0u));
-                w.rad[pix] = make_float4(rad.x, rad.y, rad.z, 0.f);
-                if (AUX) w.aux[pix] = aux4;
+                no4 = make_float4(org.x, org.y, org.z, BOUNCE_RAY_TMIN);
+                nd4 = make_float4(dir.x, dir.y, dir.z, __uint_as_float(depth));
+                na4 = make_float4(att.x, att.y, att.z, __uint_as_float(0u));
+                nr4 = make_float4(rad.x, rad.y, rad.z, 0.f);
+                nx4 = aux4;
             }
             store_rng(p, npix, pix, s);
         }
         const uint32_t slot = wave_append(alive, nout);
-        if (alive) qout[slot] = pix;
+        if (alive) {
+            const int ob = sb ^ 1;
+            qout[slot] = pix;
+            w.ray_o[ob][slot] = no4;
+            w.ray_d[ob][slot] = nd4;
+            w.att[ob][slot] = na4;
+            w.rad[ob][slot] = nr4;
+            if (AUX) w.aux[ob][slot] = nx4;
+        }
     }
     if (STATS) {
         const uint64_t a = wave_sum(hits), b = wave_sum(misses);
@@ -291,8 +303,8 @@ static hipError_t wf_render_t(const KParams& p, WfState& w, hipStream_t stream, 
             uint32_t* nxt_n = w.counts + (b & 1);
             e = hipMemsetAsync(nxt_n, 0, sizeof(uint32_t), stream);
             if (e != hipSuccess) break;
-            hipLaunchKernelGGL((k_wf_extend<S, T>), dim3(ge), dim3(eb), 0, stream, p, w, cur, cur_n);
-            hipLaunchKernelGGL((k_wf_shade<S, A>), dim3(gs), dim3(256), 0, stream, p, w, cur, cur_n, nxt, nxt_n);
+            hipLaunchKernelGGL((k_wf_extend<S, T>), dim3(ge), dim3(eb), 0, stream, p, w, cur_n, b & 1);
+            hipLaunchKernelGGL((k_wf_shade<S, A>), dim3(gs), dim3(256), 0, stream, p, w, cur, cur_n, nxt, nxt_n, b & 1);
             n += 2;
             cur = nxt;
             cur_n = nxt_n;
