@@ -403,6 +403,10 @@ void free_frame(cpt_ctx* c) {
         (void)hipFree(*a);
         *a = nullptr;
     }
+    for (int b = 0; b < 2; ++b) {
+        (void)hipFree(c->wf.rng_a[b]); c->wf.rng_a[b] = nullptr;
+        (void)hipFree(c->wf.rng_b[b]); c->wf.rng_b[b] = nullptr;
+    }
     (void)hipFree(c->wf.queue[0]); c->wf.queue[0] = nullptr;
     (void)hipFree(c->wf.queue[1]); c->wf.queue[1] = nullptr;
     (void)hipFree(c->wf.ident); c->wf.ident = nullptr;
@@ -1188,6 +1192,10 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
                            &c->wf.ray_o[1], &c->wf.ray_d[1], &c->wf.att[1], &c->wf.rad[1], &c->wf.aux[1], &c->wf.hit_p,
                            &c->wf.hit_n})
             HIP_TRY(c, hipMalloc((void**)a, npix * sizeof(float4)));
+        for (int b = 0; b < 2; ++b) {
+            HIP_TRY(c, hipMalloc((void**)&c->wf.rng_a[b], npix * sizeof(uint4)));
+            HIP_TRY(c, hipMalloc((void**)&c->wf.rng_b[b], npix * sizeof(uint2)));
+        }
         HIP_TRY(c, hipMalloc((void**)&c->wf.queue[0], npix * sizeof(int32_t)));
         HIP_TRY(c, hipMalloc((void**)&c->wf.queue[1], npix * sizeof(int32_t)));
         HIP_TRY(c, hipMalloc((void**)&c->wf.ident, npix * sizeof(int32_t)));

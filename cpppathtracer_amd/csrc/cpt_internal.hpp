@@ -69,6 +69,8 @@ hipError_t launch_tile_schedule(const KParams& p, int passes, void* scratch, siz
 struct WfState {
     float4 *ray_o[2], *ray_d[2], *att[2], *rad[2], *aux[2];
     float4 *hit_p, *hit_n;
+    uint4* rng_a[2];      // a live path's XORWOW state by slot: (v0, v1, v2, v3) ...
+    uint2* rng_b[2];      // ... and (v4, d); back in the per-pixel planes when the path ends
     int32_t* queue[2];
     int32_t* ident;       // tile-ordered identity queue (first bounce)
     uint32_t* counts;     // [0], [1]: queue sizes; [3]: ident size

@@ -51,6 +51,18 @@ __device__ __forceinline__ void load_rng(const KParams& p, size_t npix, size_t p
     s.d = p.rng[5 * npix + pix];
 }
 
+__device__ __forceinline__ void load_rng_slot(const WfState& w, int b, uint32_t i, Xorwow& s) {
+    const uint4 a = w.rng_a[b][i];
+    const uint2 c = w.rng_b[b][i];
+    s.v0 = a.x; s.v1 = a.y; s.v2 = a.z; s.v3 = a.w;
+    s.v4 = c.x; s.d = c.y;
+}
+
+__device__ __forceinline__ void store_rng_slot(const WfState& w, int b, uint32_t i, const Xorwow& s) {
+    w.rng_a[b][i] = make_uint4(s.v0, s.v1, s.v2, s.v3);
+    w.rng_b[b][i] = make_uint2(s.v4, s.d);
+}
+
 __device__ __forceinline__ void store_rng(const KParams& p, size_t npix, size_t pix, const Xorwow& s) {
     p.rng[pix] = s.v0;
     p.rng[npix + pix] = s.v1;
@@ -73,8 +85,8 @@ __global__ void __launch_bounds__(256) k_wf_raygen(const KParams p, WfState w) {
         Xorwow s;
         load_rng(p, npix, pix, s);
         const Ray ray = ray_gen(p, x, p.rows[ri], s);
-        store_rng(p, npix, pix, s);
         if (p.max_depth == 0) {
+            store_rng(p, npix, pix, s);
             float4 a = p.accum[pix];
             p.accum[pix] = make_float4(a.x + 0.f, a.y + 0.f, a.z + 0.f, a.w + 1.0f);
             if (AUX) {
@@ -90,6 +102,7 @@ __global__ void __launch_bounds__(256) k_wf_raygen(const KParams p, WfState w) {
         w.att[0][i] = make_float4(1.f, 1.f, 1.f, __uint_as_float(1u));
         w.rad[0][i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (AUX) w.aux[0][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        store_rng_slot(w, 0, (uint32_t)i, s);   // the path carries its stream until it ends
     }
 }
 
@@ -159,10 +172,10 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
         bool alive = false;
         int pix = 0;
         float4 no4, nd4, na4, nr4, nx4;   // the surviving path's state for buffer sb ^ 1
+        Xorwow s;
         if (i < n) {
             pix = qin[i];
-            Xorwow s;
-            load_rng(p, npix, pix, s);
+            load_rng_slot(w, sb, i, s);
             const float4 o4 = w.ray_o[sb][i], d4 = w.ray_d[sb][i], a4 = w.att[sb][i], r4 = w.rad[sb][i];
             const float4 hp = w.hit_p[i];
             v3 dir = mk(d4.x, d4.y, d4.z);
@@ -211,6 +224,7 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
                     p.normal[3 * (size_t)pix + 2] = aux4.z;
                     p.depth[pix] = aux4.w;
                 }
+                store_rng(p, npix, pix, s);
             } else {
                 alive = true;
                 no4 = make_float4(org.x, org.y, org.z, BOUNCE_RAY_TMIN);
@@ -219,7 +233,6 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
                 nr4 = make_float4(rad.x, rad.y, rad.z, 0.f);
                 nx4 = aux4;
             }
-            store_rng(p, npix, pix, s);
         }
         const uint32_t slot = wave_append(alive, nout);
         if (alive) {
@@ -230,6 +243,7 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
             w.att[ob][slot] = na4;
             w.rad[ob][slot] = nr4;
             if (AUX) w.aux[ob][slot] = nx4;
+            store_rng_slot(w, ob, slot, s);
         }
     }
     if (STATS) {
