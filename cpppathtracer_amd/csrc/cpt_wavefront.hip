@@ -168,7 +168,27 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
     const uint32_t stride = gridDim.x * blockDim.x;
     // all lanes run the same trip count so the wave-level append sees the whole wave
     const uint32_t trips = (n + stride - 1) / stride;
-    for (uint32_t t = 0, i = blockIdx.x * blockDim.x + threadIdx.x; t < trips; ++t, i += stride) {
+    // The block's 256 slots are regrouped misses-first through LDS (a counting sort on
+    // miss / hit / past-the-queue), so a wave runs the sky path or the material path, rarely both.
+    __shared__ uint32_t s_cnt[3][4];
+    __shared__ uint32_t s_slot[256];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t t = 0, i0 = blockIdx.x * blockDim.x + threadIdx.x; t < trips; ++t, i0 += stride) {
+        const int key = i0 < n ? (__float_as_int(w.hit_p[i0].w) >= 0 ? 1 : 0) : 2;
+        uint64_t mk_[3];
+        for (int k = 0; k < 3; ++k) mk_[k] = __ballot(key == k);
+        if (lane == 0)
+            for (int k = 0; k < 3; ++k) s_cnt[k][wv] = (uint32_t)__popcll(mk_[k]);
+        __syncthreads();
+        uint32_t pos = 0;
+        for (int k = 0; k < 3; ++k)
+            for (int v = 0; v < 4; ++v)
+                if (k < key || (k == key && v < wv)) pos += s_cnt[k][v];
+        const uint64_t mine = mk_[key];
+        pos += __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+        s_slot[pos] = i0;
+        __syncthreads();
+        const uint32_t i = s_slot[threadIdx.x];
         bool alive = false;
         int pix = 0;
         float4 no4, nd4, na4, nr4, nx4;   // the surviving path's state for buffer sb ^ 1
