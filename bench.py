@@ -34,8 +34,8 @@ sys.path.insert(0, REPO)
 
 METRIC = "Mpaths/sec (pixels×spp/s) at 1920×1080; achieved HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
-WIDE_NODE_BYTES = 112   # a 4-wide walk node visit loads 7 x dwordx4 (cpt_path.hpp load_wide)
-LDS_TREE_NODES = 512    # k_megakernel stages the wide tree in LDS up to this size (cpt_path.hpp)
+WIDE_NODE_BYTES = 112   # a 4-wide walk node visit reads 7 x 16 B of the compact image (cpt_path.hpp)
+LDS_TREE_NODES = 512    # the LDS kernels stage the image's first 512 nodes (cpt_path.hpp lds_tree_nodes)
 
 
 def parse_args(argv=None):
@@ -49,6 +49,8 @@ def parse_args(argv=None):
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--objects", type=int, default=None,
+                    help="S1000 generator with this many primitives instead of 1000 (BVH-size scaling runs)")
     ap.add_argument("--path", default="megakernel", choices=["megakernel", "wavefront"])
     ap.add_argument("--walk", default="ordered", choices=["reference", "ordered"],
                     help="BVH node order: the reference's right-first DFS, or near-first per ray octant "
@@ -218,7 +220,11 @@ def run(args):
     if args.scaling == "weak" and world > 1 and not (args.width or args.height):
         cfg["width"], cfg["height"] = tiling.weak_scaled_size(cfg["width"], cfg["height"], world)
     W, H, spp, depth = cfg["width"], cfg["height"], cfg["spp"], cfg["depth"]
-    objs = scenes.SCENES[cfg["scene"]]()
+    if args.objects and cfg["scene"] == "s1000":
+        objs = scenes.scene_s1000(n=args.objects)
+        cfg["scene"] = f"s1000(n={args.objects})"
+    else:
+        objs = scenes.SCENES[cfg["scene"]]()
     sky = texture_io.load_cptex()
     cam = camera_get_copy(scenes.camera_for(W, H))
     rows = tiling.partition_rows(H, world, rank)
@@ -283,19 +289,22 @@ def run(args):
         r.render(cam, spp, depth, stats=True, path=args.path, ordered=walk_ordered)
         torch.cuda.synchronize()
         loc = r.stats()
-        v = torch.tensor([loc[k] for k in KEYS], dtype=torch.float64, device=dev)
+        loc["global_nodes"] = r.raw_counters()[6]   # wide-node visits past the LDS image
+        v = torch.tensor([loc[k] for k in KEYS + ("global_nodes",)], dtype=torch.float64, device=dev)
         if world > 1:
             v = _all_reduce(v)
-        return dict(zip(KEYS, (int(x) for x in v.tolist())))
+        return dict(zip(KEYS + ("global_nodes",), (int(x) for x in v.tolist())))
 
     walk_info = r.walk_info()
     hbm_ceiling = r.measure_read_bandwidth(4 << 30, 10) if not args.no_hbm_probe else None
     wide = ordered and walk_info["n_wide"] > 0
-    # Global-memory bytes per node visit of the executed walk: the 4-wide nodes come from the
-    # workgroup's LDS image when it fits (loaded once per workgroup per launch, priced below), so
-    # a visit moves no global-memory bytes; otherwise 112 B per wide visit, 32 B per binary one.
-    lds_image = wide and args.path == "megakernel" and walk_info["n_wide"] <= LDS_TREE_NODES
-    walk_node_bytes = 0 if lds_image else (WIDE_NODE_BYTES if wide else 32)
+    # Global-memory bytes per node visit of the executed walk: the wide walk reads the top
+    # LDS_TREE_NODES nodes from the workgroup's LDS image (loaded once per workgroup per launch,
+    # priced below), so those visits move no global-memory bytes; visits past the image read
+    # 112 B from global memory (counted separately); a binary visit reads 32 B.
+    lds_image = wide
+    n_lds = min(walk_info["n_wide"], LDS_TREE_NODES)
+    walk_node_bytes = 0 if lds_image else 32
     st = walk_counts = walk_diff = None
     if not args.no_count:
         st = count_pass(False)
@@ -376,8 +385,8 @@ def run(args):
             share = npix_local / float(W * H)
             bytes_launch = byte_model(walk_counts, paths_total, walk_node_bytes) * share
             if lds_image:   # every workgroup stages the image once (one workgroup per CU)
-                bytes_launch += walk_info["n_wide"] * WIDE_NODE_BYTES * torch.cuda.get_device_properties(
-                    dev).multi_processor_count
+                bytes_launch += n_lds * WIDE_NODE_BYTES * torch.cuda.get_device_properties(dev).multi_processor_count
+                bytes_launch += walk_counts["global_nodes"] * WIDE_NODE_BYTES * share
             bytes_ref = byte_model(st, paths_total) * share
             kms = avg_kernel_ms_max if world > 1 else avg_kernel_ms
             t_render = kms * max(1, launches) / 1e3   # the byte counts cover every launch of the render
@@ -400,9 +409,10 @@ def run(args):
                 "byte_model": (f"SURVEY.md 8(d): 76 S + {walk_node_bytes} nodes + 32 prims + 40 hits + 16 misses + 16 P "
                                "on the executed walk's counts" +
                                (" (4-wide nodes read from the workgroup's LDS image: no global-memory bytes per "
-                                "visit, + the image's 112 B x n_wide once per workgroup)" if lds_image else
-                                " (4-wide walk tree: 7 x 16 B loaded per node visit)" if wide else " (binary nodes)")),
-                "lds_node_bytes_per_launch": int(walk_counts["nodes"] * WIDE_NODE_BYTES * share) if lds_image else 0,
+                                "visit, + the image's 112 B x min(n_wide, 512) once per workgroup, + 112 B per "
+                                "visit of a node past the LDS image)" if lds_image else " (binary nodes)")),
+                "lds_node_bytes_per_launch": int((walk_counts["nodes"] - walk_counts["global_nodes"]) *
+                                                 WIDE_NODE_BYTES * share) if lds_image else 0,
                 "walk_info": walk_info,
                 "walk_counts": walk_counts,
                 "reference_counts": st,

@@ -42,6 +42,7 @@ PROTOTYPES = {
     "cpt_clear_accum": (_I, [_P]),
     "cpt_read_aux": (_I, [_P, _P, _P]),
     "cpt_copy_accum_device": (_I, [_P, _P, _SZ]),
+    "cpt_gather_rows": (_I, [_P, _P]),
     "cpt_get_stats": (_I, [_P, _P]),
     "cpt_reset_stats": (_I, [_P]),
     "cpt_get_raw_counters": (_I, [_P, _P]),
@@ -56,6 +57,7 @@ PROTOTYPES = {
     "cpt_reset_display": (_I, [_P]),
     "cpt_math_batch": (_I, [_P, _I, _P, _P, _P, _SZ]),
     "cpt_selftest_qdiv": (_I, [_P, _I, _U64, _U64, _P, _I]),
+    "cpt_set_debug_consolidation": (_I, [_P, _U32, _I, _I]),
 }
 
 CPT_RENDER_ACCUMULATE = 0x1
@@ -69,6 +71,8 @@ CPT_TRAVERSAL_PLAIN_LEAVES = 0x400
 CPT_SCHEDULE_COST = 0x800
 CPT_SCHEDULE_CONSOLIDATE = 0x1000
 CPT_SCHEDULE_NO_CONSOLIDATE = 0x2000
+CPT_ERR_STATE = 5
+CPT_ERR_DEVICE = 7   # a kernel abandoned work (reported at the next synchronising call)
 
 
 class CptError(RuntimeError):
@@ -92,7 +96,10 @@ def load(build_if_missing: bool = True):
             raise CptError(-1, f"{path} missing: run __graft_entry__.build() (hipcc) first")
         _build.build()
     L = ctypes.CDLL(path)
+    ab_variant = "CPT_LIB_PATH" in os.environ
     for name, (res, args) in PROTOTYPES.items():
+        if ab_variant and not hasattr(L, name):
+            continue   # an older A/B build may predate an entry point; the shipped library has all
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

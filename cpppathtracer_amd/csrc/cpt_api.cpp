@@ -298,11 +298,14 @@ PathTracer::PathTracer() {}
 
 PathTracer::~PathTracer() {
     Stop();
-    if (ctx_) cpt_destroy(ctx_);
+    for (Tile& t : tiles_)
+        if (t.ctx) cpt_destroy(t.ctx);
+    if (frame_) cpt_destroy(frame_);
 }
 
-bool PathTracer::Fail(const char* what) {
-    err_ = std::string(what) + ": " + (ctx_ ? cpt_last_error(ctx_) : cpt_last_error(nullptr));
+bool PathTracer::Fail(const char* what, cpt_ctx* ctx) {
+    if (!ctx) ctx = FrameCtx();
+    err_ = std::string(what) + ": " + (ctx ? cpt_last_error(ctx) : cpt_last_error(nullptr));
     fprintf(stderr, "[cpt] %s\n", err_.c_str());   // the reference logs and continues
     return false;
 }
@@ -324,122 +327,202 @@ bool PathTracer::SetMaxRecursionDepth(uint depth) {
 void PathTracer::SetSeed(uint64_t seed) {
     std::lock_guard<std::mutex> lk(mu_);
     seed_ = seed;
-    rng_ready_ = false;
+    for (Tile& t : tiles_) t.rng_ready = false;
 }
 
 bool PathTracer::SetDevice(int device) {
     std::lock_guard<std::mutex> lk(mu_);
-    if (ctx_) {
+    if (!tiles_.empty()) {
         err_ = "SetDevice: the context already exists";
         return false;
     }
     device_ = device;
+    device_list_.clear();
+    return true;
+}
+
+bool PathTracer::SetDevices(int n) {
+    if (n < 1) {
+        err_ = "SetDevices: n must be >= 1";
+        return false;
+    }
+    int visible = 0;
+    if (cpt_get_device_count(&visible) != CPT_OK || visible < 1) {
+        err_ = "SetDevices: no HIP device visible";
+        return false;
+    }
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) devs[i] = i % visible;
+    return SetDevices(devs);
+}
+
+bool PathTracer::SetDevices(const std::vector<int>& devices) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!tiles_.empty()) {
+        err_ = "SetDevices: the contexts already exist";
+        return false;
+    }
+    if (devices.empty()) {
+        err_ = "SetDevices: empty device list";
+        return false;
+    }
+    device_list_ = devices.size() > 1 ? devices : std::vector<int>{};
+    device_ = devices[0];
     return true;
 }
 
 bool PathTracer::SetEnvTexture(PocaTexture tex) {
     std::lock_guard<std::mutex> lk(mu_);
     env_ = tex;
-    env_uploaded_ = false;
+    for (Tile& t : tiles_) t.env_uploaded = false;
     return true;
 }
 
+// One context per device of the row tiling (a single one without SetDevices), plus, with
+// several, the frame context on the first device that receives the gathered tiles.
 bool PathTracer::EnsureContext() {
-    if (ctx_) return true;
-    if (cpt_create(device_, &ctx_) != CPT_OK) {
-        ctx_ = nullptr;
-        return Fail("cpt_create");
+    if (!tiles_.empty()) return true;
+    const std::vector<int> devs = device_list_.empty() ? std::vector<int>{device_} : device_list_;
+    std::vector<Tile> tiles(devs.size());
+    for (size_t i = 0; i < devs.size(); ++i) {
+        tiles[i].device = devs[i];
+        if (cpt_create(devs[i], &tiles[i].ctx) != CPT_OK) {
+            tiles[i].ctx = nullptr;
+            for (Tile& t : tiles)
+                if (t.ctx) cpt_destroy(t.ctx);
+            return Fail("cpt_create", nullptr);
+        }
     }
+    if (devs.size() > 1 && cpt_create(devs[0], &frame_) != CPT_OK) {
+        frame_ = nullptr;
+        for (Tile& t : tiles) cpt_destroy(t.ctx);
+        return Fail("cpt_create", nullptr);
+    }
+    tiles_ = std::move(tiles);
     return true;
 }
 
 // Binds every material texture handle `objs` use that the context does not hold yet.
-bool PathTracer::BindTextures(const std::vector<cpt_object>& objs) {
+bool PathTracer::BindTextures(Tile& tile, const std::vector<cpt_object>& objs) {
     for (const cpt_object& o : objs) {
         if (!o.material.have_tex) continue;
         const uint64_t h = o.material.u.tex;
-        if (std::find(bound_textures_.begin(), bound_textures_.end(), h) != bound_textures_.end()) continue;
+        if (std::find(tile.bound_textures.begin(), tile.bound_textures.end(), h) != tile.bound_textures.end()) continue;
         const PocaTextureData* t = PocaTextureUtils::Get(h);
         if (!t) { err_ = "textured material uses an unknown PocaTexture handle"; return false; }
-        if (cpt_bind_texture(ctx_, h, t->rgba.data(), t->width, t->height, t->valid_cols, address_mode_of(t->addr),
+        if (cpt_bind_texture(tile.ctx, h, t->rgba.data(), t->width, t->height, t->valid_cols, address_mode_of(t->addr),
                              t->filter == PocaFilterMode::Point ? CPT_FILTER_POINT : CPT_FILTER_LINEAR) != CPT_OK)
-            return Fail("cpt_bind_texture");
-        bound_textures_.push_back(h);
+            return Fail("cpt_bind_texture", tile.ctx);
+        tile.bound_textures.push_back(h);
     }
     return true;
 }
 
-// Brings the context to SceneBVH's state: a new build is uploaded as BuildBVH copied it (the
+// Brings one context to SceneBVH's state: a new build is uploaded as BuildBVH copied it (the
 // reference's topology), then the objects UpdateObject re-copied since are refit in one batch
 // (bvh.cu:144-157).  The state is read under one lock (SceneBVH::GetState).
-bool PathTracer::SyncScene() {
-    if (!EnsureContext()) return false;
-    if (!scene_synced_ || SceneBVH::Revision() != scene_rev_) {
+bool PathTracer::SyncTile(Tile& tile) {
+    if (!tile.scene_synced || SceneBVH::Revision() != tile.scene_rev) {
         uint64_t build = 0, rev = 0;
         std::vector<cpt_object> built, current;
         std::vector<uint64_t> updates;
-        const bool rebuild = !scene_synced_ || SceneBVH::BuildId() != scene_build_;
+        const bool rebuild = !tile.scene_synced || SceneBVH::BuildId() != tile.scene_build;
         SceneBVH::GetState(build, rev, rebuild ? &built : nullptr, current, updates);
-        if (!rebuild && build != scene_build_)   // rebuilt between the two reads
+        if (!rebuild && build != tile.scene_build)   // rebuilt between the two reads
             SceneBVH::GetState(build, rev, &built, current, updates);
-        if (rebuild || build != scene_build_) {
-            bound_textures_.clear();
-            if (!BindTextures(built)) return false;
-            if (cpt_set_scene(ctx_, built.empty() ? nullptr : built.data(), (int)built.size()) != CPT_OK)
-                return Fail("cpt_set_scene");
-            scene_build_ = build;
-            updates_seen_.assign(built.size(), 0);
+        if (rebuild || build != tile.scene_build) {
+            tile.bound_textures.clear();
+            if (!BindTextures(tile, built)) return false;
+            if (cpt_set_scene(tile.ctx, built.empty() ? nullptr : built.data(), (int)built.size()) != CPT_OK)
+                return Fail("cpt_set_scene", tile.ctx);
+            tile.scene_build = build;
+            tile.updates_seen.assign(built.size(), 0);
         }
         std::vector<int> idx;
         std::vector<cpt_object> objs;
-        for (size_t i = 0; i < updates.size() && i < updates_seen_.size(); ++i)
-            if (updates[i] != updates_seen_[i]) {
+        for (size_t i = 0; i < updates.size() && i < tile.updates_seen.size(); ++i)
+            if (updates[i] != tile.updates_seen[i]) {
                 idx.push_back((int)i);
                 objs.push_back(current[i]);
             }
         if (!idx.empty()) {
-            if (!BindTextures(objs)) return false;
-            if (cpt_update_objects(ctx_, (int)idx.size(), idx.data(), objs.data()) != CPT_OK)
-                return Fail("cpt_update_objects");
+            if (!BindTextures(tile, objs)) return false;
+            if (cpt_update_objects(tile.ctx, (int)idx.size(), idx.data(), objs.data()) != CPT_OK)
+                return Fail("cpt_update_objects", tile.ctx);
         }
-        updates_seen_ = updates;
-        scene_rev_ = rev;
-        scene_synced_ = true;
+        tile.updates_seen = updates;
+        tile.scene_rev = rev;
+        tile.scene_synced = true;
     }
-    if (!env_uploaded_) {
+    if (!tile.env_uploaded) {
         if (env_ == 0) env_ = PocaTextureUtils::AddTexByFile(default_sky_path());   // path_tracer.cu:47
         const PocaTextureData* t = PocaTextureUtils::Get(env_);
-        int rc = t ? cpt_set_env_texture(ctx_, t->rgba.data(), t->width, t->height, t->valid_cols)
-                   : cpt_set_env_texture(ctx_, nullptr, 1, 1, 0);
-        if (rc != CPT_OK) return Fail("cpt_set_env_texture");
-        env_uploaded_ = true;
+        int rc = t ? cpt_set_env_texture(tile.ctx, t->rgba.data(), t->width, t->height, t->valid_cols)
+                   : cpt_set_env_texture(tile.ctx, nullptr, 1, 1, 0);
+        if (rc != CPT_OK) return Fail("cpt_set_env_texture", tile.ctx);
+        tile.env_uploaded = true;
     }
     return true;
+}
+
+bool PathTracer::SyncScene() {
+    if (!EnsureContext()) return false;
+    for (Tile& t : tiles_)
+        if (!SyncTile(t)) return false;
+    return true;
+}
+
+// Image rows of tile r of n: interleaved 8-row blocks (cpppathtracer_amd/tiling.py).
+static std::vector<int32_t> tile_rows(int height, int n, int r) {
+    std::vector<int32_t> rows;
+    for (int y = 0; y < height; ++y)
+        if ((y / 8) % n == r) rows.push_back(y);
+    return rows;
 }
 
 // InitBuffers (path_tracer.cu:44-115): per-pixel buffers and RNG when the size changes.
 bool PathTracer::EnsureFrame(const MotionalCamera& cam) {
+    const int n = (int)tiles_.size();
     if (cam.width_ != width_ || cam.height_ != height_) {
-        if (cpt_set_frame(ctx_, cam.width_, cam.height_, nullptr, 0) != CPT_OK) return Fail("cpt_set_frame");
+        for (int r = 0; r < n; ++r) {
+            const std::vector<int32_t> rows = tile_rows(cam.height_, n, r);
+            const int rc = n == 1 ? cpt_set_frame(tiles_[r].ctx, cam.width_, cam.height_, nullptr, 0)
+                                  : cpt_set_frame(tiles_[r].ctx, cam.width_, cam.height_, rows.data(), (int)rows.size());
+            if (rc != CPT_OK) return Fail("cpt_set_frame", tiles_[r].ctx);
+            tiles_[r].rng_ready = false;
+        }
+        if (frame_ && cpt_set_frame(frame_, cam.width_, cam.height_, nullptr, 0) != CPT_OK) return Fail("cpt_set_frame", frame_);
         width_ = cam.width_;
         height_ = cam.height_;
-        rng_ready_ = false;
         output_buffer_.assign((size_t)width_ * height_ * 4, 0);
     }
-    if (!rng_ready_) {
-        if (cpt_init_rng(ctx_, seed_) != CPT_OK) return Fail("cpt_init_rng");
-        rng_ready_ = true;
-    }
+    for (Tile& t : tiles_)
+        if (!t.rng_ready) {
+            if (cpt_init_rng(t.ctx, seed_) != CPT_OK) return Fail("cpt_init_rng", t.ctx);
+            t.rng_ready = true;
+        }
     return true;
 }
 
+// One render of `spp` passes: every tile's launch is queued first (each context's work runs on
+// its own device and stream), then the tiles are gathered into the frame context.
 bool PathTracer::RenderPass(MotionalCamera& cam, int spp, bool accumulate) {
     if (!SyncScene() || !EnsureFrame(cam)) return false;
     // many passes per pixel: heaviest tiles first (same image, shorter tail)
-    uint32_t flags = CPT_RENDER_AUX | (accumulate ? CPT_RENDER_ACCUMULATE : 0u) | CPT_RENDER_SYNC |
-                     (ordered_walk_ ? CPT_TRAVERSAL_ORDERED : 0u) | (spp >= 64 ? CPT_SCHEDULE_COST : 0u);
-    if (cpt_render(ctx_, reinterpret_cast<const cpt_camera*>(&cam), spp, (int)max_recursion_depth_, flags) != CPT_OK)
-        return Fail("cpt_render");
+    const uint32_t flags = CPT_RENDER_AUX | (accumulate ? CPT_RENDER_ACCUMULATE : 0u) |
+                           (ordered_walk_ ? CPT_TRAVERSAL_ORDERED : 0u) | (spp >= 64 ? CPT_SCHEDULE_COST : 0u);
+    if (!frame_) {
+        if (cpt_render(tiles_[0].ctx, reinterpret_cast<const cpt_camera*>(&cam), spp, (int)max_recursion_depth_,
+                       flags | CPT_RENDER_SYNC) != CPT_OK)
+            return Fail("cpt_render", tiles_[0].ctx);
+        return true;
+    }
+    for (Tile& t : tiles_)
+        if (cpt_render(t.ctx, reinterpret_cast<const cpt_camera*>(&cam), spp, (int)max_recursion_depth_, flags) != CPT_OK)
+            return Fail("cpt_render", t.ctx);
+    for (Tile& t : tiles_)
+        if (cpt_gather_rows(frame_, t.ctx) != CPT_OK) return Fail("cpt_gather_rows", frame_);
+    if (cpt_synchronize(frame_) != CPT_OK) return Fail("cpt_synchronize", frame_);
     return true;
 }
 
@@ -480,7 +563,7 @@ void PathTracer::PipelineLoop() {
         {
             std::lock_guard<std::mutex> lk(mu_);
             ok = RenderPass(cma, 1, false);
-            if (ok && cpt_denoise_mix(ctx_, cma.cur_sample_idx_, output_buffer_.data()) != CPT_OK)
+            if (ok && cpt_denoise_mix(FrameCtx(), cma.cur_sample_idx_, output_buffer_.data()) != CPT_OK)
                 ok = Fail("cpt_denoise_mix");
         }
         if (ok && task.Callback) task.Callback(output_buffer_.data(), width_, height_, task.cbParam);
@@ -506,12 +589,12 @@ bool PathTracer::Render(int spp, bool accumulate) {
 
 bool PathTracer::ReadRadiance(std::vector<float>& rgb) {
     std::lock_guard<std::mutex> lk(mu_);
-    if (!ctx_ || width_ == 0) {
+    if (!FrameCtx() || width_ == 0) {
         err_ = "ReadRadiance: nothing rendered";
         return false;
     }
     std::vector<float> acc((size_t)width_ * height_ * 4);
-    if (cpt_read_accum(ctx_, acc.data()) != CPT_OK) return Fail("cpt_read_accum");
+    if (cpt_read_accum(FrameCtx(), acc.data()) != CPT_OK) return Fail("cpt_read_accum");
     rgb.resize((size_t)width_ * height_ * 3);
     for (size_t i = 0; i < (size_t)width_ * height_; ++i) {
         float n = acc[4 * i + 3] > 0.f ? acc[4 * i + 3] : 1.f;
@@ -542,8 +625,20 @@ bool PathTracer::SaveRadiancePFM(const std::string& path) {
     return (bool)f;
 }
 
+// Counters summed over the tiles (the render flags do not ask for CPT_RENDER_STATS, so these
+// are the counters of the last counting render; GetStats after cpt-level counting renders).
 bool PathTracer::GetStats(cpt_stats* out) {
     std::lock_guard<std::mutex> lk(mu_);
-    if (!ctx_) return false;
-    return cpt_get_stats(ctx_, out) == CPT_OK;
+    if (tiles_.empty() || !out) return false;
+    *out = cpt_stats{};
+    for (Tile& t : tiles_) {
+        cpt_stats s{};
+        if (cpt_get_stats(t.ctx, &s) != CPT_OK) return Fail("cpt_get_stats", t.ctx);
+        out->segments += s.segments;
+        out->node_visits += s.node_visits;
+        out->prim_tests += s.prim_tests;
+        out->hits += s.hits;
+        out->misses += s.misses;
+    }
+    return true;
 }

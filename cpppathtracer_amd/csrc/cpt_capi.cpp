@@ -12,6 +12,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <queue>
 #include <string>
 #include <functional>
 #include <vector>
@@ -356,6 +357,16 @@ struct cpt_ctx {
     int band_y0 = -1, band_y1 = -1;   // display band the buffers hold
     float last_kernel_ms = 0.f;
     int last_launches = 0;
+    // row-tile gather (cpt_gather_rows): a source's rows staged on this device, and the frame
+    // row each goes to
+    float4* d_gather = nullptr;
+    size_t cap_gather = 0;
+    int32_t* d_gather_map = nullptr;
+    size_t cap_gather_map = 0;
+    std::vector<int32_t> gather_map_h;
+    // consolidation test hooks (cpt_set_debug_consolidation)
+    uint32_t dbg = 0;
+    int keeper_spin_log2 = 0, publish_wait_log2 = 0;
 
     hipStream_t stream() const { return user_stream ? user_stream : own_stream; }
 };
@@ -547,18 +558,10 @@ int build(HostBvh& t, const std::vector<cpt_object>& O, std::vector<int>& idx, i
 // 4-wide walk tree (DESIGN.md §Wide walk).  The binary SAH walk tree is collapsed into
 // nodes of up to four children: starting from a node's two children, the internal child
 // with the largest box is replaced by its own two children until there are four (or only
-// leaves).  Every octant gets its own copy: the children in the near-first order of the
-// binary splits between the node and them (the binary octant order's rule), each child's
-// box in octant form (entry planes, exit planes).  Layout of one 128-B node, 32 dwords:
-//   [0..3] entry x of children 0..3, [4..7] entry y, [8..11] entry z,
-//   [12..15] exit x, [16..19] exit y, [20..23] exit z,
-//   [24..27] child refs: >= 0 a wide node of the same octant, <= -2 a leaf as ~(absolute
-//            Node index of the leaf in the octant-0 binary order), empty slots -1 with an
-//            inverted box that every ray rejects,
-//   [28..31] 0.
-// Nodes are numbered in preorder (root 0); octant o's node k starts at Node slot
-// n_bvh + 8 n_walk + 4 (o n_wide + k).  Returns n_wide, or 0 when the device walk's stack
-// (WIDE_STACK entries per lane, cpt_path.hpp) could overflow on this tree.
+// leaves).  Appended to `out` (after the eight binary octant orders): the compact image,
+// 7 x 16 B per node (layout below), then the leaf array.  Nodes are numbered largest box
+// first (root 0).  Returns n_wide, or 0 when the device walk's stack (WIDE_STACK entries per
+// lane, cpt_path.hpp) could overflow on this tree or a ref would not fit 15 bits.
 // ------------------------------------------------------------------------------------
 constexpr int WIDE_STACK = CPT_WSTACK;
 
@@ -598,6 +601,34 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
     make(root, n_unb);   // the walk starts with the root and the platforms on the stack
     if (max_push + 1 > WIDE_STACK) return 0;
     const int n_wide = (int)wbin.size();
+    // Renumber the wide nodes largest box first, every node after its parent (a best-first
+    // expansion from the root by surface area, which a random ray hits in proportion to): the
+    // device stages the first LDS_TREE_NODES of them in LDS, so a larger tree keeps its top there.
+    {
+        std::vector<int> order;   // new id -> old id
+        order.reserve(n_wide);
+        std::priority_queue<std::pair<float, int>, std::vector<std::pair<float, int>>, std::greater<>> pq;
+        pq.emplace(-area(wbin[0]), 0);
+        while (!pq.empty()) {
+            const int id = pq.top().second;
+            pq.pop();
+            order.push_back(id);
+            for (int x : kids[id])
+                if (!w.nodes[x].is_object) pq.emplace(-area(x), wide_of[x]);
+        }
+        std::vector<int> new_id(n_wide);
+        for (int k = 0; k < n_wide; ++k) new_id[order[k]] = k;
+        std::vector<int> wbin2(n_wide);
+        std::vector<std::vector<int>> kids2(n_wide);
+        for (int k = 0; k < n_wide; ++k) {
+            wbin2[k] = wbin[order[k]];
+            kids2[k] = kids[order[k]];
+        }
+        wbin.swap(wbin2);
+        kids.swap(kids2);
+        for (int& x : wide_of)
+            if (x >= 0) x = new_id[x];
+    }
     // the device stack holds 16-bit refs: wide node ids and ~(leaf position) within 15 bits
     if (n_wide > 32767) return 0;
     for (int p : pos0)
@@ -617,76 +648,44 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
     if ((int)leaf_pos.size() > 32765) return 0;
     const size_t base = out.size();
     const size_t n_compact = (size_t)(n_wide * 7 + 1) / 2;
-    out.resize(base + (size_t)8 * n_wide * 4 + n_compact + leaf_pos.size());
-    for (size_t i = 0; i < leaf_pos.size(); ++i)
-        out[base + (size_t)8 * n_wide * 4 + n_compact + i] = out[(size_t)n_bvh + leaf_pos[i]];
+    out.resize(base + n_compact + leaf_pos.size());
+    for (size_t i = 0; i < leaf_pos.size(); ++i) out[base + n_compact + i] = out[(size_t)n_bvh + leaf_pos[i]];
     *n_leaves_out = (int)leaf_pos.size();
-    // The compact image after the eight octant copies (k_megakernel stages it in LDS when it
-    // fits, cpt_path.hpp trace_wide): 7 x 16 B per node, one copy for every octant --
-    //   [min x][max x][min y][max y][min z][max z] of the four slots (octant 0's order), then
+    // The compact image (cpt_path.hpp trace_wide; its first LDS_TREE_NODES nodes are staged in
+    // LDS): 7 x 16 B per node, one copy for every direction octant --
+    //   [min x][max x][min y][max y][min z][max z] of the four slots, then
     //   {refs of slots 0..3 as int16, 8 B zero}.
-    // A lane reads its entry planes at min or max by the sign of its direction, so its slab
-    // distances are bit for bit those of its octant's copy; it orders the hit children by
-    // their entry distances.
-    uint32_t* compact = reinterpret_cast<uint32_t*>(&out[base + (size_t)8 * n_wide * 4]);
-    std::vector<std::vector<int>> ord0(n_wide);
-    for (int o = 0; o < 8; ++o) {
-        for (int id = 0; id < n_wide; ++id) {
-            const std::vector<int>& ch = kids[id];
-            std::vector<int> ord;
-            std::function<void(int)> rec = [&](int x) {
-                if (std::find(ch.begin(), ch.end(), x) != ch.end()) { ord.push_back(x); return; }
-                const BNode& n = w.nodes[x];
-                const bool right_first = (o >> n.axis) & 1;
-                rec(right_first ? n.right : n.left);
-                rec(right_first ? n.left : n.right);
-            };
-            rec(wbin[id]);
-            if (o == 0) ord0[id] = ord;
-            {
-                const std::vector<int>& o0 = ord0[id];
-                uint32_t* q = compact + (size_t)id * 28;
-                if (o == 0) {
-                    for (int k = 0; k < 4; ++k) {
-                        F3 lo{1e30f, 1e30f, 1e30f}, hi{-1e30f, -1e30f, -1e30f};
-                        int32_t r = -1;
-                        if (k < (int)o0.size()) {
-                            const BNode& n = w.nodes[o0[k]];
-                            lo = n.bmin;
-                            hi = n.bmax;
-                            r = n.is_object ? ~(li_of[o0[k]] + 1) : wide_of[o0[k]];
-                        }
-                        const float l3[3] = {lo.x, lo.y, lo.z}, h3[3] = {hi.x, hi.y, hi.z};
-                        for (int a = 0; a < 3; ++a) {
-                            std::memcpy(&q[(2 * a) * 4 + k], &l3[a], 4);
-                            std::memcpy(&q[(2 * a + 1) * 4 + k], &h3[a], 4);
-                        }
-                        q[24 + (k >> 1)] |= (uint32_t)(uint16_t)(int16_t)r << (16 * (k & 1));
-                    }
-                }
+    // A lane reads its entry planes at min or max by the sign of its direction, i.e. the planes
+    // its octant enters through, and orders the hit children by their entry distances.  The
+    // slots are in the order of the binary splits between the node and its children (left
+    // first); an empty slot has an inverted box that every ray rejects.
+    uint32_t* compact = reinterpret_cast<uint32_t*>(&out[base]);
+    std::memset(compact, 0, n_compact * sizeof(Node));
+    for (int id = 0; id < n_wide; ++id) {
+        const std::vector<int>& ch = kids[id];
+        std::vector<int> ord;
+        std::function<void(int)> rec = [&](int x) {
+            if (std::find(ch.begin(), ch.end(), x) != ch.end()) { ord.push_back(x); return; }
+            rec(w.nodes[x].left);
+            rec(w.nodes[x].right);
+        };
+        rec(wbin[id]);
+        uint32_t* q = compact + (size_t)id * 28;
+        for (int k = 0; k < 4; ++k) {
+            F3 lo{1e30f, 1e30f, 1e30f}, hi{-1e30f, -1e30f, -1e30f};
+            int32_t r = -1;
+            if (k < (int)ord.size()) {
+                const BNode& n = w.nodes[ord[k]];
+                lo = n.bmin;
+                hi = n.bmax;
+                r = n.is_object ? ~(li_of[ord[k]] + 1) : wide_of[ord[k]];
             }
-            float f[24];
-            int32_t ref[4];
-            for (int k = 0; k < 4; ++k) {
-                F3 lo{1e30f, 1e30f, 1e30f}, hi{-1e30f, -1e30f, -1e30f};
-                ref[k] = -1;
-                if (k < (int)ord.size()) {
-                    const BNode& n = w.nodes[ord[k]];
-                    lo = n.bmin;
-                    hi = n.bmax;
-                    ref[k] = n.is_object ? ~pos0[ord[k]] : wide_of[ord[k]];
-                }
-                const float l3[3] = {lo.x, lo.y, lo.z}, h3[3] = {hi.x, hi.y, hi.z};
-                for (int a = 0; a < 3; ++a) {
-                    const bool neg = (o >> a) & 1;
-                    f[a * 4 + k] = neg ? h3[a] : l3[a];         // entry plane
-                    f[12 + a * 4 + k] = neg ? l3[a] : h3[a];    // exit plane
-                }
+            const float l3[3] = {lo.x, lo.y, lo.z}, h3[3] = {hi.x, hi.y, hi.z};
+            for (int a = 0; a < 3; ++a) {
+                std::memcpy(&q[(2 * a) * 4 + k], &l3[a], 4);
+                std::memcpy(&q[(2 * a + 1) * 4 + k], &h3[a], 4);
             }
-            uint32_t dw[32] = {0};
-            std::memcpy(dw, f, sizeof(f));
-            std::memcpy(dw + 24, ref, sizeof(ref));
-            std::memcpy(&out[base + ((size_t)o * n_wide + id) * 4], dw, sizeof(dw));
+            q[24 + (k >> 1)] |= (uint32_t)(uint16_t)(int16_t)r << (16 * (k & 1));
         }
     }
     return n_wide;
@@ -740,6 +739,26 @@ int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, s
     for (size_t i = 0; i < w.nodes.size(); ++i)
         if (w.nodes[i].is_object) rank[i] = c->pos_of_node[c->bvh.leaf_of_object[w.nodes[i].obj]];
     return root;
+}
+
+// The kernels' sticky error word (KParams::error, CPT_DEVERR_*): read after the context's
+// stream has drained; a set word is cleared and reported once, like a sticky HIP error.
+int check_device_error(cpt_ctx* c) {
+    uint32_t v = 0;
+    HIP_TRY(c, hipMemcpy(&v, c->d_work + 4, sizeof(v), hipMemcpyDeviceToHost));
+    if (v == 0) return CPT_OK;
+    HIP_TRY(c, hipMemset(c->d_work + 4, 0, sizeof(v)));
+    return fail(c, CPT_ERR_DEVICE, "device error 0x%x:%s%s%s", v,
+                (v & cpt::CPT_DEVERR_KEEPER_TIMEOUT) ? " a keeper wave gave up with chains still live (pixels left unfinished);" : "",
+                (v & cpt::CPT_DEVERR_PUBLISH_TIMEOUT) ? " a handed-over chain was never published (its pixel was not written);" : "",
+                (v & cpt::CPT_DEVERR_RESUME_CAP) ? " the consolidation slab is too small for the grid;" : "");
+}
+
+// Drain the context's stream, then report a device-side error of the work it ran.
+int sync_checked(cpt_ctx* c) {
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    return check_device_error(c);
 }
 
 int upload_scene(cpt_ctx* c) {
@@ -804,6 +823,7 @@ const char* cpt_status_string(int status) {
         case CPT_ERR_OUT_OF_MEMORY: return "out of device memory";
         case CPT_ERR_STATE: return "invalid state";
         case CPT_ERR_UNSUPPORTED: return "unsupported";
+        case CPT_ERR_DEVICE: return "device-side error";
         default: return "unknown status";
     }
 }
@@ -832,7 +852,8 @@ int cpt_create(int device, cpt_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&c->ev_stop);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_main);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 32 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMalloc((void**)&c->d_work, 64);
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_work, 64);   // [0] dequeue counter, [4] error word
+    if (e == hipSuccess) e = hipMemset(c->d_work, 0, 64);
     if (e == hipSuccess) e = hipMemset(c->d_stats, 0, 32 * sizeof(unsigned long long));
     if (e == hipSuccess) {
         const std::vector<uint32_t>& J = jump_tables();
@@ -864,6 +885,8 @@ int cpt_destroy(cpt_ctx* c) {
     (void)hipFree(c->d_stats);
     (void)hipFree(c->d_work);
     (void)hipFree(c->d_resume);
+    (void)hipFree(c->d_gather);
+    (void)hipFree(c->d_gather_map);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
@@ -1112,8 +1135,7 @@ int cpt_init_rng(cpt_ctx* c, uint64_t seed) {
 int cpt_read_rng(cpt_ctx* c, uint32_t* planar6) {
     if (!c || !planar6) return CPT_ERR_INVALID_ARG;
     if (!c->frame_set) return fail(c, CPT_ERR_STATE, "cpt_read_rng: no frame");
-    HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    if (int rc = sync_checked(c)) return rc;
     size_t n = 6 * (size_t)c->n_rows * c->width;
     if (n) HIP_TRY(c, hipMemcpy(planar6, c->d_rng, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return CPT_OK;
@@ -1184,7 +1206,14 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     p.max_depth = max_depth;
     p.accumulate = (flags & CPT_RENDER_ACCUMULATE) ? 1 : 0;
     p.lanes = 64;
-    if (const char* e = getenv("CPT_LANES_PER_WAVE")) p.lanes = std::max(1, std::min(64, atoi(e)));   // DIAGNOSTIC
+#ifdef CPT_DIAGNOSTIC_LANES
+    // lane-latency experiments (tools/lane_latency.py builds with -DCPT_DIAGNOSTIC_LANES)
+    if (const char* e = getenv("CPT_LANES_PER_WAVE")) p.lanes = std::max(1, std::min(64, atoi(e)));
+#endif
+    p.error = c->d_work + 4;
+    p.dbg = c->dbg;
+    p.keeper_spin_log2 = c->keeper_spin_log2;
+    p.publish_wait_log2 = c->publish_wait_log2;
     const bool wavefront = (flags & CPT_PATH_WAVEFRONT) != 0;
     if (wavefront && !c->wf_ready && c->n_rows > 0) {
         const size_t npix = (size_t)c->n_rows * c->width;
@@ -1254,22 +1283,78 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     }
     HIP_TRY(c, hipEventRecord(c->ev_stop, s));
     c->have_timing = true;
-    if (flags & CPT_RENDER_SYNC) HIP_TRY(c, hipStreamSynchronize(s));
+    if (flags & CPT_RENDER_SYNC) return sync_checked(c);
+    return CPT_OK;
+}
+
+// Row-tile gather: the rows `src` rendered, placed into `dst`'s frame at the
+// same global rows.  One peer copy of src's buffers to dst's device (hipMemcpyPeerAsync: xGMI
+// between two MI355X, a plain device copy when both contexts share a GPU), then one stitch
+// kernel on dst's stream.  Waits for src; asynchronous with respect to dst.
+int cpt_gather_rows(cpt_ctx* dst, cpt_ctx* src) {
+    if (!dst || !src || dst == src) return dst ? fail(dst, CPT_ERR_INVALID_ARG, "cpt_gather_rows: bad contexts") : CPT_ERR_INVALID_ARG;
+    if (!dst->frame_set || !src->frame_set) return fail(dst, CPT_ERR_STATE, "cpt_gather_rows: both contexts need a frame");
+    if (dst->width != src->width || dst->height != src->height)
+        return fail(dst, CPT_ERR_INVALID_ARG, "cpt_gather_rows: frame %dx%d vs %dx%d", dst->width, dst->height, src->width,
+                    src->height);
+    std::vector<int32_t> at(dst->height, -1);   // dst row index of each global row (first occurrence)
+    for (int j = dst->n_rows - 1; j >= 0; --j) at[dst->rows_h[j]] = j;
+    dst->gather_map_h.resize(src->n_rows);
+    for (int i = 0; i < src->n_rows; ++i) {
+        const int32_t j = at[src->rows_h[i]];
+        if (j < 0) return fail(dst, CPT_ERR_INVALID_ARG, "cpt_gather_rows: row %d is not in the destination frame", src->rows_h[i]);
+        dst->gather_map_h[i] = j;
+    }
+    if (src->n_rows == 0) return CPT_OK;
+    if (int rc = sync_checked(src)) return fail(dst, rc, "cpt_gather_rows: source: %s", src->err.c_str());
+    const size_t npix = (size_t)src->n_rows * src->width;
+    const bool aux = src->d_normal && src->d_depth;
+    HIP_TRY(dst, hipSetDevice(dst->device));
+    hipStream_t s = dst->stream();
+    const size_t dst_npix = (size_t)dst->n_rows * dst->width;
+    if (aux) {
+        if (!dst->d_normal) HIP_TRY(dst, hipMalloc((void**)&dst->d_normal, dst_npix * 3 * sizeof(float)));
+        if (!dst->d_depth) HIP_TRY(dst, hipMalloc((void**)&dst->d_depth, dst_npix * sizeof(float)));
+    }
+    int rc;
+    // staging: accumulator (npix float4), then normals (3 npix floats) and depths (npix floats)
+    if ((rc = ensure(dst, &dst->d_gather, &dst->cap_gather, aux ? 2 * npix : npix)) != CPT_OK) return rc;
+    if ((rc = ensure(dst, &dst->d_gather_map, &dst->cap_gather_map, (size_t)src->n_rows)) != CPT_OK) return rc;
+    float* st_nrm = reinterpret_cast<float*>(dst->d_gather + npix);
+    float* st_dep = st_nrm + 3 * npix;
+    HIP_TRY(dst, hipMemcpyAsync(dst->d_gather_map, dst->gather_map_h.data(), src->n_rows * sizeof(int32_t),
+                                hipMemcpyHostToDevice, s));
+    HIP_TRY(dst, hipMemcpyPeerAsync(dst->d_gather, dst->device, src->d_accum, src->device, npix * sizeof(float4), s));
+    if (aux) {
+        HIP_TRY(dst, hipMemcpyPeerAsync(st_nrm, dst->device, src->d_normal, src->device, npix * 3 * sizeof(float), s));
+        HIP_TRY(dst, hipMemcpyPeerAsync(st_dep, dst->device, src->d_depth, src->device, npix * sizeof(float), s));
+    }
+    HIP_TRY(dst, cpt::launch_stitch_rows(dst->d_gather, aux ? st_nrm : nullptr, aux ? st_dep : nullptr, dst->d_gather_map,
+                                         dst->width, src->n_rows, dst->d_accum, dst->d_normal, dst->d_depth, s));
+    // the host row map is read by the async upload: keep it until the stream passes the copy
+    HIP_TRY(dst, hipStreamSynchronize(s));
+    return CPT_OK;
+}
+
+int cpt_set_debug_consolidation(cpt_ctx* c, uint32_t flags, int keeper_spin_log2, int publish_wait_log2) {
+    if (!c || keeper_spin_log2 < 0 || keeper_spin_log2 > 30 || publish_wait_log2 < 0 || publish_wait_log2 > 30 ||
+        (flags & ~3u))
+        return c ? fail(c, CPT_ERR_INVALID_ARG, "cpt_set_debug_consolidation: bad arguments") : CPT_ERR_INVALID_ARG;
+    c->dbg = flags;
+    c->keeper_spin_log2 = keeper_spin_log2;
+    c->publish_wait_log2 = publish_wait_log2;
     return CPT_OK;
 }
 
 int cpt_synchronize(cpt_ctx* c) {
     if (!c) return CPT_ERR_INVALID_ARG;
-    HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, hipStreamSynchronize(c->stream()));
-    return CPT_OK;
+    return sync_checked(c);
 }
 
 int cpt_read_accum(cpt_ctx* c, float* rgba) {
     if (!c || !rgba) return CPT_ERR_INVALID_ARG;
     if (!c->frame_set) return fail(c, CPT_ERR_STATE, "cpt_read_accum: no frame");
-    HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    if (int rc = sync_checked(c)) return rc;
     size_t n = (size_t)c->n_rows * c->width;
     if (n) HIP_TRY(c, hipMemcpy(rgba, c->d_accum, n * sizeof(float4), hipMemcpyDeviceToHost));
     return CPT_OK;

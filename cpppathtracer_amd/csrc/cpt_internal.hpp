@@ -53,6 +53,22 @@ struct KParams {
     // boundary by retiring waves, 5 x uint4 per chain, ho_slots chains per workgroup.
     uint4* resume;
     size_t resume_cap;      // chains (all workgroups)
+    // Sticky device error word (CPT_DEVERR_*), or-ed by a kernel that had to abandon work; the
+    // host reads and clears it at its next synchronising call (cpt_capi.cpp check_device_error).
+    uint32_t* error;
+    // Test hooks of the consolidation's error paths (cpt_set_debug_consolidation; 0 in normal
+    // use): dbg bit 0 = a phantom live chain in every workgroup (a lost count), bit 1 = hand-overs
+    // never publish their slot; the keeper's idle-spin limit and the hand-over wait as log2
+    // (0 = the defaults, 2^26 and 2^22).
+    uint32_t dbg;
+    int keeper_spin_log2, publish_wait_log2;
+};
+
+// Device error bits (KParams::error).
+enum : uint32_t {
+    CPT_DEVERR_KEEPER_TIMEOUT = 1u,    // a keeper wave gave up waiting while chains were live
+    CPT_DEVERR_PUBLISH_TIMEOUT = 2u,   // a taken hand-over slot was never published (chain lost)
+    CPT_DEVERR_RESUME_CAP = 4u,        // consolidation slab too small for the grid
 };
 
 // Cost schedule (cpt_kernels.hip, DESIGN.md §Cost schedule): a `passes`-pass pilot of the
@@ -87,6 +103,8 @@ hipError_t launch_math_batch(int op, const float* a, const float* b, float* out,
 hipError_t launch_stream_read(const float4* p, size_t n, float* out, int grid, hipStream_t stream);
 hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len,
                                 hipStream_t stream);
+hipError_t launch_stitch_rows(const float4* src_acc, const float* src_nrm, const float* src_dep, const int32_t* dst_row,
+                              int width, int n_rows, float4* acc, float* nrm, float* dep, hipStream_t stream);
 hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
                               int width, int height, int row0, int y0, int y1, uint32_t cur_sample_idx,
                               hipStream_t stream);

@@ -106,10 +106,10 @@ constexpr bool STATIC_FIRST = CPT_STATIC_FIRST != 0;
 #endif
 constexpr int DEFER_MISS_ROUND = CPT_DEFER_MISS_ROUND;
 
-// LDST: the 4-wide walk tree's compact image (<= LDS_TREE_NODES nodes) is staged in LDS once
-// per workgroup, and the walk reads its nodes there instead of from the octant copies in HBM
-// (a lane's node loads become ds_read_b128s: LDS latency instead of L1/L2 latency on every
-// dependent step of the walk).  One 768-lane workgroup per CU shares the copy.
+// LDST: the 4-wide walk tree's compact image (its first LDS_TREE_NODES nodes: the top of the
+// tree) is staged in LDS once per workgroup, and the walk reads those nodes there (a lane's
+// node loads become ds_read_b128s: LDS latency instead of L1/L2 latency on every dependent
+// step of the walk); a larger tree's other nodes come from the image in global memory.
 // One LDS workgroup per CU: 16 waves, 4 per SIMD (the image, the 16-bit stacks and the pending
 // sky fetches take 156 KB of the CU's 160 KB), which caps the kernel at 128 VGPRs.
 #ifndef CPT_LDS_BLOCK
@@ -124,8 +124,8 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     constexpr int BLK = mk_block<LDST>();
     __shared__ uint4 s_tree[LDST ? LDS_TREE_NODES * 7 : 1];
     if (LDST) {
-        const uint4* src = reinterpret_cast<const uint4*>(p.nodes + p.n_nodes + 8 * p.n_walk + 32 * p.n_wide);
-        for (int i = threadIdx.x; i < 7 * p.n_wide; i += BLK) s_tree[i] = src[i];
+        const uint4* src = reinterpret_cast<const uint4*>(p.nodes + wide_image_base(p));
+        for (int i = threadIdx.x; i < 7 * lds_tree_nodes(p.n_wide); i += BLK) s_tree[i] = src[i];
         __syncthreads();
     }
     const int lane = threadIdx.x & 63;
@@ -154,16 +154,22 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     // tail consolidation (see above): this wave's level, the lanes one level holds over the grid
     static_assert(!CONS || (LDST && !PROBE && ho_slots<BLK>() > 0), "consolidation needs the LDS walk");
     constexpr int QS = CONS ? ho_slots<BLK>() : 1;
-    __shared__ uint32_t s_q[CONS ? 3 : 1];   // hand-over queue head, tail; the workgroup's live chains
+    // hand-over queue head, tail; the workgroup's live chains (taken, not finished, counted
+    // before the taking wave can be seen exhausted); its waves still taking pixels
+    __shared__ uint32_t s_q[CONS ? 4 : 1];
     __shared__ uint8_t s_qflag[QS];          // slot published
     const bool cons = CONS && (size_t)(blockIdx.x + 1) * QS <= p.resume_cap;
+    if (CONS && !cons && threadIdx.x == 0) atomicOr(p.error, CPT_DEVERR_RESUME_CAP);   // runs unconsolidated
     uint4* const qslab = cons ? p.resume + 5 * (size_t)blockIdx.x * QS : nullptr;
     volatile uint32_t* const vq = s_q;
     const uint32_t level = __builtin_amdgcn_readfirstlane((uint32_t)(threadIdx.x >> 8));
     bool retiring = false;       // wave-uniform: hand every chain over at its next pass end
     uint32_t idle_spins = 0;
+    const uint32_t keeper_spins = 1u << (p.keeper_spin_log2 > 0 ? p.keeper_spin_log2 : 26);
+    const uint32_t publish_wait = 1u << (p.publish_wait_log2 > 0 ? p.publish_wait_log2 : 22);
     if (cons) {
-        if (threadIdx.x < 3) s_q[threadIdx.x] = 0u;
+        if (threadIdx.x < 4)
+            s_q[threadIdx.x] = threadIdx.x == 3 ? (uint32_t)(BLK / 64) : (threadIdx.x == 2 ? (p.dbg & 1u) : 0u);
         for (int i = threadIdx.x; i < QS; i += BLK) s_qflag[i] = 0;
         __syncthreads();
     }
@@ -186,7 +192,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     for (;;) {
         stamps::lap(5);
         stamps::count(8);
-        if (cons && !retiring && level > 0 && exhausted && vq[2] <= level * 256u) retiring = true;
+        if (cons && !retiring && level > 0 && exhausted && vq[3] == 0u && vq[2] <= level * 256u) retiring = true;
         bool begin = false;   // a lane took a chain: start its next pass
         // ---- take handed-over chains into idle lanes (consolidation) ---------------------
         if (cons && !retiring && exhausted) {
@@ -208,11 +214,21 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 h = __shfl(h, leader);
                 n = __shfl(n, leader);
                 const uint32_t rank = lane_rank(need);
+                bool lost = false;
                 if (((need >> lane) & 1ull) && rank < n) {
                     const uint32_t slot = h + rank;
                     // the slot was allocated before it was written: wait for its publication
                     const volatile uint8_t* fl = s_qflag + slot;
-                    for (uint32_t w = 0; *fl == 0 && w < (1u << 22); ++w) __builtin_amdgcn_s_sleep(1);
+                    for (uint32_t w = 0; *fl == 0 && w < publish_wait; ++w) __builtin_amdgcn_s_sleep(1);
+                    lost = *fl == 0;
+                }
+                if (lost) {
+                    // never published: the chain is abandoned (its pixel is not written) and
+                    // the render reports CPT_DEVERR_PUBLISH_TIMEOUT instead of reading the slot
+                    atomicOr(p.error, CPT_DEVERR_PUBLISH_TIMEOUT);
+                    atomicSub(&s_q[2], 1u);
+                } else if (((need >> lane) & 1ull) && rank < n) {
+                    const uint32_t slot = h + rank;
                     const uint32_t* e = reinterpret_cast<const uint32_t*>(qslab + 5 * (size_t)slot);
                     auto ld4 = [&](int q) {
                         return make_uint4(ld_coherent(e + 4 * q), ld_coherent(e + 4 * q + 1), ld_coherent(e + 4 * q + 2),
@@ -292,6 +308,10 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 if (cons) {   // live chains (taken, not finished): the consolidation's measure
                     const uint64_t t = __ballot(took);
                     if (t && lane == leader) atomicAdd(&s_q[2], (uint32_t)__popcll(t));
+                    // this wave takes no more pixels: after its takes are counted (LDS atomics of
+                    // one wave complete in order), so a keeper that sees no wave still taking and
+                    // no live chain has seen every chain of the workgroup finish
+                    if (exhausted && lane == leader) atomicSub(&s_q[3], 1u);
                 }
             }
         }
@@ -302,8 +322,13 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             if (exhausted) {
                 // a keeper with nothing to do: wait for hand-overs while any chain is live (a
                 // chain in flight is never more than a pass away from its hand-over or its end)
-                if (vq[2] == 0u) break;
-                if (++idle_spins > (1u << 26)) break;   // never hang the device on a lost count
+                if (vq[3] == 0u && vq[2] == 0u) break;
+                if (++idle_spins > keeper_spins) {
+                    // never hang the device on a lost count, but never end silently either:
+                    // chains of this workgroup may be left unfinished
+                    if (lane == 0) atomicOr(p.error, CPT_DEVERR_KEEPER_TIMEOUT);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(16);
             }
             continue;   // taken ids past the frame's rows: take again
@@ -415,7 +440,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                         for (int k = 0; k < 17; ++k)
                             if (AUX || k < 12 || k == 16) st_coherent(e + k, w[k]);
                         wait_stores();   // the payload is in memory before the flag
-                        *(volatile uint8_t*)(s_qflag + slot) = 1;
+                        if (!(p.dbg & 2u)) *(volatile uint8_t*)(s_qflag + slot) = 1;
                         busy = false;
                     }
                     hand_over = false;
@@ -457,6 +482,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         uint64_t a = wave_sum(cnt.segments), b = wave_sum(cnt.nodes), c = wave_sum(cnt.prims);
         uint64_t d = wave_sum(cnt.hits), e = wave_sum(cnt.misses);
         const uint64_t f = wave_sum(cnt.fallbacks);   // ordered walk: certificate fallbacks
+        const uint64_t g = wave_sum(cnt.gnodes);      // wide nodes read from global memory
         if (lane == 0) {
             atomicAdd((unsigned long long*)&p.stats[0], (unsigned long long)a);
             atomicAdd((unsigned long long*)&p.stats[1], (unsigned long long)b);
@@ -464,6 +490,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             atomicAdd((unsigned long long*)&p.stats[3], (unsigned long long)d);
             atomicAdd((unsigned long long*)&p.stats[4], (unsigned long long)e);
             if (f) atomicAdd((unsigned long long*)&p.stats[5], (unsigned long long)f);
+            if (g) atomicAdd((unsigned long long*)&p.stats[6], (unsigned long long)g);
         }
     }
 }
@@ -718,6 +745,36 @@ hipError_t launch_denoise_mix(const float4* accum, const float* normal, const fl
 }
 
 // ======================================================================================
+// Row-tile gather (cpt_gather_rows): a source context's rows, copied to this device as one
+// block (accumulator float4s, then first-hit normals and depths), are scattered to the rows
+// the destination frame holds them at.  One thread per pixel; every access is coalesced.
+// ======================================================================================
+__global__ void __launch_bounds__(256) k_stitch_rows(const float4* __restrict__ src_acc, const float* __restrict__ src_nrm,
+                                                     const float* __restrict__ src_dep, const int32_t* __restrict__ dst_row,
+                                                     int width, float4* __restrict__ acc, float* __restrict__ nrm,
+                                                     float* __restrict__ dep) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.y;
+    if (x >= width) return;
+    const size_t s = (size_t)r * width + x, d = (size_t)dst_row[r] * width + x;
+    acc[d] = src_acc[s];
+    if (src_nrm) {
+        nrm[3 * d] = src_nrm[3 * s];
+        nrm[3 * d + 1] = src_nrm[3 * s + 1];
+        nrm[3 * d + 2] = src_nrm[3 * s + 2];
+        dep[d] = src_dep[s];
+    }
+}
+
+hipError_t launch_stitch_rows(const float4* src_acc, const float* src_nrm, const float* src_dep, const int32_t* dst_row,
+                              int width, int n_rows, float4* acc, float* nrm, float* dep, hipStream_t stream) {
+    if (width <= 0 || n_rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_stitch_rows, dim3((width + 255) / 256, n_rows), dim3(256), 0, stream, src_acc, src_nrm, src_dep,
+                       dst_row, width, acc, nrm, dep);
+    return hipGetLastError();
+}
+
+// ======================================================================================
 // Device-math KAT (see cpt.h cpt_math_batch).
 // ======================================================================================
 __global__ void k_math_batch(int op, const float* a, const float* b, float* out, size_t n) {
@@ -764,14 +821,9 @@ static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// The LDS walk needs the wide tree (ordered walk) and an image that fits.
-static bool use_lds_tree(const KParams& p) {
-#ifdef CPT_NO_LDS_TREE
-    return false;
-#else
-    return p.ordered == 1 && p.n_wide > 0 && p.n_wide <= LDS_TREE_NODES;
-#endif
-}
+// The wide walk (ordered walk on a 4-wide tree) runs in the LDS kernels: the image's first
+// LDS_TREE_NODES nodes in LDS, the rest of a larger tree from global memory.
+static bool use_lds_tree(const KParams& p) { return p.ordered == 1 && p.n_wide > 0; }
 
 template <bool S, bool A, bool P>
 static hipError_t launch_mk_any(const KParams& p, hipStream_t stream) {

@@ -289,6 +289,7 @@ __device__ __forceinline__ Hit hit_attributes(const Node& nd, const RayK& ray, f
 
 struct Counters {
     uint32_t segments, nodes, prims, hits, misses, fallbacks;
+    uint32_t gnodes;   // wide-node visits read from the image in global memory (not the LDS copy)
 };
 
 // Slab test of one internal node (bvh.cu:181-200).  The six plane distances use the exact
@@ -414,16 +415,17 @@ struct BufSrc {
 };
 
 // The wide tree's compact image (cpt_capi.cpp linearise_wide): 7 x 16 B per node, after the
-// eight octant copies; padded to whole 32-B Nodes.
+// eight binary octant orders; padded to whole 32-B Nodes.
 __host__ __device__ __forceinline__ int wide_compact_nodes(int n_wide) { return (7 * n_wide + 1) / 2; }
-// Node index of the wide tree's leaf array (the compact image's leaf refs index it).
+// Node index of the compact image, and of the wide tree's leaf array after it (the image's
+// leaf refs index that array).
+__host__ __device__ __forceinline__ int wide_image_base(const KParams& p) { return p.n_nodes + 8 * p.n_walk; }
 __host__ __device__ __forceinline__ int wide_leaves_base(const KParams& p) {
-    return p.n_nodes + 8 * p.n_walk + 32 * p.n_wide + wide_compact_nodes(p.n_wide);
+    return wide_image_base(p) + wide_compact_nodes(p.n_wide);
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t node_rsrc(const KParams& p) {
-    const uint32_t bytes = (uint32_t)(p.n_nodes + 8 * p.n_walk + 32 * p.n_wide + wide_compact_nodes(p.n_wide) +
-                                      p.n_leaves) * (uint32_t)sizeof(Node);
+    const uint32_t bytes = (uint32_t)(wide_leaves_base(p) + p.n_leaves) * (uint32_t)sizeof(Node);
     return __builtin_amdgcn_make_buffer_rsrc((void*)p.nodes, (short)0, (int)bytes, 0x00020000);
 }
 
@@ -579,8 +581,8 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
 constexpr int SPEC_LEAF_ROUND = CPT_SPEC_LEAF_ROUND;
 
 // ======================================================================================
-// The ordered walk on the 4-wide walk tree (DESIGN.md §Wide walk).  One iteration loads a
-// 128-B node (cpt_capi.cpp linearise_wide; 112 B of it are read) and tests its four
+// The ordered walk on the 4-wide walk tree (DESIGN.md §Wide walk).  One iteration reads a
+// 112-B node of the tree's compact image (cpt_capi.cpp linearise_wide) and tests its four
 // children's boxes with the conservative octant-form slab; the nearest hit child is taken
 // next, the other hits go onto a per-lane stack in LDS (far ones first).  Leaves are parked
 // and tested in wave-wide rounds: a lane that meets a leaf parks it and walks on; it stops at
@@ -590,41 +592,32 @@ constexpr int SPEC_LEAF_ROUND = CPT_SPEC_LEAF_ROUND;
 // tests, whose box passes the conservative test, is tested here too, under a limit that is
 // never below the final tmax; the rank rule and the certificate are unchanged.
 // ======================================================================================
-constexpr int WIDE_LANES = 256;   // block size of the kernels that walk the octant copies in HBM
+constexpr int WIDE_LANES = 256;   // block size of the kernels without the LDS image
 
 typedef __attribute__((address_space(3))) int16_t lds_i16;
 
-// LDS image of the wide tree (k_megakernel<..., LDST>): up to this many nodes of 7 x 16 B.
+// The compact image's first LDS_TREE_NODES nodes are staged in LDS (k_megakernel<..., LDST>,
+// k_wf_extend<..., LDST>); a larger tree's remaining nodes are read from the image in global
+// memory (L2-resident).  The host numbers the wide nodes largest box first, parents before
+// children (cpt_capi.cpp linearise_wide), so the LDS part is the top of the tree, the part
+// every ray walks.
 constexpr int LDS_TREE_NODES = 512;
+__host__ __device__ __forceinline__ int lds_tree_nodes(int n_wide) { return n_wide < LDS_TREE_NODES ? n_wide : LDS_TREE_NODES; }
 
 struct WideNode {
     f2v e[3][2], x[3][2];   // entry / exit planes per axis, children (0,1) and (2,3)
     int ref[4];
 };
 
-__device__ __forceinline__ WideNode load_wide(__amdgpu_buffer_rsrc_t rsrc, uint32_t off) {
+// A node of the compact image for a ray whose direction signs are (sx, sy, sz): the entry
+// planes of an axis are the slots' max planes when the ray runs toward -axis, else the min
+// planes, i.e. the planes the ray enters through; quad(k) reads the node's k-th 16 B.
+template <typename QUAD>
+__device__ __forceinline__ WideNode wide_node(const QUAD& quad, int sx, int sy, int sz) {
     WideNode n;
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-        const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16 * q, 0, 0);
-        f2v lo = {__uint_as_float(v.x), __uint_as_float(v.y)}, hi = {__uint_as_float(v.z), __uint_as_float(v.w)};
-        if (q < 3) { n.e[q][0] = lo; n.e[q][1] = hi; }
-        else { n.x[q - 3][0] = lo; n.x[q - 3][1] = hi; }
-    }
-    const v4u32 r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 96, 0, 0);
-    n.ref[0] = (int)r.x; n.ref[1] = (int)r.y; n.ref[2] = (int)r.z; n.ref[3] = (int)r.w;
-    return n;
-}
-
-// A node of the LDS image for a ray whose direction signs are (sx, sy, sz): the entry planes
-// of an axis are the slots' max planes when the ray runs toward -axis, else the min planes
-// (exactly the octant copy's choice), so the slab decisions are those of load_wide on the
-// ray's octant copy.
-__device__ __forceinline__ WideNode load_wide_lds(const uint4* tree, int cur, int sx, int sy, int sz) {
-    const uint4* q = tree + cur * 7;
-    WideNode n;
-    const uint4 ex = q[sx], xx = q[1 - sx], ey = q[2 + sy], xy = q[3 - sy], ez = q[4 + sz], xz = q[5 - sz];
-    const uint4 r = q[6];
+    const uint4 ex = quad(sx), xx = quad(1 - sx), ey = quad(2 + sy), xy = quad(3 - sy), ez = quad(4 + sz),
+                xz = quad(5 - sz);
+    const uint4 r = quad(6);
     auto lo = [](uint4 v) { return f2v{__uint_as_float(v.x), __uint_as_float(v.y)}; };
     auto hi = [](uint4 v) { return f2v{__uint_as_float(v.z), __uint_as_float(v.w)}; };
     n.e[0][0] = lo(ex); n.e[0][1] = hi(ex); n.x[0][0] = lo(xx); n.x[0][1] = hi(xx);
@@ -633,6 +626,24 @@ __device__ __forceinline__ WideNode load_wide_lds(const uint4* tree, int cur, in
     n.ref[0] = (int)(int16_t)(r.x & 0xffffu); n.ref[1] = (int)(int16_t)(r.x >> 16);
     n.ref[2] = (int)(int16_t)(r.y & 0xffffu); n.ref[3] = (int)(int16_t)(r.y >> 16);
     return n;
+}
+
+// Node `cur` from the LDS image (cur < n_lds: ds_read_b128) or from the image in global memory
+// (buffer loads at per-lane offsets).  Both hold the same bits, so the walk's decisions do not
+// depend on where a node was read.
+__device__ __forceinline__ WideNode load_wide_node(const uint4* tree, int n_lds, __amdgpu_buffer_rsrc_t rsrc,
+                                                   uint32_t image_off, int cur, int sx, int sy, int sz) {
+    if (__builtin_expect(cur < n_lds, 1)) {
+        const uint4* q = tree + cur * 7;
+        return wide_node([&](int k) { return q[k]; }, sx, sy, sz);
+    }
+    const uint32_t off = image_off + (uint32_t)cur * 112u;
+    return wide_node(
+        [&](int k) {
+            const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16u * (uint32_t)k, 0, 0);
+            return make_uint4(v.x, v.y, v.z, v.w);
+        },
+        sx, sy, sz);
 }
 
 // Hit mask of children (a, b) of a pair: slab_reject_octant for each, in scalar f32 ops (the
@@ -659,13 +670,9 @@ __device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], co
     return (rej0 ? 0u : 1u) | (rej1 ? 0u : 2u);
 }
 
-// Child refs (node words 24..27, cpt_capi.cpp linearise_wide): >= 0 a wide node of the same
-// octant, -1 none, <= -2 a leaf: on an octant copy ~k with k its position in the octant-0
-// binary order (absolute Node index n_nodes + k), on the LDS image ~(i + 1) with i its index in
-// the leaf array.  The host keeps the ranges within 15 bits, so the LDS stack holds 16-bit
-// entries (BLK lanes x CPT_WSTACK x 2 B per block).
-// LDST: the nodes come from the block's LDS image `tree` (k_megakernel stages it), else from
-// the ray's octant copy in HBM through `rsrc`.
+// Child refs (the image's int16 words, cpt_capi.cpp linearise_wide): >= 0 a wide node, -1 none,
+// <= -2 leaf i of the leaf array as ~(i + 1).  The host keeps the ranges within 15 bits, so the
+// LDS stack holds 16-bit entries (BLK lanes x CPT_WSTACK x 2 B per block).
 // A lane's wide walk in progress, kept across rounds of the megakernel when the walk is
 // suspended (trace_wide's `suspend_at`): the stack itself stays in LDS.
 struct WalkState {
@@ -688,7 +695,8 @@ struct WalkState {
 #endif
 constexpr int SUSPEND_MIN_DONE = CPT_SUSPEND_MIN_DONE;
 
-template <bool STATS, int BLK = WIDE_LANES, bool LDST = false>
+// `tree` is the block's LDS copy of the image's first lds_tree_nodes(n_wide) nodes.
+template <bool STATS, int BLK>
 __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc_t rsrc, int oct, const RayK& ray,
                                           Hit& h, int& code_out, Counters& cnt, const uint4* tree, WalkState& ws,
                                           int suspend_at) {
@@ -696,16 +704,15 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     // an LDS-typed pointer: 32-bit ds_read/ds_write addressing (a generic pointer costs a
     // 64-bit multiply-add per push and pop)
     lds_i16* const stk = (lds_i16*)wstack + threadIdx.x;
-    // Leaves: on the octant copies by absolute Node index (the platforms at n_nodes + k); on the
-    // LDS image by index into the wide tree's leaf array (platforms first, 32 B each, contiguous
-    // in HBM; staging it in LDS as well needs the pending sky fetches' LDS and measured 1.5%
-    // slower than keeping those).
-    const int leaf0 = LDST ? 0 : p.n_nodes;
-    // the leaf a ref <= -2 names: Node n_nodes + ~ref on the octant copies, leaf ~ref - 1 of
-    // the leaf array on the LDS image
-    auto leaf_of = [&](int ref) { return LDST ? ~ref - 1 : p.n_nodes + ~ref; };
-    const BufSrc leaf_src{rsrc, LDST ? (uint32_t)wide_leaves_base(p) * (uint32_t)sizeof(Node) : 0u};
+    // Leaves by index into the wide tree's leaf array (platforms first, 32 B each, contiguous in
+    // HBM; staging it in LDS as well needs the pending sky fetches' LDS and measured 1.5% slower
+    // than keeping those).
+    constexpr int leaf0 = 0;
+    auto leaf_of = [&](int ref) { return ~ref - 1; };
+    const BufSrc leaf_src{rsrc, (uint32_t)wide_leaves_base(p) * (uint32_t)sizeof(Node)};
     auto leaf = [&](int i) -> Node { return leaf_src(i); };
+    const int n_lds = lds_tree_nodes(p.n_wide);
+    const uint32_t image_off = (uint32_t)wide_image_base(p) * (uint32_t)sizeof(Node);
     constexpr int NONE = -1;
     const uint64_t participants = __ballot(1);
     stamps::lap(6);
@@ -728,7 +735,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         ws.limit = walk_limit(ws.tmax);   // changes only in leaf rounds
         ws.top = stk;
         ws.cur = 0;        // the root
-        ws.parked = -1;    // absolute Node index of the parked leaf
+        ws.parked = -1;    // leaf-array index of the parked leaf
     }
     stamps::lap(7);
     // the walk runs on the lane's WalkState itself (one copy of it lives across the round)
@@ -740,7 +747,6 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     lds_i16*& top = ws.top;   // the next free stack entry (entries are BLK apart)
     int& cur = ws.cur;
     int& parked = ws.parked;
-    const uint32_t wbase = (uint32_t)(p.n_nodes + 8 * p.n_walk + 4 * oct * p.n_wide) * (uint32_t)sizeof(Node);
     const int sx = oct & 1, sy = (oct >> 1) & 1, sz = oct >> 2;
     auto pop = [&]() -> int {
         if (top == stk) return NONE;
@@ -755,22 +761,23 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
             cur = pop();
         }
         if (cur >= 0) {
-            if (STATS) cnt.nodes++;
-            const WideNode n = LDST ? load_wide_lds(tree, cur, sx, sy, sz) : load_wide(rsrc, wbase + (uint32_t)cur * 128u);
+            if (STATS) {
+                cnt.nodes++;
+                cnt.gnodes += cur >= n_lds ? 1u : 0u;
+            }
+            const WideNode n = load_wide_node(tree, n_lds, rsrc, image_off, cur, sx, sy, sz);
             const f2v e01[3] = {n.e[0][0], n.e[1][0], n.e[2][0]}, x01[3] = {n.x[0][0], n.x[1][0], n.x[2][0]};
             const f2v e23[3] = {n.e[0][1], n.e[1][1], n.e[2][1]}, x23[3] = {n.x[0][1], n.x[1][1], n.x[2][1]};
             float lo[4];
             const uint32_t m = wide_pair(e01, x01, ray, limit, lo[0], lo[1]) |
                                (wide_pair(e23, x23, ray, limit, lo[2], lo[3]) << 2);
-            // The hit child walked next: on the LDS image the one with the nearest entry
-            // distance (first slot on ties), on an octant copy the first in its near-first
-            // slot order.  The other hits are pushed (slot 3 first) without branches: every
-            // slot is written at the top, and the top moves past it only when it is pushed
-            // (the host bounds the depth, so a write at an unmoved top stays inside the
-            // lane's stack).
-            int bk;
-            if (LDST) {
-                bk = 0;
+            // The hit child walked next is the one with the nearest entry distance (first slot
+            // on ties).  The other hits are pushed (slot 3 first) without branches: every slot
+            // is written at the top, and the top moves past it only when it is pushed (the
+            // host bounds the depth, so a write at an unmoved top stays inside the lane's
+            // stack).
+            int bk = 0;
+            {
                 float bd = (m & 1u) ? lo[0] : __builtin_inff();
 #pragma unroll
                 for (int k = 1; k < 4; ++k) {
@@ -780,8 +787,6 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
                     bk = closer ? k : bk;
                 }
                 if (bd == __builtin_inff()) bk = __builtin_ctz(m | 16u);   // no finite distance
-            } else {
-                bk = __builtin_ctz(m | 16u);
             }
 #pragma unroll
             for (int k = 3; k >= 0; --k) {
@@ -832,8 +837,8 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
 
 // TraceRay for one segment: the reference order, or the ordered walk with its certificate
 // and the reference-order fallback (CPT_TRAVERSAL_ORDERED): the 4-wide walk with parked
-// leaves (ordered == 1 and a wide tree), else the binary octant orders testing each leaf
-// where the walk meets it.
+// leaves (ordered == 1, a wide tree, and a kernel that staged its image in LDS: LDST), else
+// the binary octant orders testing each leaf where the walk meets it.
 // Returns 1 hit, 0 miss, or 2 when the walk was suspended (only with suspend_at > 0; the
 // lane calls again in a later round with the same ray and `ws`).
 template <bool STATS, int BLK = WIDE_LANES, bool LDST = false>
@@ -841,11 +846,16 @@ __device__ __forceinline__ int trace_segment(const KParams& p, const RayK& rk, b
                                              Counters& cnt, const uint4* tree, WalkState& ws, int suspend_at) {
     const __amdgpu_buffer_rsrc_t rsrc = node_rsrc(p);
     if (p.ordered && __builtin_expect(finite, 1)) {
-        int n, r;
-        if (p.ordered == 1 && p.n_wide > 0) {
-            const int oct = (rk.d.x < 0.f ? 1 : 0) | (rk.d.y < 0.f ? 2 : 0) | (rk.d.z < 0.f ? 4 : 0);
-            r = trace_wide<STATS, BLK, LDST>(p, rsrc, oct, rk, h, code, cnt, tree, ws, suspend_at);
-        } else {
+        int n, r = -1;
+        bool wide = false;
+        if constexpr (LDST) {
+            if (p.ordered == 1 && p.n_wide > 0) {
+                const int oct = (rk.d.x < 0.f ? 1 : 0) | (rk.d.y < 0.f ? 2 : 0) | (rk.d.z < 0.f ? 4 : 0);
+                r = trace_wide<STATS, BLK>(p, rsrc, oct, rk, h, code, cnt, tree, ws, suspend_at);
+                wide = true;
+            }
+        }
+        if (!wide) {
             const BufSrc order{rsrc, walk_order(p, rk.d, n) * (uint32_t)sizeof(Node)};
             r = trace<STATS, true, true>(order, n, rk, h, code, cnt);
         }

@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(256) k_wf_raygen(const KParams p, WfState w) {
 }
 
 // LDST: the megakernel's wide walk on the workgroup's LDS image of the tree (1024-lane blocks,
-// one per CU; the image is staged only by blocks that have rays), else the octant copies in HBM.
+// one per CU; the image is staged only by blocks that have rays), else the binary walks.
 constexpr int WF_LDS_BLOCK = 1024;
 template <bool LDST> constexpr int wf_extend_block() { return LDST ? WF_LDS_BLOCK : 256; }
 
@@ -120,8 +120,8 @@ __global__ void __launch_bounds__(wf_extend_block<LDST>()) k_wf_extend(const KPa
     __shared__ uint4 s_tree[LDST ? LDS_TREE_NODES * 7 : 1];
     if (LDST) {
         if ((uint32_t)blockIdx.x * BLK >= n) return;   // no ray for this block in this bounce
-        const uint4* src = reinterpret_cast<const uint4*>(p.nodes + p.n_nodes + 8 * p.n_walk + 32 * p.n_wide);
-        for (int i = threadIdx.x; i < 7 * p.n_wide; i += BLK) s_tree[i] = src[i];
+        const uint4* src = reinterpret_cast<const uint4*>(p.nodes + wide_image_base(p));
+        for (int i = threadIdx.x; i < 7 * lds_tree_nodes(p.n_wide); i += BLK) s_tree[i] = src[i];
         __syncthreads();
     }
     Counters cnt{};
@@ -154,6 +154,8 @@ __global__ void __launch_bounds__(wf_extend_block<LDST>()) k_wf_extend(const KPa
         }
         const uint64_t f = wave_sum(cnt.fallbacks);   // ordered walk: certificate fallbacks
         if ((threadIdx.x & 63) == 0 && f) atomicAdd((unsigned long long*)&p.stats[5], (unsigned long long)f);
+        const uint64_t g = wave_sum(cnt.gnodes);      // wide nodes read from global memory
+        if ((threadIdx.x & 63) == 0 && g) atomicAdd((unsigned long long*)&p.stats[6], (unsigned long long)g);
     }
 }
 
@@ -359,8 +361,9 @@ static hipError_t wf_render_any(const KParams& p, WfState& w, bool stats, bool a
 
 hipError_t launch_wavefront(const KParams& p, WfState& w, bool stats, bool aux, hipStream_t stream, int* launches) {
     if (p.width <= 0 || p.n_rows <= 0) return hipSuccess;
-    // the wide walk's LDS image when it fits (as in the megakernel, cpt_kernels.hip use_lds_tree)
-    const bool lds = p.ordered == 1 && p.n_wide > 0 && p.n_wide <= LDS_TREE_NODES;
+    // the wide walk runs on the LDS image (+ global memory past LDS_TREE_NODES), as in the
+    // megakernel (cpt_kernels.hip use_lds_tree)
+    const bool lds = p.ordered == 1 && p.n_wide > 0;
     return lds ? wf_render_any<true>(p, w, stats, aux, stream, launches)
                : wf_render_any<false>(p, w, stats, aux, stream, launches);
 }

@@ -29,6 +29,10 @@ class TileGather:
         """The full (height, width, 4) fp32 framebuffer (rgb sums + pass count) after this
         rank's render: device copy of the local tile, all-gather, row stitch."""
         renderer.copy_accum_device(self.send.data_ptr(), self.rows.size * self.width * 16)
+        # the copy runs on the context's stream: wait for it before torch's stream reads `send`
+        # (a no-op wait when the context launches on torch's stream, as bench.py sets up), and
+        # surface any device error of the render
+        renderer.synchronize()
         if self.world == 1:
             return self.send.view(self.max_rows, self.width, 4)[: self.height]
         if self.backend == "nccl":

@@ -197,6 +197,10 @@ class Renderer:
     def copy_accum_device(self, device_ptr, nbytes):
         self._check(self._L.cpt_copy_accum_device(self._ctx, ctypes.c_void_p(device_ptr), nbytes))
 
+    def gather_rows(self, src):
+        """cpt_gather_rows: place the rows Renderer `src` rendered into this frame (row tiling)."""
+        self._check(self._L.cpt_gather_rows(self._ctx, src._ctx))
+
     def stats(self):
         s = (ctypes.c_uint64 * 5)()
         self._check(self._L.cpt_get_stats(self._ctx, s))
@@ -224,6 +228,10 @@ class Renderer:
         out = ctypes.c_float(0.0)
         self._check(self._L.cpt_measure_read_bandwidth(self._ctx, int(nbytes), int(iters), ctypes.byref(out)))
         return float(out.value)
+
+    def set_debug_consolidation(self, flags=0, keeper_spin_log2=0, publish_wait_log2=0):
+        """TEST HOOK (cpt_set_debug_consolidation): provoke the tail consolidation's error paths."""
+        self._check(self._L.cpt_set_debug_consolidation(self._ctx, flags, keeper_spin_log2, publish_wait_log2))
 
     def reset_stats(self):
         self._check(self._L.cpt_reset_stats(self._ctx))

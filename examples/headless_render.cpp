@@ -3,7 +3,12 @@
 //
 //   cpt_headless [--scene s3|s4|s1000] [--width W] [--height H] [--spp N] [--depth D] [--seed S]
 //                [--out radiance.bin] [--dispatch K --bgra frame.bin] [--pfm image.pfm]
-//                [--texture file.ppm|file.cptex] [--dump-scene objects.bin]
+//                [--texture file.ppm|file.cptex] [--dump-scene objects.bin] [--devices N]
+//                [--objects N]
+//
+// --devices N row-tiles the image over N contexts (PathTracer::SetDevices: device i % visible
+// devices, so N > the GPU count puts several tiles on one GPU) and gathers each pass's tiles
+// into one frame; the image is the single-device image, bit for bit.
 //
 // --dump-scene writes the objects as SceneBVH::BuildBVH copied them (cpt_object records, the
 // C-ABI layout) and exits without rendering (no GPU needed).
@@ -129,7 +134,7 @@ void on_frame(uint8_t* data, int width, int height, void* param) {
 
 int main(int argc, char** argv) {
     std::string scene = "s4", out, bgra_out, pfm, texture, dump_scene;
-    int W = 64, H = 36, spp = 2, depth = 8, dispatch = 0;
+    int W = 64, H = 36, spp = 2, depth = 8, dispatch = 0, devices = 1, n_objects = 1000;
     unsigned long long seed = 1234;
     for (int i = 1; i + 1 < argc; i += 2) {
         std::string k = argv[i], v = argv[i + 1];
@@ -145,6 +150,8 @@ int main(int argc, char** argv) {
         else if (k == "--pfm") pfm = v;
         else if (k == "--texture") texture = v;
         else if (k == "--dump-scene") dump_scene = v;
+        else if (k == "--devices") devices = std::stoi(v);
+        else if (k == "--objects") n_objects = std::stoi(v);
         else { fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
     }
 
@@ -153,11 +160,12 @@ int main(int argc, char** argv) {
         new MotionalCamera(W, H, make_float3(130.f, 103.f, 130.f), make_float3(0.f, 0.f, 0.f)));
     tracer.SetCamera(cam);
     tracer.SetSeed(seed);
+    if (devices > 1 && !tracer.SetDevices(devices)) { fprintf(stderr, "%s\n", tracer.LastError().c_str()); return 1; }
     if (!tracer.SetMaxRecursionDepth((uint)depth)) { fprintf(stderr, "%s\n", tracer.LastError().c_str()); return 1; }
 
     // The same scenes as cpppathtracer_amd/scenes.py (S3, S4, S1000).
     if (scene == "s1000") {
-        add_s1000(tracer);
+        add_s1000(tracer, 20250124u, n_objects);
     } else if (scene == "s3") {
         tracer.AddObject(make_sphere(make_material(MaterialType::Diffuse, make_float3(0.8f, 0.3f, 0.3f)), make_float3(-35.f, 15.f, 0.f), 15.f));
         tracer.AddObject(make_sphere(make_material(MaterialType::Diffuse, make_float3(0.3f, 0.8f, 0.3f)), make_float3(0.f, 15.f, 0.f), 15.f));
@@ -224,7 +232,8 @@ int main(int argc, char** argv) {
     if (!tracer.ReadRadiance(rgb)) { fprintf(stderr, "ReadRadiance: %s\n", tracer.LastError().c_str()); return 1; }
     double mean = 0;
     for (float v : rgb) mean += v;
-    printf("rendered %dx%d x %d spp (depth %d): mean radiance %.6f\n", W, H, spp, depth, mean / rgb.size());
+    printf("rendered %dx%d x %d spp (depth %d) on %d device context(s): mean radiance %.6f\n", W, H, spp, depth,
+           tracer.DeviceCount(), mean / rgb.size());
     if (!out.empty()) {
         std::ofstream f(out, std::ios::binary);
         f.write(reinterpret_cast<const char*>(rgb.data()), (std::streamsize)(rgb.size() * sizeof(float)));

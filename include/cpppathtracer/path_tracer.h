@@ -9,12 +9,14 @@
 //                                 then calls Callback(BGRA8, width, height, cbParam) (:256-306)
 //   SetCamera / GetCamera
 // Additions the headless configs need (the reference has no setters for these):
-//   SetMaxRecursionDepth, SetSeed, SetDevice, SetEnvTexture, Render(spp) (synchronous),
-//   ReadRadiance, ReadFrameBGRA, SaveRadiancePFM, GetStats, Stop.
+//   SetMaxRecursionDepth, SetSeed, SetDevice, SetDevices (row tiling over several GPUs),
+//   SetEnvTexture, Render(spp) (synchronous), ReadRadiance, ReadFrameBGRA, SaveRadiancePFM,
+//   GetStats, Stop.
 // Errors: the reference logs CUDA errors and continues; here every call that reaches the
 // GPU returns false on failure and LastError() holds the message (no exceptions).
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -47,6 +49,16 @@ public:
     bool SetMaxRecursionDepth(uint depth);      // 0..32; reference default 8 (path_tracer.h:43)
     void SetSeed(uint64_t seed);                // reference seeds with clock() (path_tracer.cu:107)
     bool SetDevice(int device);                 // before the first render
+    // Row tiling, before the first render: the image rows are dealt to n
+    // contexts in interleaved 8-row blocks, one context per device (device i % visible devices,
+    // or the listed devices; a device may repeat), each rendering its rows of every pass.  Each
+    // pass's tiles are gathered into one frame on the first device (peer copies + a stitch
+    // kernel, cpt_gather_rows), which ReadRadiance, ReadFrameBGRA and the DispatchRay display
+    // path read.  A pixel's stream depends only on (seed, x, y): the image is bit-identical to
+    // a single-device render.
+    bool SetDevices(int n);
+    bool SetDevices(const std::vector<int>& devices);
+    int DeviceCount() const { return (int)std::max<size_t>(1, device_list_.size()); }
     bool SetEnvTexture(PocaTexture tex);        // default: textures/sky (assets/sky.cptex)
     // BVH walk: true (default) = CPT_TRAVERSAL_ORDERED (same image, fewer node visits);
     // false = the reference's right-first DFS order (its node/prim counts in GetStats).
@@ -63,28 +75,37 @@ public:
     const std::string& LastError() const { return err_; }
 
 private:
+    // One libcpt context: the renderer of one row tile (or of the whole frame).
+    struct Tile {
+        cpt_ctx* ctx = nullptr;
+        int device = 0;
+        bool scene_synced = false;
+        uint64_t scene_build = 0;      // SceneBVH::BuildId() uploaded to the context
+        uint64_t scene_rev = 0;        // SceneBVH::Revision() the context is at
+        std::vector<uint64_t> updates_seen;     // per-object UpdateObject counts refit so far
+        std::vector<uint64_t> bound_textures;   // material texture handles bound on the context
+        bool env_uploaded = false;
+        bool rng_ready = false;
+    };
     bool EnsureContext();
     bool SyncScene();
-    bool BindTextures(const std::vector<cpt_object>& objs);
+    bool SyncTile(Tile& t);
+    bool BindTextures(Tile& t, const std::vector<cpt_object>& objs);
     bool EnsureFrame(const MotionalCamera& cam);
     bool RenderPass(MotionalCamera& cam, int spp, bool accumulate);
     void PipelineLoop();
-    bool Fail(const char* what);
+    bool Fail(const char* what, cpt_ctx* ctx = nullptr);
+    cpt_ctx* FrameCtx() const { return frame_ ? frame_ : (tiles_.empty() ? nullptr : tiles_[0].ctx); }
 
-    cpt_ctx* ctx_ = nullptr;
+    std::vector<Tile> tiles_;       // one per device of the row tiling (one: the whole frame)
+    cpt_ctx* frame_ = nullptr;      // row tiling: the gathered frame on the first device
     int device_ = 0;
+    std::vector<int> device_list_;  // SetDevices (empty: the single device_)
     uint64_t seed_ = 1234;
     uint max_recursion_depth_ = 8;
     bool ordered_walk_ = true;
     int width_ = 0, height_ = 0;
-    bool scene_synced_ = false;
-    uint64_t scene_build_ = 0;      // SceneBVH::BuildId() uploaded to the context
-    uint64_t scene_rev_ = 0;        // SceneBVH::Revision() the context is at
-    std::vector<uint64_t> updates_seen_;       // per-object UpdateObject counts refit so far
-    std::vector<uint64_t> bound_textures_;     // material texture handles bound on the context
-    bool rng_ready_ = false;
     PocaTexture env_ = 0;
-    bool env_uploaded_ = false;
     std::shared_ptr<MotionalCamera> camera_;
     std::vector<uint8_t> output_buffer_;   // BGRA8 handed to the callback
     std::string err_;

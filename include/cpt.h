@@ -54,7 +54,12 @@ enum cpt_status {
     CPT_ERR_HIP = 3,
     CPT_ERR_OUT_OF_MEMORY = 4,
     CPT_ERR_STATE = 5,       /* e.g. render before scene/frame/rng were set */
-    CPT_ERR_UNSUPPORTED = 6
+    CPT_ERR_UNSUPPORTED = 6,
+    /* A kernel had to abandon work (e.g. a tail-consolidation hand-over timed out, so some
+     * pixels were not finished); reported by the next synchronising call on the context
+     * (cpt_synchronize, cpt_read_accum, cpt_read_rng, cpt_render with CPT_RENDER_SYNC, ...),
+     * like the reference's logged CUDA errors (path_tracer.cu:279-283).  Sticky until read. */
+    CPT_ERR_DEVICE = 7
 };
 
 /* PrimitiveType::Enum (object.h:7-15) and MaterialType::Enum (material.h:5-15). */
@@ -155,8 +160,9 @@ typedef struct cpt_ctx cpt_ctx;
  * waves of a workgroup hand their chains over at pass boundaries so that each SIMD runs fewer,
  * fuller waves while chains finish.  Identical results.  By default it runs when spp >= 512 and
  * the frame holds at most 4 pixels per lane of the persistent grid (a strong-scaled row tile);
- * these flags force it on or off (on needs spp > 1).  Only the walk on the LDS tree image consolidates
- * (CPT_TRAVERSAL_ORDERED, trees of up to 512 4-wide nodes). */
+ * these flags force it on or off (on needs spp > 1).  Only the 4-wide walk consolidates
+ * (CPT_TRAVERSAL_ORDERED with a 4-wide walk tree, cpt_get_walk_info [2] > 0).  A hand-over that
+ * cannot complete ends the render with CPT_ERR_DEVICE, never with silently missing pixels. */
 #define CPT_SCHEDULE_CONSOLIDATE    0x1000u
 #define CPT_SCHEDULE_NO_CONSOLIDATE 0x2000u
 
@@ -234,19 +240,29 @@ int cpt_clear_accum(cpt_ctx* ctx);
 int cpt_read_aux(cpt_ctx* ctx, float* normal3, float* depth); /* either may be NULL */
 /* Device-to-device copy of the accumulator (e.g. into an RCCL send buffer). */
 int cpt_copy_accum_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
+/* Row-tile gather (multi-GPU row tiling; the single-GPU reference writes the
+ * whole frame from SamplePixel, path_tracer.cu:172-174): places the rows `src` rendered -- its
+ * accumulator, and its first-hit normals and depths when it rendered with CPT_RENDER_AUX --
+ * into `dst`'s frame at the same global rows (dst must hold every one of them, e.g. a full
+ * frame).  src and dst may live on different devices (peer copy over xGMI) or on the same one.
+ * Waits for src's work (and reports its device errors); dst then holds a stitched frame for
+ * cpt_read_accum, cpt_read_aux and cpt_denoise_mix. */
+int cpt_gather_rows(cpt_ctx* dst, cpt_ctx* src);
 int cpt_get_stats(cpt_ctx* ctx, cpt_stats* out);
 int cpt_reset_stats(cpt_ctx* ctx);
 /* All 8 raw device counters (0-4 = cpt_stats; 5 = ordered-walk segments that failed the
- * winner certificate and took the reference walk (CPT_RENDER_STATS | CPT_TRAVERSAL_ORDERED)). */
+ * winner certificate and took the reference walk (CPT_RENDER_STATS | CPT_TRAVERSAL_ORDERED);
+ * 6 = 4-wide node visits read from global memory, i.e. past the LDS image's first 512 nodes). */
 int cpt_get_raw_counters(cpt_ctx* ctx, uint64_t* out8);
 /* DIAGNOSTIC: the 16 wave-time stamp slots of a CPT_STAMPS build (cpt_stamps.hpp; all zero in
  * the shipped library), summed over the renders since the last cpt_reset_stats. */
 int cpt_get_diag_counters(cpt_ctx* ctx, uint64_t* out16);
 /* Node counts of the scene's walk structures (host-side, no GPU work): [0] the reference
  * order (bvh.cu's tree, 32-B nodes), [1] each octant order of the binary walk tree, [2] the
- * 4-wide walk tree's nodes per octant (128 B each; 0 = the ordered walk uses the binary
- * orders), [3] the unbounded (platform) leaves tested before the walk tree.  With [2] > 0,
- * the `nodes` counter of an ordered render counts 4-wide node visits. */
+ * 4-wide walk tree's nodes (112 B each in its compact image, the first 512 staged in LDS; 0 =
+ * the ordered walk uses the binary orders), [3] the unbounded (platform) leaves tested before
+ * the walk tree.  With [2] > 0, the `nodes` counter of an ordered render counts 4-wide node
+ * visits. */
 int cpt_get_walk_info(cpt_ctx* ctx, int32_t* out4);
 /* Device time of the last cpt_render (HIP events on the launch stream); waits for it. */
 int cpt_last_render_ms(cpt_ctx* ctx, float* ms);
@@ -289,6 +305,12 @@ int cpt_math_batch(cpt_ctx* ctx, int op, const float* a, const float* b, float* 
  * out[0] receives the mismatch count (0 expected), out[1..out_len) up to out_len-1 failing
  * pairs as (a bits << 32 | d bits). */
 int cpt_selftest_qdiv(cpt_ctx* ctx, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len);
+/* TEST HOOK for the tail consolidation's error paths (all zero = normal operation): flags bit 0
+ * starts every workgroup with a phantom live chain (a lost count: the keeper waves can never
+ * see the workgroup drained), bit 1 makes hand-overs never publish their slot; the keeper's
+ * idle-spin limit and the hand-over wait as log2 (0 = the defaults, 26 and 22).  A render that
+ * trips either limit must end with CPT_ERR_DEVICE. */
+int cpt_set_debug_consolidation(cpt_ctx* ctx, uint32_t flags, int keeper_spin_log2, int publish_wait_log2);
 
 #ifdef __cplusplus
 }  /* extern "C" */

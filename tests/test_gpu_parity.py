@@ -418,6 +418,26 @@ def test_wide_walk_structure_and_deep_tree_fallback(gpu, oracle_mod, sky):
         _check_stats(gs, os_, path)
 
 
+LDS_TREE_NODES = 512   # cpt_path.hpp: wide nodes staged in LDS; the rest are read from global memory
+
+
+@pytest.mark.parametrize("path", ["megakernel:ordered", "megakernel:ordered+timed", "megakernel:ordered+timed+cons",
+                                  "wavefront:ordered", "wavefront:ordered+timed"])
+def test_wide_walk_beyond_lds_image(gpu, oracle_mod, sky, path):
+    """A 4-wide tree larger than the LDS image (S1000's generator with 3000 primitives): the
+    walk reads the top LDS_TREE_NODES nodes from LDS and the others from the image in global
+    memory (cpt_path.hpp load_wide_node).  Images, RNG end states, segment/hit/miss counts and
+    certificate fallbacks equal the oracle's (bvh.cu:167-205 is the reference walk)."""
+    objs = scenes.scene_s1000(n=3000)
+    gpu.set_scene(objs)
+    info = gpu.walk_info()
+    assert info["n_wide"] > LDS_TREE_NODES, info
+    (ga, gr, gs, _), (oa, orng, os_, _) = _run_both(gpu, oracle_mod, sky, objs, 64, 36, 2, 16, path=path)
+    np.testing.assert_array_equal(gr, orng)
+    _check_stats(gs, os_, path)
+    np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
+
+
 def test_hbm_read_probe(gpu):
     """cpt_measure_read_bandwidth (the bench's measured roofline ceiling) returns a sane GB/s
     for a 1 GiB buffer: above 1 TB/s, below the 8 TB/s spec (with 5% slack for timer noise)."""
