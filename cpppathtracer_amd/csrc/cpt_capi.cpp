@@ -601,21 +601,41 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
     make(root, n_unb);   // the walk starts with the root and the platforms on the stack
     if (max_push + 1 > WIDE_STACK) return 0;
     const int n_wide = (int)wbin.size();
-    // Renumber the wide nodes largest box first, every node after its parent (a best-first
-    // expansion from the root by surface area, which a random ray hits in proportion to): the
-    // device stages the first LDS_TREE_NODES of them in LDS, so a larger tree keeps its top there.
-    {
-        std::vector<int> order;   // new id -> old id
-        order.reserve(n_wide);
+    // The leaf array after the compact image: the platforms (the head of every octant order),
+    // then the walk tree's leaves in the order the wide nodes, in preorder, first reference
+    // them (a subtree's leaves share cache lines); Node copies of octant 0's inline leaves.
+    // The compact image refers to leaf i as ~(i + 1) (<= -2, apart from the empty slot's -1).
+    std::vector<int> li_of(w.nodes.size(), -1), leaf_pos;
+    for (int k = 0; k < n_unb; ++k) leaf_pos.push_back(k);
+    for (int id = 0; id < n_wide; ++id)
+        for (int x : kids[id])
+            if (w.nodes[x].is_object && li_of[x] < 0) {
+                li_of[x] = (int)leaf_pos.size();
+                leaf_pos.push_back(pos0[x]);
+            }
+    if ((int)leaf_pos.size() > 32765) return 0;
+    // The ids are preorder (make's recursion order), which keeps a subtree's nodes and leaves
+    // together in memory.  A tree larger than the LDS image is renumbered so that its first
+    // LDS_TREE_NODES ids -- the part the device stages in LDS -- are its top: the nodes a
+    // best-first expansion from the root by surface area (which a random ray hits in
+    // proportion to) reaches first, each after its parent; those first, then the rest, each
+    // part in preorder.
+    if (n_wide > cpt::LDS_TREE_NODES) {
+        std::vector<char> top(n_wide, 0);
         std::priority_queue<std::pair<float, int>, std::vector<std::pair<float, int>>, std::greater<>> pq;
         pq.emplace(-area(wbin[0]), 0);
-        while (!pq.empty()) {
+        for (int taken = 0; !pq.empty() && taken < cpt::LDS_TREE_NODES; ++taken) {
             const int id = pq.top().second;
             pq.pop();
-            order.push_back(id);
+            top[id] = 1;
             for (int x : kids[id])
                 if (!w.nodes[x].is_object) pq.emplace(-area(x), wide_of[x]);
         }
+        std::vector<int> order;   // new id -> old id: the top in preorder, then the rest
+        order.reserve(n_wide);
+        for (int part = 1; part >= 0; --part)
+            for (int id = 0; id < n_wide; ++id)
+                if (top[id] == part) order.push_back(id);
         std::vector<int> new_id(n_wide);
         for (int k = 0; k < n_wide; ++k) new_id[order[k]] = k;
         std::vector<int> wbin2(n_wide);
@@ -633,19 +653,6 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
     if (n_wide > 32767) return 0;
     for (int p : pos0)
         if (p > 32766) return 0;
-    // The leaf array after the compact image (staged in LDS with it when it fits): the
-    // platforms (the head of every octant order), then the walk tree's leaves in the order the
-    // wide nodes first reference them; Node copies of octant 0's inline leaves.  The compact
-    // image refers to leaf i as ~(i + 1) (<= -2, apart from the empty slot's -1).
-    std::vector<int> li_of(w.nodes.size(), -1), leaf_pos;
-    for (int k = 0; k < n_unb; ++k) leaf_pos.push_back(k);
-    for (int id = 0; id < n_wide; ++id)
-        for (int x : kids[id])
-            if (w.nodes[x].is_object && li_of[x] < 0) {
-                li_of[x] = (int)leaf_pos.size();
-                leaf_pos.push_back(pos0[x]);
-            }
-    if ((int)leaf_pos.size() > 32765) return 0;
     const size_t base = out.size();
     const size_t n_compact = (size_t)(n_wide * 7 + 1) / 2;
     out.resize(base + n_compact + leaf_pos.size());

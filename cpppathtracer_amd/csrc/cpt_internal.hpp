@@ -12,6 +12,11 @@
 
 namespace cpt {
 
+// Wide-tree nodes staged in LDS by the LDS kernels (cpt_path.hpp trace_wide); the host numbers
+// a larger tree so that these are its top (cpt_capi.cpp linearise_wide).
+constexpr int LDS_TREE_NODES = 512;
+__host__ __device__ __forceinline__ int lds_tree_nodes(int n_wide) { return n_wide < LDS_TREE_NODES ? n_wide : LDS_TREE_NODES; }
+
 // Camera snapshot as the kernel needs it (the reference passes the whole MotionalCamera by
 // value in PathTracerParams, path_tracer.cu:14-27; only these fields are read by RayGen).
 struct CamK {
@@ -29,8 +34,8 @@ struct KParams {
                             // the walk tree's eight octant orders (n_walk each)
     const Mat* mats;        // deduplicated materials, indexed by Node::code >> 2
     int n_nodes, n_walk;
-    int n_wide;             // 4-wide walk-tree nodes per octant, after the eight octant orders
-                            // (0: the ordered walk uses the binary octant orders)
+    int n_wide;             // 4-wide walk-tree nodes: their compact image follows the eight octant
+                            // orders (0: the ordered walk uses the binary octant orders)
     int n_unb;              // unbounded leaves at the head of every octant order
     int n_leaves;           // the wide tree's leaf array (platforms first), after its compact image
     int ordered;            // CPT_TRAVERSAL_ORDERED: walk the ray's octant order (2: plain leaves)

@@ -118,7 +118,9 @@ constexpr int DEFER_MISS_ROUND = CPT_DEFER_MISS_ROUND;
 template <bool LDST> constexpr int mk_block() { return LDST ? CPT_LDS_BLOCK : 256; }
 template <bool LDST> constexpr int mk_waves() { return LDST ? CPT_LDS_BLOCK / 256 : CPT_WAVES_PER_SIMD; }
 
-template <bool STATS, bool AUX, bool PROBE, bool LDST, bool CONS>
+// HYB (LDST): the wide tree has more nodes than the LDS image holds; the rest are read from
+// global memory (cpt_path.hpp load_wide_node).
+template <bool STATS, bool AUX, bool PROBE, bool LDST, bool CONS, bool HYB>
 __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakernel(const KParams p) {
     constexpr bool COUNT = STATS || PROBE;
     constexpr int BLK = mk_block<LDST>();
@@ -344,7 +346,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             const RayK rk = make_rayk(ray);
             const bool finite_ray = !(ray.o.x != ray.o.x || ray.o.y != ray.o.y || ray.o.z != ray.o.z ||
                                       ray.d.x != ray.d.x || ray.d.y != ray.d.y || ray.d.z != ray.d.z);
-            tr = trace_segment<COUNT, BLK, LDST>(p, rk, finite_ray, h, code, cnt, s_tree, ws, LDST ? SUSPEND_AT : 0);
+            tr = trace_segment<COUNT, BLK, LDST, HYB>(p, rk, finite_ray, h, code, cnt, s_tree, ws, LDST ? SUSPEND_AT : 0);
         }
         stamps::lap(3);
         if (busy && L.left > 0 && tr != 2) {
@@ -799,7 +801,7 @@ __global__ void k_math_batch(int op, const float* a, const float* b, float* out,
 // ======================================================================================
 // Host-side launchers (called from cpt_capi.cpp).
 // ======================================================================================
-template <bool S, bool A, bool P, bool T, bool C = false>
+template <bool S, bool A, bool P, bool T, bool C = false, bool H = false>
 static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
     static int blocks_per_cu = -1, cus = 0;
     constexpr int block = mk_block<T>();
@@ -808,7 +810,7 @@ static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
         hipError_t e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_megakernel<S, A, P, T, C>, block, 0);
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, k_megakernel<S, A, P, T, C, H>, block, 0);
         if (e != hipSuccess) return e;
         if (blocks_per_cu < 1) blocks_per_cu = 1;
     }
@@ -817,7 +819,7 @@ static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
     long long want = (tiles * 64 * ((64 + p.lanes - 1) / p.lanes) + block - 1) / block;
     long long grid = std::min<long long>(want, (long long)blocks_per_cu * cus);
     if (grid < 1) return hipSuccess;
-    hipLaunchKernelGGL((k_megakernel<S, A, P, T, C>), dim3((unsigned)grid), dim3(block), 0, stream, p);
+    hipLaunchKernelGGL((k_megakernel<S, A, P, T, C, H>), dim3((unsigned)grid), dim3(block), 0, stream, p);
     return hipGetLastError();
 }
 
@@ -825,13 +827,19 @@ static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
 // LDS_TREE_NODES nodes in LDS, the rest of a larger tree from global memory.
 static bool use_lds_tree(const KParams& p) { return p.ordered == 1 && p.n_wide > 0; }
 
+template <bool S, bool A, bool P, bool H>
+static hipError_t launch_mk_lds(const KParams& p, hipStream_t stream) {
+    if constexpr (!P && ho_slots<mk_block<true>()>() > 0) {
+        if (p.resume) return launch_mk<S, A, P, true, true, H>(p, stream);   // tail consolidation
+    }
+    return launch_mk<S, A, P, true, false, H>(p, stream);
+}
+
 template <bool S, bool A, bool P>
 static hipError_t launch_mk_any(const KParams& p, hipStream_t stream) {
     if (!use_lds_tree(p)) return launch_mk<S, A, P, false>(p, stream);
-    if constexpr (!P && ho_slots<mk_block<true>()>() > 0) {
-        if (p.resume) return launch_mk<S, A, P, true, true>(p, stream);   // tail consolidation
-    }
-    return launch_mk<S, A, P, true>(p, stream);
+    if (p.n_wide > LDS_TREE_NODES) return launch_mk_lds<S, A, P, true>(p, stream);
+    return launch_mk_lds<S, A, P, false>(p, stream);
 }
 
 hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t stream) {

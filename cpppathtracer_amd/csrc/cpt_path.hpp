@@ -601,8 +601,7 @@ typedef __attribute__((address_space(3))) int16_t lds_i16;
 // memory (L2-resident).  The host numbers the wide nodes largest box first, parents before
 // children (cpt_capi.cpp linearise_wide), so the LDS part is the top of the tree, the part
 // every ray walks.
-constexpr int LDS_TREE_NODES = 512;
-__host__ __device__ __forceinline__ int lds_tree_nodes(int n_wide) { return n_wide < LDS_TREE_NODES ? n_wide : LDS_TREE_NODES; }
+// (LDS_TREE_NODES, lds_tree_nodes: cpt_internal.hpp)
 
 struct WideNode {
     f2v e[3][2], x[3][2];   // entry / exit planes per axis, children (0,1) and (2,3)
@@ -630,10 +629,11 @@ __device__ __forceinline__ WideNode wide_node(const QUAD& quad, int sx, int sy, 
 
 // Node `cur` from the LDS image (cur < n_lds: ds_read_b128) or from the image in global memory
 // (buffer loads at per-lane offsets).  Both hold the same bits, so the walk's decisions do not
-// depend on where a node was read.
+// depend on where a node was read.  HYB = false: the whole tree is in LDS (no per-node check).
+template <bool HYB>
 __device__ __forceinline__ WideNode load_wide_node(const uint4* tree, int n_lds, __amdgpu_buffer_rsrc_t rsrc,
                                                    uint32_t image_off, int cur, int sx, int sy, int sz) {
-    if (__builtin_expect(cur < n_lds, 1)) {
+    if (!HYB || __builtin_expect(cur < n_lds, 1)) {
         const uint4* q = tree + cur * 7;
         return wide_node([&](int k) { return q[k]; }, sx, sy, sz);
     }
@@ -695,8 +695,9 @@ struct WalkState {
 #endif
 constexpr int SUSPEND_MIN_DONE = CPT_SUSPEND_MIN_DONE;
 
-// `tree` is the block's LDS copy of the image's first lds_tree_nodes(n_wide) nodes.
-template <bool STATS, int BLK>
+// `tree` is the block's LDS copy of the image's first lds_tree_nodes(n_wide) nodes; HYB: the
+// tree is larger (n_wide > LDS_TREE_NODES), so some nodes come from global memory.
+template <bool STATS, int BLK, bool HYB>
 __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc_t rsrc, int oct, const RayK& ray,
                                           Hit& h, int& code_out, Counters& cnt, const uint4* tree, WalkState& ws,
                                           int suspend_at) {
@@ -763,9 +764,9 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         if (cur >= 0) {
             if (STATS) {
                 cnt.nodes++;
-                cnt.gnodes += cur >= n_lds ? 1u : 0u;
+                cnt.gnodes += HYB && cur >= n_lds ? 1u : 0u;
             }
-            const WideNode n = load_wide_node(tree, n_lds, rsrc, image_off, cur, sx, sy, sz);
+            const WideNode n = load_wide_node<HYB>(tree, n_lds, rsrc, image_off, cur, sx, sy, sz);
             const f2v e01[3] = {n.e[0][0], n.e[1][0], n.e[2][0]}, x01[3] = {n.x[0][0], n.x[1][0], n.x[2][0]};
             const f2v e23[3] = {n.e[0][1], n.e[1][1], n.e[2][1]}, x23[3] = {n.x[0][1], n.x[1][1], n.x[2][1]};
             float lo[4];
@@ -841,7 +842,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
 // the binary octant orders testing each leaf where the walk meets it.
 // Returns 1 hit, 0 miss, or 2 when the walk was suspended (only with suspend_at > 0; the
 // lane calls again in a later round with the same ray and `ws`).
-template <bool STATS, int BLK = WIDE_LANES, bool LDST = false>
+template <bool STATS, int BLK = WIDE_LANES, bool LDST = false, bool HYB = true>
 __device__ __forceinline__ int trace_segment(const KParams& p, const RayK& rk, bool finite, Hit& h, int& code,
                                              Counters& cnt, const uint4* tree, WalkState& ws, int suspend_at) {
     const __amdgpu_buffer_rsrc_t rsrc = node_rsrc(p);
@@ -851,7 +852,7 @@ __device__ __forceinline__ int trace_segment(const KParams& p, const RayK& rk, b
         if constexpr (LDST) {
             if (p.ordered == 1 && p.n_wide > 0) {
                 const int oct = (rk.d.x < 0.f ? 1 : 0) | (rk.d.y < 0.f ? 2 : 0) | (rk.d.z < 0.f ? 4 : 0);
-                r = trace_wide<STATS, BLK>(p, rsrc, oct, rk, h, code, cnt, tree, ws, suspend_at);
+                r = trace_wide<STATS, BLK, HYB>(p, rsrc, oct, rk, h, code, cnt, tree, ws, suspend_at);
                 wide = true;
             }
         }
