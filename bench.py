@@ -12,9 +12,12 @@ Multi-GPU: one process per GPU.  Run under torchrun (WORLD_SIZE set; it must equ
 or give `--gpus N` without a launcher: the parent then starts N ranks through
 `torch.distributed.run` before it touches the GPU, relays rank 0's line and exits with the
 launcher's status.  The image rows are dealt to the ranks in interleaved 8-row blocks (row
-tiling).  Scaling: "strong" (default) renders the
-configuration's image (C4: 1920x1080) at every N; "weak" (opt-in) keeps the pixels per GPU
-fixed by scaling each axis by sqrt(N).
+tiling).  Scaling: "weak" (default; the path shards
+into independent row tiles) keeps the pixels per GPU fixed by scaling each axis by sqrt(N)
+(N = 4: 3840x2160, C5's frame); "strong" renders the configuration's image (C4: 1920x1080) at
+every N.  A weak-scaled run with N > 1 also times the configuration's own frame strong-scaled
+over the same ranks and reports it as `strong_scaling` (the north star's 1920x1080 at N GPUs;
+its ceiling is the longest pixel chain).
 
 Rank 0 prints one JSON line with `roofline` (SURVEY.md §8(d) algorithmic bytes ÷ the kernel's
 HIP-event time, beside the rocprof-measured HBM bytes and VALU issue of a committed profile of
@@ -60,8 +63,10 @@ def parse_args(argv=None):
     ap.add_argument("--schedule", default="cost", choices=["cost", "tiles"],
                     help="megakernel pixel dequeue order: 8x8 tiles heaviest first from a pilot pass "
                          "(CPT_SCHEDULE_COST), or tiles in row-major order")
-    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
-                    help="strong: the config's image at every N; weak: pixels per GPU fixed (image grows by sqrt(N))")
+    ap.add_argument("--scaling", default="weak", choices=["strong", "weak"],
+                    help="weak: pixels per GPU fixed (image grows by sqrt(N)); strong: the config's image at every N")
+    ap.add_argument("--no-strong-check", action="store_true",
+                    help="weak scaling, N > 1: skip the extra strong-scaled timing of the config's own frame")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hbm-probe", action="store_true", help="skip the streaming-read ceiling probe")
     ap.add_argument("--no-count", action="store_true",
@@ -217,6 +222,7 @@ def run(args):
     if args.height:
         cfg["height"] = args.height
     cfg["seed"] = args.seed
+    W0, H0 = cfg["width"], cfg["height"]   # the configuration's own frame (strong-scaling check)
     if args.scaling == "weak" and world > 1 and not (args.width or args.height):
         cfg["width"], cfg["height"] = tiling.weak_scaled_size(cfg["width"], cfg["height"], world)
     W, H, spp, depth = cfg["width"], cfg["height"], cfg["spp"], cfg["depth"]
@@ -346,6 +352,35 @@ def run(args):
         t = _all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, avg_kernel_ms_max = t.tolist()
 
+    # Weak scaling, N > 1: the configuration's own frame strong-scaled over the same ranks (each
+    # rank its interleaved 8-row blocks of W0 x H0), 1 untimed + 2 timed frames with the gather.
+    strong = None
+    if world > 1 and args.scaling == "weak" and not args.no_strong_check and (W0, H0) != (W, H):
+        rows0 = tiling.partition_rows(H0, world, rank)
+        cam0 = camera_get_copy(scenes.camera_for(W0, H0))
+        r.set_frame(W0, H0, rows0)
+        r.init_rng(cfg["seed"])
+        gather0 = multigpu.TileGather(W0, H0, world, rank, dev, backend)
+        n_strong = 2
+        for k in range(n_strong + 1):
+            if k == 1:
+                dist.barrier()
+                torch.cuda.synchronize()
+                ts = time.perf_counter()
+            r.render(cam0, spp, depth, path=args.path, ordered=ordered, schedule=schedule, consolidate=consolidate)
+            gather0(r)
+        torch.cuda.synchronize()
+        dist.barrier()
+        ts = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=dev)
+        ts = _all_reduce(ts, op=dist.ReduceOp.MAX).item()
+        strong = {
+            "workload": f"{args.config}: {cfg['scene']} {W0}x{H0} {spp}spp depth {depth}",
+            "n_gpus": world, "steps": n_strong, "ms_per_step": round(ts / n_strong * 1e3, 3),
+            "value": round(W0 * H0 * spp * n_strong / ts / 1e6, 3), "unit": "Mpaths/s",
+            "note": "the configuration's own frame row-tiled over the same ranks (strong scaling); its ceiling is "
+                    "the longest pixel chain (DESIGN.md §Multi-GPU)",
+        }
+
     if rank == 0:
         paths_total = W * H * spp
         value = paths_total * args.steps / elapsed / 1e6
@@ -377,6 +412,8 @@ def run(args):
             },
             "rng_init_ms": round(t_init * 1e3, 2),
         }
+        if strong:
+            out["strong_scaling"] = strong
         if st is not None:
             # Algorithmic bytes of one launch: SURVEY.md 8(d)'s per-unit model x the units the
             # launch processes (the executed walk's own counts; a 4-wide node visit = 112 B),

@@ -50,6 +50,7 @@ PROTOTYPES = {
     "cpt_measure_read_bandwidth": (_I, [_P, _SZ, _I, _P]),
     "cpt_last_render_ms": (_I, [_P, _P]),
     "cpt_get_diag_counters": (_I, [_P, _P]),
+    "cpt_get_execdiag_counters": (_I, [_P, _P]),
     "cpt_last_kernel_stats": (_I, [_P, _P, _P]),
     "cpt_denoise_mix": (_I, [_P, _U32, _P]),
     "cpt_denoise_mix_band": (_I, [_P, _U32, _I, _I, _P]),

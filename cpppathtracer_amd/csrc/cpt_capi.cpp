@@ -858,10 +858,10 @@ int cpt_create(int device, cpt_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&c->ev_start);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_stop);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_main);
-    if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 32 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 128 * sizeof(unsigned long long));   // [64..128) execdiag
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_work, 64);   // [0] dequeue counter, [4] error word
     if (e == hipSuccess) e = hipMemset(c->d_work, 0, 64);
-    if (e == hipSuccess) e = hipMemset(c->d_stats, 0, 32 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(c->d_stats, 0, 128 * sizeof(unsigned long long));
     if (e == hipSuccess) {
         const std::vector<uint32_t>& J = jump_tables();
         e = hipMalloc((void**)&c->d_jumps, J.size() * sizeof(uint32_t));
@@ -1216,7 +1216,9 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
 #ifdef CPT_DIAGNOSTIC_LANES
     // lane-latency experiments (tools/lane_latency.py builds with -DCPT_DIAGNOSTIC_LANES)
     if (const char* e = getenv("CPT_LANES_PER_WAVE")) p.lanes = std::max(1, std::min(64, atoi(e)));
+    if (const char* e = getenv("CPT_REPLICATE")) p.replicate = std::max(1, std::min(64, atoi(e)));
 #endif
+    if (p.replicate < 1) p.replicate = 1;
     p.error = c->d_work + 4;
     p.dbg = c->dbg;
     p.keeper_spin_log2 = c->keeper_spin_log2;
@@ -1426,6 +1428,14 @@ int cpt_get_diag_counters(cpt_ctx* c, uint64_t* out16) {
     return CPT_OK;
 }
 
+int cpt_get_execdiag_counters(cpt_ctx* c, uint64_t* out64) {
+    if (!c || !out64) return CPT_ERR_INVALID_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    HIP_TRY(c, hipMemcpy(out64, c->d_stats + 64, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return CPT_OK;
+}
+
 int cpt_get_walk_info(cpt_ctx* c, int32_t* out4) {
     if (!c || !out4) return CPT_ERR_INVALID_ARG;
     out4[0] = c->n_bvh;
@@ -1438,7 +1448,7 @@ int cpt_get_walk_info(cpt_ctx* c, int32_t* out4) {
 int cpt_reset_stats(cpt_ctx* c) {
     if (!c) return CPT_ERR_INVALID_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, 32 * sizeof(unsigned long long), c->stream()));
+    HIP_TRY(c, hipMemsetAsync(c->d_stats, 0, 128 * sizeof(unsigned long long), c->stream()));
     return CPT_OK;
 }
 

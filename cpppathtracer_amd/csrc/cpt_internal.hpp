@@ -54,6 +54,7 @@ struct KParams {
     uint32_t* tile_cost;    // pilot launch only: per-tile work (cost schedule)
     int spp, max_depth, accumulate;
     int lanes;              // lanes per wave that take pixels (64; fewer: DIAGNOSTIC CPT_LANES_PER_WAVE)
+    int replicate;          // lanes per taken pixel (1; more: DIAGNOSTIC CPT_REPLICATE, identical copies)
     // Tail consolidation (LDS walk only; nullptr: off): slabs of chains handed over at a pass
     // boundary by retiring waves, 5 x uint4 per chain, ho_slots chains per workgroup.
     uint4* resume;

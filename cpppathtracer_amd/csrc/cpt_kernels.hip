@@ -88,23 +88,7 @@ __device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int&
     return x < p.width && ri < p.n_rows;
 }
 
-// LDST: a round's walks are suspended once at most this many lanes of the wave still walk
-// (cpt_path.hpp trace_wide).
-#ifndef CPT_SUSPEND_AT
-#define CPT_SUSPEND_AT 8
-#endif
-constexpr int SUSPEND_AT = CPT_SUSPEND_AT;
-
-#ifndef CPT_STATIC_FIRST
-#define CPT_STATIC_FIRST 1
-#endif
-constexpr bool STATIC_FIRST = CPT_STATIC_FIRST != 0;
-
-// Deferred sky fetches run when this many 64ths of the tracing lanes hold one.
-#ifndef CPT_DEFER_MISS_ROUND
-#define CPT_DEFER_MISS_ROUND 40
-#endif
-constexpr int DEFER_MISS_ROUND = CPT_DEFER_MISS_ROUND;
+// Scheduling constants (SUSPEND_AT, STATIC_FIRST, DEFER_MISS_ROUND, CPT_LDS_BLOCK): cpt_tuning.hpp.
 
 // LDST: the 4-wide walk tree's compact image (its first LDS_TREE_NODES nodes: the top of the
 // tree) is staged in LDS once per workgroup, and the walk reads those nodes there (a lane's
@@ -112,9 +96,6 @@ constexpr int DEFER_MISS_ROUND = CPT_DEFER_MISS_ROUND;
 // step of the walk); a larger tree's other nodes come from the image in global memory.
 // One LDS workgroup per CU: 16 waves, 4 per SIMD (the image, the 16-bit stacks and the pending
 // sky fetches take 156 KB of the CU's 160 KB), which caps the kernel at 128 VGPRs.
-#ifndef CPT_LDS_BLOCK
-#define CPT_LDS_BLOCK 1024
-#endif
 template <bool LDST> constexpr int mk_block() { return LDST ? CPT_LDS_BLOCK : 256; }
 template <bool LDST> constexpr int mk_waves() { return LDST ? CPT_LDS_BLOCK / 256 : CPT_WAVES_PER_SIMD; }
 
@@ -261,24 +242,30 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             if (need) {
                 const int leader = __ffsll((unsigned long long)need) - 1;
                 uint32_t base = 0;
-                if (stat && first_take) {
+                const bool first_take_was = first_take;
+                first_take = false;
+                if (stat && first_take_was) {
                     // the wave's first tile by level: the heaviest tiles (cost order) go to the
                     // level-0 waves (one per SIMD), the lightest to level 3, so every SIMD holds
                     // one heavy wave that runs alone once its lighter neighbours finish
                     base = (level * (gridDim.x * 4u) + blockIdx.x * 4u + ((threadIdx.x >> 6) & 3u)) * 64u;
                     if (n_static >= n_work) exhausted = true;
                 } else {
-                    if (lane == leader) base = atomicAdd(p.work, (uint32_t)__popcll(need));
+                    // DIAGNOSTIC p.replicate > 1: every taken pixel runs on that many lanes, as
+                    // identical copies (tools/lane_latency.py); 1 in normal use
+                    const uint32_t rep = (uint32_t)p.replicate;
+                    const uint32_t n_take = ((uint32_t)__popcll(need) + rep - 1) / rep;
+                    if (lane == leader) base = atomicAdd(p.work, n_take);
                     base = __shfl(base, leader) + (stat ? n_static : 0u);
-                    if (base + (uint32_t)__popcll(need) >= n_work) exhausted = true;
+                    if (base + n_take >= n_work) exhausted = true;
                 }
-                first_take = false;
                 bool took = false;
                 if ((need >> lane) & 1ull) {
-                    const uint32_t rank = lane_rank(need);
+                    const uint32_t rank = stat && first_take_was ? lane_rank(need) : lane_rank(need) / (uint32_t)p.replicate;
                     const uint32_t id = base + rank;
                     int x, ri;
                     if (id < n_work && decode_pixel(p, id, x, ri, L.tile)) {
+                        execdiag::lanes(p.stats + 64, 0);
                         L.xy = (uint32_t)x | ((uint32_t)p.rows[ri] << 16);
                         L.pix = (uint32_t)ri * (uint32_t)p.width + (uint32_t)x;
                         L.s.v0 = p.rng[L.pix];
@@ -317,7 +304,10 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 }
             }
         }
-        if (begin) start_pass();
+        if (begin) {
+            execdiag::lanes(p.stats + 64, 10);
+            start_pass();
+        }
         stamps::lap(0);
         if (!__any(busy)) {
             if (!cons || retiring) break;
@@ -343,6 +333,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             // ---- one path segment: TraceRay (path_tracer.cu:141-158); a walk suspended in an
             // earlier round resumes here (LDST: trace_wide's suspension) -------------------
             if (COUNT && !ws.active) cnt.segments++;
+            execdiag::lanes(p.stats + 64, 12);
             const RayK rk = make_rayk(ray);
             const bool finite_ray = !(ray.o.x != ray.o.x || ray.o.y != ray.o.y || ray.o.z != ray.o.z ||
                                       ray.d.x != ray.d.x || ray.d.y != ray.d.y || ray.d.z != ray.d.z);
@@ -352,12 +343,18 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         if (busy && L.left > 0 && tr != 2) {
             // ---- ClosetHit / Miss and the path bookkeeping (path_tracer.cu:159-169) --------
             const bool hit = tr == 1;
+            execdiag::lanes(p.stats + 64, 13);
             Shade sh;
             v3 attr_normal;
             if (hit) {
                 if (COUNT) cnt.hits++;
+                execdiag::lanes(p.stats + 64, 4);
                 const Mat m = p.mats[code >> 2];
+#ifdef CPT_EXECDIAG
+                eval_material(m, h.normal, ray.d, L.s, sh, p.stats + 64);
+#else
                 eval_material(m, h.normal, ray.d, L.s, sh);
+#endif
                 attr_normal = h.normal;
                 ray.o = h.pos;                         // payload.hit_pos = position
                 stamps::lap(4);
@@ -380,17 +377,39 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 const bool flush = DEFER_MISS_ROUND == 0 || retiring || __ballot(need_now) != 0 ||
                                    __popcll(__ballot(pend || !hit)) * 64 >= DEFER_MISS_ROUND * __popcll(__ballot(1));
                 if (flush) {
+                    // One sky fetch per lane that needs one: the pending (older) direction, else
+                    // this miss.  A lane holding both fetches the pending one here; its new miss
+                    // becomes the pending fetch (or, on the chain's last pass, is fetched below).
                     const KParams& p = kernarg_params();   // cold fields (see the refill)
-                    if (pend) {   // older pending fetches first (their pass came first)
-                        const v3 pd = mk(pq[0 * BLK], pq[1 * BLK], pq[2 * BLK]);
-                        const v3 sky = miss_radiance(p, pd);
-                        const v3 pr = mk(pq[3 * BLK], pq[4 * BLK], pq[5 * BLK]);
-                        const v3 pa = mk(pq[6 * BLK], pq[7 * BLK], pq[8 * BLK]);
-                        L.sum = L.sum + (pr + pa * sky);
-                        pend = false;
+                    const bool had = pend;
+                    if (had || !hit) {
+                        execdiag::lanes(p.stats + 64, 6);
+                        const v3 dir = had ? mk(pq[0 * BLK], pq[1 * BLK], pq[2 * BLK]) : ray.d;
+                        const v3 sky = miss_radiance(p, dir);
+                        if (had) {
+                            const v3 pr = mk(pq[3 * BLK], pq[4 * BLK], pq[5 * BLK]);
+                            const v3 pa = mk(pq[6 * BLK], pq[7 * BLK], pq[8 * BLK]);
+                            L.sum = L.sum + (pr + pa * sky);
+                            pend = false;
+                        } else {
+                            sh.radiance = sky;
+                        }
                     }
-                    if (!hit) sh.radiance = miss_radiance(p, ray.d);
+                    if (had && !hit) {
+                        if (L.left == 1 || retiring) {   // the chain ends or is handed over: due now
+                            execdiag::lanes(p.stats + 64, 7);
+                            sh.radiance = miss_radiance(p, ray.d);
+                        } else {
+                            pq[0 * BLK] = ray.d.x; pq[1 * BLK] = ray.d.y; pq[2 * BLK] = ray.d.z;
+                            pq[3 * BLK] = rad.x; pq[4 * BLK] = rad.y; pq[5 * BLK] = rad.z;
+                            pq[6 * BLK] = att.x; pq[7 * BLK] = att.y; pq[8 * BLK] = att.z;
+                            pend = true;
+                            deferred = true;
+                            sh.radiance = mk1(0.f);
+                        }
+                    }
                 } else if (!hit) {
+                    execdiag::lanes(p.stats + 64, 8);
                     pq[0 * BLK] = ray.d.x; pq[1 * BLK] = ray.d.y; pq[2 * BLK] = ray.d.z;
                     pq[3 * BLK] = rad.x; pq[4 * BLK] = rad.y; pq[5 * BLK] = rad.z;
                     pq[6 * BLK] = att.x; pq[7 * BLK] = att.y; pq[8 * BLK] = att.z;
@@ -417,7 +436,10 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 if (AUX) { first_normal = nrm_acc; first_depth = dep_acc; }
                 if (--L.left > 0) {
                     if (retiring) hand_over = true;   // the next pass runs in a keeper wave
-                    else start_pass();
+                    else {
+                        execdiag::lanes(p.stats + 64, 9);
+                        start_pass();
+                    }
                 }
             }
         }
@@ -430,6 +452,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 if (lane == leader) base = atomicAdd(&s_q[1], (uint32_t)__popcll(ho));
                 base = __shfl(base, leader);
                 if (hand_over) {
+                    execdiag::lanes(p.stats + 64, 14);
                     const uint32_t slot = base + lane_rank(ho);
                     {   // slot < QS (ho_slots)
                         uint32_t* e = reinterpret_cast<uint32_t*>(qslab + 5 * (size_t)slot);
@@ -457,6 +480,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 atomicAdd(&p.tile_cost[L.tile], cnt.segments + cnt.nodes + cnt.prims - work_at_take);
             } else {
                 // ---- pixel finished: write back (path_tracer.cu:172-174) -----------------
+                execdiag::lanes(p.stats + 64, 11);
                 p.accum[L.pix] = make_float4(L.sum.x, L.sum.y, L.sum.z, L.passes);
                 if (AUX && p.spp > 0) {
                     p.normal[3 * (size_t)L.pix + 0] = first_normal.x;
@@ -816,7 +840,9 @@ static hipError_t launch_mk(const KParams& p, hipStream_t stream) {
     }
     // persistent grid: every resident slot once; lanes pull pixels from p.work
     const long long tiles = (long long)((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
-    long long want = (tiles * 64 * ((64 + p.lanes - 1) / p.lanes) + block - 1) / block;
+    // a wave holds p.lanes / p.replicate pixels at once (64 in normal use; fewer: DIAGNOSTIC)
+    const int per_wave = std::max(1, p.lanes / std::max(1, p.replicate));
+    long long want = (tiles * 64 * ((64 + per_wave - 1) / per_wave) + block - 1) / block;
     long long grid = std::min<long long>(want, (long long)blocks_per_cu * cus);
     if (grid < 1) return hipSuccess;
     hipLaunchKernelGGL((k_megakernel<S, A, P, T, C, H>), dim3((unsigned)grid), dim3(block), 0, stream, p);

@@ -9,6 +9,7 @@
 #include "cpt_device.hpp"
 #include "cpt_internal.hpp"
 #include "cpt_stamps.hpp"
+#include "cpt_tuning.hpp"
 
 namespace cpt {
 
@@ -283,9 +284,6 @@ __device__ __forceinline__ Hit hit_attributes(const Node& nd, const RayK& ray, f
 // reference's visit sequence, leaf-before-box order and pruning against the shrinking tmax
 // one for one — no stack, no scratch memory.
 // ======================================================================================
-#ifndef CPT_WAVES_PER_SIMD
-#define CPT_WAVES_PER_SIMD 3   // occupancy target of k_megakernel (launch bounds)
-#endif
 
 struct Counters {
     uint32_t segments, nodes, prims, hits, misses, fallbacks;
@@ -573,12 +571,8 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
     return 1;
 }
 
-// Leaf rounds of the wide walk run when this many 64ths of the wave's working lanes are
-// stopped at a parked leaf.
-#ifndef CPT_SPEC_LEAF_ROUND
-#define CPT_SPEC_LEAF_ROUND 28
-#endif
-constexpr int SPEC_LEAF_ROUND = CPT_SPEC_LEAF_ROUND;
+// Leaf rounds of the wide walk run when SPEC_LEAF_ROUND 64ths of the wave's working lanes are
+// stopped at a parked leaf (cpt_tuning.hpp).
 
 // ======================================================================================
 // The ordered walk on the 4-wide walk tree (DESIGN.md §Wide walk).  One iteration reads a
@@ -690,10 +684,6 @@ struct WalkState {
 // one iteration runs per call, so every walk progresses.  The result does not depend on
 // where a walk is suspended: it is the closest hit over a superset of the primitives the
 // reference tests, whatever the culling limit was at each node (DESIGN.md §Ordered walk).
-#ifndef CPT_SUSPEND_MIN_DONE
-#define CPT_SUSPEND_MIN_DONE 40
-#endif
-constexpr int SUSPEND_MIN_DONE = CPT_SUSPEND_MIN_DONE;
 
 // `tree` is the block's LDS copy of the image's first lds_tree_nodes(n_wide) nodes; HYB: the
 // tree is larger (n_wide > LDS_TREE_NODES), so some nodes come from global memory.
@@ -762,6 +752,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
             cur = pop();
         }
         if (cur >= 0) {
+            execdiag::lanes(p.stats + 64, 1);
             if (STATS) {
                 cnt.nodes++;
                 cnt.gnodes += HYB && cur >= n_lds ? 1u : 0u;
@@ -811,6 +802,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         if (__popcll(w) <= suspend_at && __popcll(participants & ~w) >= SUSPEND_MIN_DONE && it > 0) break;
         if (__popcll(__ballot(stopped)) * 64 >= SPEC_LEAF_ROUND * __popcll(w) && parked >= 0) {
             stamps::count(10);
+            execdiag::lanes(p.stats + 64, 2);
             if (STATS) cnt.prims++;
             const Node lf = leaf(parked);
             int k;
@@ -827,6 +819,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     ws.active = working;
     if (working) return 2;   // suspended
     if (best < 0) return 0;
+    execdiag::lanes(p.stats + 64, 3);
     const Node wn = leaf(best);
     Node box;
     leaf_aabb(wn, box);
@@ -938,7 +931,8 @@ __device__ __forceinline__ bool refract(v3 v, v3 n, float ni_over_nt, v3& refrac
 //                                       reflect(dir, N) : lobe(1/2) about N
 //   Glass (:101-143):  x1 x2; refract/schlick; u;  lobe(1/alpha) about reflect(in, N) or
 //                      the refracted direction
-__device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow& rng, Shade& out) {
+__device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow& rng, Shade& out,
+                                     unsigned long long* diag = nullptr) {
     const v3 kd = mk(m.att_x, m.att_y, m.att_z);   // GetKd(0, 0)
     const v3 zero = mk(0.0f, 0.0f, 0.0f);
     const int type = (m.type >= 1 && m.type <= 3) ? m.type : 0;   // Test / unknown: Diffuse (:161)
@@ -948,9 +942,11 @@ __device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow&
     if (type == 1) {
         axis = reflect(in_dir, normal);
     } else if (type == 2) {
+        if (diag) execdiag::lanes(diag, 15);
         if (uniform(rng) < m.reflectivity) axis = reflect(in_dir, normal);
         else ia = 1.0 / 2.0;
     } else if (type == 3) {
+        if (diag) execdiag::lanes(diag, 5);
         v3 outward, refracted = mk1(0.0f);
         float ni_over_nt, reflect_prob, cosine;
         const v3 in = normalize(in_dir);

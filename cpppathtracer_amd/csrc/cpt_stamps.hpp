@@ -49,4 +49,29 @@ __device__ __forceinline__ void count(int) {}
 __device__ __forceinline__ void flush(unsigned long long*) {}
 #endif
 }  // namespace stamps
+
+// DIAGNOSTIC exec-mask census (CPT_EXECDIAG builds only; never the timed library): lanes(out, r)
+// records one entry of code region r by the wave with its active-lane count -- out[r] entries,
+// out[16 + r] entries with <= 16 active lanes, out[32 + r] with <= 8, out[48 + r] the sum of
+// active lanes -- by global atomics from the wave's first active lane.  With several waves per
+// CU a VALU instruction with few active lanes costs several times the cycles of a full one
+// (tools/exec_count_probe.hip), so a region entered thinly is a candidate for predication.
+// Regions: tools/execdiag.py.
+namespace execdiag {
+constexpr int N_REGIONS = 16;
+#ifdef CPT_EXECDIAG
+__device__ __forceinline__ void lanes(unsigned long long* out, int r) {
+    const uint64_t m = __ballot(1);
+    if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)m) - 1) {
+        const unsigned long long n = (unsigned long long)__popcll(m);
+        atomicAdd(out + r, 1ull);
+        if (n <= 16) atomicAdd(out + N_REGIONS + r, 1ull);
+        if (n <= 8) atomicAdd(out + 2 * N_REGIONS + r, 1ull);
+        atomicAdd(out + 3 * N_REGIONS + r, n);
+    }
+}
+#else
+__device__ __forceinline__ void lanes(unsigned long long*, int) {}
+#endif
+}  // namespace execdiag
 }  // namespace cpt

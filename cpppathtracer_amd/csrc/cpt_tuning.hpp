@@ -1,0 +1,51 @@
+// cpt_tuning.hpp — the megakernel's scheduling constants, in one place.  Each value was chosen by
+// interleaved same-box A/Bs at C4 (the A/B tables; logs under profiles/); none changes
+// a result, only which lanes work together when.  The #ifndef lets an A/B build
+// (cpppathtracer_amd/build.py defines=...) override one; the shipped library uses these values.
+#pragma once
+
+namespace cpt {
+
+// Persistent LDS-walk workgroup: 1024 lanes = 16 waves, 4 per SIMD (the tree image, the 16-bit
+// walk stacks and the pending sky fetches take 156 KB of the CU's 160 KB; 128 VGPRs).
+// 768 lanes (3 waves/SIMD): 1153 vs 1256 Mpaths/s (profiles/r02/ab_w4_1024.log).
+#ifndef CPT_LDS_BLOCK
+#define CPT_LDS_BLOCK 1024
+#endif
+// Occupancy target of the kernels without the LDS tree image (reference and binary walks).
+#ifndef CPT_WAVES_PER_SIMD
+#define CPT_WAVES_PER_SIMD 3
+#endif
+// A round's walks are suspended once at most this many lanes of the wave still walk and at
+// least SUSPEND_MIN_DONE lanes of the call have finished theirs (cpt_path.hpp trace_wide):
+// 1356-1392 vs 1304 Mpaths/s without suspension (profiles/r02/ab_suspend*.log, ab_threshold_combo.log).
+#ifndef CPT_SUSPEND_AT
+#define CPT_SUSPEND_AT 8
+#endif
+#ifndef CPT_SUSPEND_MIN_DONE
+#define CPT_SUSPEND_MIN_DONE 40
+#endif
+// Leaf rounds of the wide walk run when this many 64ths of the wave's working lanes are stopped
+// at a parked leaf (profiles/r01n_ab_thresholds_resweep.log, r02/ab_threshold_combo.log).
+#ifndef CPT_SPEC_LEAF_ROUND
+#define CPT_SPEC_LEAF_ROUND 28
+#endif
+// Deferred sky fetches run when this many 64ths of the tracing lanes hold one
+// (profiles/r01l_ab_defer_miss.log, r02/ab_threshold_combo.log).
+#ifndef CPT_DEFER_MISS_ROUND
+#define CPT_DEFER_MISS_ROUND 40
+#endif
+// With the cost schedule, each wave's first tile is placed by consolidation level (the heaviest
+// tiles to the level-0 wave of every SIMD) instead of taken from the counter
+// (profiles/r02/reh_static_first_*.log).
+#ifndef CPT_STATIC_FIRST
+#define CPT_STATIC_FIRST 1
+#endif
+
+constexpr int SUSPEND_AT = CPT_SUSPEND_AT;
+constexpr int SUSPEND_MIN_DONE = CPT_SUSPEND_MIN_DONE;
+constexpr int SPEC_LEAF_ROUND = CPT_SPEC_LEAF_ROUND;
+constexpr int DEFER_MISS_ROUND = CPT_DEFER_MISS_ROUND;
+constexpr bool STATIC_FIRST = CPT_STATIC_FIRST != 0;
+
+}  // namespace cpt

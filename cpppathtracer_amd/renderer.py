@@ -217,6 +217,12 @@ class Renderer:
         self._check(self._L.cpt_get_diag_counters(self._ctx, _p(out)))
         return [int(x) for x in out]
 
+    def execdiag_counters(self):
+        """DIAGNOSTIC: the exec-mask census of a CPT_EXECDIAG build (cpt_stamps.hpp execdiag)."""
+        out = np.zeros(64, dtype=np.uint64)
+        self._check(self._L.cpt_get_execdiag_counters(self._ctx, _p(out)))
+        return out.reshape(4, 16)
+
     def walk_info(self):
         """[reference-order nodes, binary octant-order nodes, 4-wide nodes per octant, platforms]."""
         out = np.zeros(4, dtype=np.int32)

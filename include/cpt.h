@@ -257,6 +257,10 @@ int cpt_get_raw_counters(cpt_ctx* ctx, uint64_t* out8);
 /* DIAGNOSTIC: the 16 wave-time stamp slots of a CPT_STAMPS build (cpt_stamps.hpp; all zero in
  * the shipped library), summed over the renders since the last cpt_reset_stats. */
 int cpt_get_diag_counters(cpt_ctx* ctx, uint64_t* out16);
+/* DIAGNOSTIC: the exec-mask census of a CPT_EXECDIAG build (cpt_stamps.hpp execdiag; all zero in
+ * the shipped library): per code region r < 16, [r] entries, [16 + r] entries with <= 16 active
+ * lanes, [32 + r] with <= 8, [48 + r] the sum of active lanes, since the last cpt_reset_stats. */
+int cpt_get_execdiag_counters(cpt_ctx* ctx, uint64_t* out64);
 /* Node counts of the scene's walk structures (host-side, no GPU work): [0] the reference
  * order (bvh.cu's tree, 32-B nodes), [1] each octant order of the binary walk tree, [2] the
  * 4-wide walk tree's nodes (112 B each in its compact image, the first 512 staged in LDS; 0 =

@@ -59,5 +59,5 @@ def test_main_spawns_before_touching_the_gpu(monkeypatch):
 def test_defaults_are_the_baseline_workload():
     b = _bench()
     a = b.parse_args([])
-    assert (a.gpus, a.config, a.scaling, a.walk, a.path) == (None, "c4", "strong", "ordered", "megakernel")
+    assert (a.gpus, a.config, a.scaling, a.walk, a.path) == (None, "c4", "weak", "ordered", "megakernel")
     assert b.parse_args(["--config", "c5"]).config == "c5"

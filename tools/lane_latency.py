@@ -55,6 +55,9 @@ def main():
     ap.add_argument("--row", type=int, default=600, help="first of 8 rows")
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--max-chain", type=float, default=None, help="oracle: longest chain (segments) of the set")
+    ap.add_argument("--replicate", action="store_true",
+                    help="k lanes per wave run ONE pixel as k identical copies (CPT_REPLICATE=k): does a lone "
+                         "chain run faster on more lanes?")
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
@@ -62,6 +65,8 @@ def main():
     res = {}
     for k in (int(x) for x in a.lanes.split(",")):
         env = dict(os.environ, CPT_LANES_PER_WAVE=str(k))
+        if a.replicate:
+            env["CPT_REPLICATE"] = str(k)
         out = subprocess.run([sys.executable, __file__, "--child", "--width", str(a.width), "--row", str(a.row),
                               "--spp", str(a.spp)], env=env, capture_output=True, text=True, timeout=300)
         if out.returncode != 0:
@@ -73,7 +78,7 @@ def main():
             res[k]["us_per_segment_longest_chain"] = round(1000.0 * ms / a.max_chain, 3)
         print(k, res[k], flush=True)
     print(json.dumps({"lib": os.environ.get("CPT_LIB_PATH", "libcpt.so"), "width": a.width, "row": a.row,
-                      "spp": a.spp, "lanes": res}), flush=True)
+                      "spp": a.spp, "replicate": a.replicate, "lanes": res}), flush=True)
 
 
 if __name__ == "__main__":
