@@ -104,6 +104,13 @@ __device__ inline v3 tex2d(const KParams& p, float u, float v) {
 // ======================================================================================
 // Per-segment ray with its exact reciprocals (see qdiv in cpt_device.hpp).
 // ======================================================================================
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// Margins of the ordered walk's conservative slab test (slab_pass below): relative to the
+// plane distances, and absolute (the exit offsets carry 2 x WALK_MARGIN_ABS, rounded up).
+constexpr float WALK_MARGIN_REL = 1e-3f, WALK_MARGIN_ABS = 1e-4f;
+constexpr float SLAB_ABS = 2.0f * WALK_MARGIN_ABS * (1.0f + 2.0f * WALK_MARGIN_REL);
+
 struct RayK {
     v3 o, d;
     float tmin;
@@ -111,11 +118,26 @@ struct RayK {
                          // yx and yz are filled by with_slab() where an exact slab test runs
     double ya;           // 1/dot(d,d)            (sphere roots, object.cu:15-20)
     double yc;           // 1/(dx*dx + dz*dz)     (cylinder side roots, object.cu:69-79)
-    float ix, iy, iz;    // f32 1/d per axis for the ordered walk's conservative slabs; 0 = the
-                         // axis is skipped (|d| < 1e-30: no constraint, which only widens)
-    float bx, by, bz;    // 2e30 on a skipped axis, else 0: fma(b - o, i, -+bias) = -+2e30 there
+    // The ordered walk's conservative slabs (slab_reject<*, true>, wide_pair): a plane p of axis
+    // a is at t = fma(p, i_a, c_a), with i_a = f32 1/d_a and c_a = -(o_a * i_a) -+ beta_a for
+    // entry (n) and exit (f) planes; beta_a = 2^-20 |o_a * i_a| covers the rounding of the
+    // product and the sum, so an entry plane's t is never above (p - o_a) * i_a before its own
+    // rounding (DESIGN.md §Ordered walk).  The exit offsets also carry the test's absolute
+    // margin.  A skipped axis (|d| < 1e-30) has i_a = 0 and c_a = -+2e30: no constraint, which
+    // only widens.
+    float ix, iy, iz;
+    float nx, ny, nz;    // entry offsets
+    float fx, fy, fz;    // exit offsets (+ SLAB_ABS)
     float t3;            // conservative tmin limit: (tmin - 1e-4) * (1 + 2e-3)
 };
+
+// Entry / exit offsets of one axis of the conservative slabs (RayK::ix ...).
+__device__ __forceinline__ void slab_axis(float o, float d, float& i, float& cn, float& cf) {
+    i = __builtin_fabsf(d) >= 1e-30f ? rcp_f(d) : 0.0f;
+    const float pr = o * i, beta = __builtin_fabsf(pr) * 0x1p-20f;
+    cn = i != 0.0f ? -pr - beta : -DEFAULT_RAY_TMAX * 2;
+    cf = i != 0.0f ? (-pr + beta) + SLAB_ABS : DEFAULT_RAY_TMAX * 2;
+}
 
 __device__ __forceinline__ RayK make_rayk(const Ray& r) {
     RayK k;
@@ -127,12 +149,9 @@ __device__ __forceinline__ RayK make_rayk(const Ray& r) {
     k.yz = 0.0;
     k.ya = rcp_d(dot(r.d, r.d));
     k.yc = rcp_d(r.d.x * r.d.x + r.d.z * r.d.z);
-    k.ix = __builtin_fabsf(r.d.x) >= 1e-30f ? rcp_f(r.d.x) : 0.0f;
-    k.iy = __builtin_fabsf(r.d.y) >= 1e-30f ? rcp_f(r.d.y) : 0.0f;
-    k.iz = __builtin_fabsf(r.d.z) >= 1e-30f ? rcp_f(r.d.z) : 0.0f;
-    k.bx = k.ix != 0.0f ? 0.0f : DEFAULT_RAY_TMAX * 2;
-    k.by = k.iy != 0.0f ? 0.0f : DEFAULT_RAY_TMAX * 2;
-    k.bz = k.iz != 0.0f ? 0.0f : DEFAULT_RAY_TMAX * 2;
+    slab_axis(r.o.x, r.d.x, k.ix, k.nx, k.fx);
+    slab_axis(r.o.y, r.d.y, k.iy, k.ny, k.fy);
+    slab_axis(r.o.z, r.d.z, k.iz, k.nz, k.fz);
     k.t3 = (r.tmin - 1e-4f) * (1.0f + 2e-3f);
     return k;
 }
@@ -300,31 +319,38 @@ struct Counters {
 // widened by a relative margin before the three comparisons, so that a primitive whose
 // computed hit lies slightly outside its box by rounding is still tested (DESIGN.md
 // §Ordered walk).  The margin dwarfs the reciprocal's few-ulp error.
-constexpr float WALK_MARGIN_REL = 1e-3f, WALK_MARGIN_ABS = 1e-4f;
 // The conservative walk's tmax limit (slab_reject<*, true>'s `tmax` argument).
 __device__ __forceinline__ float walk_limit(float tmax) {
     return (tmax + WALK_MARGIN_ABS) * (1.0f + 2.0f * WALK_MARGIN_REL);
 }
 
+// The conservative pass test on a box's entry / exit distances lo = max over axes of the entry
+// planes' fma(p, i, c_n), hi = min of the exit planes' fma(p, i, c_f) (RayK::ix ...; hi carries
+// the absolute margin through c_f).  With lo' = max(lo, t3) and hi' = min(hi, limit) the box
+// passes iff
+//     lo' - 1e-3 |lo'|  <=  hi' + 1e-3 |hi'|.
+// It passes whenever the reference test on the exact quotients (b - o) / d passes with any
+// tmax <= the walk's: that one needs lo <= hi, lo <= tmax and hi >= tmin, and each of the four
+// choices of (lo', hi') then satisfies the inequality with the relative margin to spare for
+// the planes' few-ulp rounding (DESIGN.md §Ordered walk).  lo' is also the child's sort key.
+__device__ __forceinline__ bool slab_pass(float& lo, float hi, float t3, float limit) {
+    lo = __builtin_fmaxf(lo, t3);
+    hi = __builtin_fminf(hi, limit);
+    return __builtin_fmaf(-WALK_MARGIN_REL, __builtin_fabsf(lo), lo) <= __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(hi), hi);
+}
+
 template <bool FAST, bool CONS = false>
 __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, float tmax) {
     if (CONS) {
-        // (b - o) * (1/d): a few ulps from the exact quotient, far inside the margin.  Skipped
-        // axes (i == 0) get -+2e30 through the fma's addend: no constraint.  `tmax` is the
-        // widened limit walk_limit(tmax).  Reject iff
-        //   lo - m(lo) > hi + m(hi),  i.e. lo - hi > 1e-3 (|lo| + |hi|) + 2e-4  (box missed),
-        //   lo > walk_limit(tmax)                                           (box beyond tmax),
-        //   hi < ray.t3                                                      (box behind tmin),
-        // each implied by the exact test's rejection with a margin to spare.
-        const float t0x = __builtin_fmaf(nd.a0 - ray.o.x, ray.ix, -ray.bx), t1x = __builtin_fmaf(nd.b0 - ray.o.x, ray.ix, ray.bx);
-        const float t0y = __builtin_fmaf(nd.a1 - ray.o.y, ray.iy, -ray.by), t1y = __builtin_fmaf(nd.b1 - ray.o.y, ray.iy, ray.by);
-        const float t0z = __builtin_fmaf(nd.a2 - ray.o.z, ray.iz, -ray.bz), t1z = __builtin_fmaf(nd.b2 - ray.o.z, ray.iz, ray.bz);
-        const float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
-                                         __builtin_fminf(t0z, t1z));
-        const float hi = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
-                                         __builtin_fmaxf(t0z, t1z));
-        const float m2 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo) + __builtin_fabsf(hi), 2.0f * WALK_MARGIN_ABS);
-        return lo - hi > m2 || lo > tmax || hi < ray.t3;
+        // The entry plane of an axis is its min plane when 1/d >= 0 (also on a skipped axis).
+        const bool px = ray.ix >= 0.0f, py = ray.iy >= 0.0f, pz = ray.iz >= 0.0f;
+        float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(px ? nd.a0 : nd.b0, ray.ix, ray.nx),
+                                                   __builtin_fmaf(py ? nd.a1 : nd.b1, ray.iy, ray.ny)),
+                                   __builtin_fmaf(pz ? nd.a2 : nd.b2, ray.iz, ray.nz));
+        const float hi = __builtin_fminf(__builtin_fminf(__builtin_fmaf(px ? nd.b0 : nd.a0, ray.ix, ray.fx),
+                                                         __builtin_fmaf(py ? nd.b1 : nd.a1, ray.iy, ray.fy)),
+                                         __builtin_fmaf(pz ? nd.b2 : nd.a2, ray.iz, ray.fz));
+        return !slab_pass(lo, hi, ray.t3, tmax);
     }
     float t0x = qdiv_raw(nd.a0 - ray.o.x, ray.yx), t1x = qdiv_raw(nd.b0 - ray.o.x, ray.yx);
     float t0y = qdiv_raw(nd.a1 - ray.o.y, ray.yy), t1y = qdiv_raw(nd.b1 - ray.o.y, ray.yy);
@@ -375,21 +401,14 @@ __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, flo
 // it leaves through.  For an axis with i != 0 the sign of i is the octant's, so the entry
 // plane's distance is the min of the pair and the exit plane's the max (the subtraction, the
 // product and the fma are monotone); a skipped axis gives -2e30 / +2e30 in that order.  So
-// lo and hi are bit for bit those of the min/max form and the decision is the same.  x and y
-// go through packed f32 ops (v_pk_add/v_pk_fma_f32: two lanes of IEEE f32 per instruction).
-typedef float f2v __attribute__((ext_vector_type(2)));
+// lo and hi are bit for bit those of the min/max form and the decision is the same.
 
 __device__ __forceinline__ bool slab_reject_octant(const Node& nd, const RayK& ray, float limit) {
-    const f2v oxy = {ray.o.x, ray.o.y}, ixy = {ray.ix, ray.iy}, bxy = {ray.bx, ray.by};
-    const f2v nxy = {nd.a0, nd.a1}, fxy = {nd.b0, nd.b1};
-    const f2v tn = __builtin_elementwise_fma(nxy - oxy, ixy, -bxy);
-    const f2v tf = __builtin_elementwise_fma(fxy - oxy, ixy, bxy);
-    const float tnz = __builtin_fmaf(nd.a2 - ray.o.z, ray.iz, -ray.bz);
-    const float tfz = __builtin_fmaf(nd.b2 - ray.o.z, ray.iz, ray.bz);
-    const float lo = __builtin_fmaxf(__builtin_fmaxf(tn.x, tn.y), tnz);
-    const float hi = __builtin_fminf(__builtin_fminf(tf.x, tf.y), tfz);
-    const float m2 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo) + __builtin_fabsf(hi), 2.0f * WALK_MARGIN_ABS);
-    return lo - hi > m2 || lo > limit || hi < ray.t3;
+    float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(nd.a0, ray.ix, ray.nx), __builtin_fmaf(nd.a1, ray.iy, ray.ny)),
+                               __builtin_fmaf(nd.a2, ray.iz, ray.nz));
+    const float hi = __builtin_fminf(__builtin_fminf(__builtin_fmaf(nd.b0, ray.ix, ray.fx), __builtin_fmaf(nd.b1, ray.iy, ray.fy)),
+                                     __builtin_fmaf(nd.b2, ray.iz, ray.fz));
+    return !slab_pass(lo, hi, ray.t3, limit);
 }
 
 // Node fetch.  BufSrc reads through a buffer descriptor over the whole node array (built from
@@ -640,28 +659,20 @@ __device__ __forceinline__ WideNode load_wide_node(const uint4* tree, int n_lds,
         sx, sy, sz);
 }
 
-// Hit mask of children (a, b) of a pair: slab_reject_octant for each, in scalar f32 ops (the
-// packed v_pk_add/v_pk_fma form needs the ray's o, 1/d and bias as register pairs: 9 more
-// VGPRs, spilled, and measured 0.7% slower).
+// Hit mask of children (a, b) of a pair: slab_reject_octant for each; lo_a / lo_b get their
+// sort keys (slab_pass's lo').
 __device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], const RayK& ray, float limit,
                                               float& lo_a, float& lo_b) {
-    auto near = [&](float pl, float o, float i, float b) { return __builtin_fmaf(pl - o, i, -b); };
-    auto far = [&](float pl, float o, float i, float b) { return __builtin_fmaf(pl - o, i, b); };
-    const float lo0 = __builtin_fmaxf(__builtin_fmaxf(near(e[0].x, ray.o.x, ray.ix, ray.bx), near(e[1].x, ray.o.y, ray.iy, ray.by)),
-                                      near(e[2].x, ray.o.z, ray.iz, ray.bz));
-    const float hi0 = __builtin_fminf(__builtin_fminf(far(x[0].x, ray.o.x, ray.ix, ray.bx), far(x[1].x, ray.o.y, ray.iy, ray.by)),
-                                      far(x[2].x, ray.o.z, ray.iz, ray.bz));
-    const float lo1 = __builtin_fmaxf(__builtin_fmaxf(near(e[0].y, ray.o.x, ray.ix, ray.bx), near(e[1].y, ray.o.y, ray.iy, ray.by)),
-                                      near(e[2].y, ray.o.z, ray.iz, ray.bz));
-    const float hi1 = __builtin_fminf(__builtin_fminf(far(x[0].y, ray.o.x, ray.ix, ray.bx), far(x[1].y, ray.o.y, ray.iy, ray.by)),
-                                      far(x[2].y, ray.o.z, ray.iz, ray.bz));
-    const float m0 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo0) + __builtin_fabsf(hi0), 2.0f * WALK_MARGIN_ABS);
-    const float m1 = __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(lo1) + __builtin_fabsf(hi1), 2.0f * WALK_MARGIN_ABS);
-    const bool rej0 = lo0 - hi0 > m0 || lo0 > limit || hi0 < ray.t3;
-    const bool rej1 = lo1 - hi1 > m1 || lo1 > limit || hi1 < ray.t3;
-    lo_a = lo0;
-    lo_b = lo1;
-    return (rej0 ? 0u : 1u) | (rej1 ? 0u : 2u);
+    lo_a = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(e[0].x, ray.ix, ray.nx), __builtin_fmaf(e[1].x, ray.iy, ray.ny)),
+                           __builtin_fmaf(e[2].x, ray.iz, ray.nz));
+    lo_b = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(e[0].y, ray.ix, ray.nx), __builtin_fmaf(e[1].y, ray.iy, ray.ny)),
+                           __builtin_fmaf(e[2].y, ray.iz, ray.nz));
+    const float hi_a = __builtin_fminf(__builtin_fminf(__builtin_fmaf(x[0].x, ray.ix, ray.fx), __builtin_fmaf(x[1].x, ray.iy, ray.fy)),
+                                       __builtin_fmaf(x[2].x, ray.iz, ray.fz));
+    const float hi_b = __builtin_fminf(__builtin_fminf(__builtin_fmaf(x[0].y, ray.ix, ray.fx), __builtin_fmaf(x[1].y, ray.iy, ray.fy)),
+                                       __builtin_fmaf(x[2].y, ray.iz, ray.fz));
+    const bool pa = slab_pass(lo_a, hi_a, ray.t3, limit), pb = slab_pass(lo_b, hi_b, ray.t3, limit);
+    return (pa ? 1u : 0u) | (pb ? 2u : 0u);
 }
 
 // Child refs (the image's int16 words, cpt_capi.cpp linearise_wide): >= 0 a wide node, -1 none,
@@ -783,7 +794,8 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
 #pragma unroll
             for (int k = 3; k >= 0; --k) {
                 *top = (int16_t)n.ref[k];
-                top += (((m >> k) & 1u) && k != bk) ? BLK : 0;
+                const bool pushed = ((m >> k) & 1u) && k != bk;
+                top += pushed ? BLK : 0;
             }
             const int n01 = (bk & 1) ? n.ref[1] : n.ref[0], n23 = (bk & 1) ? n.ref[3] : n.ref[2];
             cur = m == 0 ? pop() : ((bk & 2) ? n23 : n01);
