@@ -619,6 +619,7 @@ typedef __attribute__((address_space(3))) int16_t lds_i16;
 struct WideNode {
     f2v e[3][2], x[3][2];   // entry / exit planes per axis, children (0,1) and (2,3)
     int ref[4];
+    uint32_t r01, r23;      // the refs as stored: slots 0 | 1 << 16, 2 | 3 << 16
 };
 
 // A node of the compact image for a ray whose direction signs are (sx, sy, sz): the entry
@@ -637,6 +638,8 @@ __device__ __forceinline__ WideNode wide_node(const QUAD& quad, int sx, int sy, 
     n.e[2][0] = lo(ez); n.e[2][1] = hi(ez); n.x[2][0] = lo(xz); n.x[2][1] = hi(xz);
     n.ref[0] = (int)(int16_t)(r.x & 0xffffu); n.ref[1] = (int)(int16_t)(r.x >> 16);
     n.ref[2] = (int)(int16_t)(r.y & 0xffffu); n.ref[3] = (int)(int16_t)(r.y >> 16);
+    n.r01 = r.x;
+    n.r23 = r.y;
     return n;
 }
 
@@ -647,7 +650,8 @@ template <bool HYB>
 __device__ __forceinline__ WideNode load_wide_node(const uint4* tree, int n_lds, __amdgpu_buffer_rsrc_t rsrc,
                                                    uint32_t image_off, int cur, int sx, int sy, int sz) {
     if (!HYB || __builtin_expect(cur < n_lds, 1)) {
-        const uint4* q = tree + cur * 7;
+        // cur < 2^15: a 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate)
+        const uint4* q = (const uint4*)((const char*)tree + __umul24((uint32_t)cur, 112u));
         return wide_node([&](int k) { return q[k]; }, sx, sy, sz);
     }
     const uint32_t off = image_off + (uint32_t)cur * 112u;
@@ -775,30 +779,29 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
             const uint32_t m = wide_pair(e01, x01, ray, limit, lo[0], lo[1]) |
                                (wide_pair(e23, x23, ray, limit, lo[2], lo[3]) << 2);
             // The hit child walked next is the one with the nearest entry distance (first slot
-            // on ties).  The other hits are pushed (slot 3 first) without branches: every slot
+            // on ties): the minimum of sort keys made of the distance's bits with the slot in
+            // the two low bits (integer order is the float order for the distances >= 0; the
+            // few negative ones, of boxes the ray starts in, come first, and ties within 4 ulps
+            // go to the first slot -- the order only steers the walk, the hits do not depend
+            // on it).  The other hits are pushed (slot 3 first) without branches: every slot
             // is written at the top, and the top moves past it only when it is pushed (the
             // host bounds the depth, so a write at an unmoved top stays inside the lane's
             // stack).
-            int bk = 0;
-            {
-                float bd = (m & 1u) ? lo[0] : __builtin_inff();
+            int key = 0x7fffffff;
 #pragma unroll
-                for (int k = 1; k < 4; ++k) {
-                    const float d = ((m >> k) & 1u) ? lo[k] : __builtin_inff();
-                    const bool closer = d < bd;
-                    bd = closer ? d : bd;
-                    bk = closer ? k : bk;
-                }
-                if (bd == __builtin_inff()) bk = __builtin_ctz(m | 16u);   // no finite distance
+            for (int k = 0; k < 4; ++k) {
+                const int kk = (__float_as_int(lo[k]) & ~3) | k;
+                key = ((m >> k) & 1u) && kk < key ? kk : key;
             }
+            const int bk = key & 3;
+            const uint32_t pm = m & ~(1u << bk);   // the hits pushed
 #pragma unroll
             for (int k = 3; k >= 0; --k) {
                 *top = (int16_t)n.ref[k];
-                const bool pushed = ((m >> k) & 1u) && k != bk;
-                top += pushed ? BLK : 0;
+                top += ((pm >> k) & 1u) * BLK;
             }
-            const int n01 = (bk & 1) ? n.ref[1] : n.ref[0], n23 = (bk & 1) ? n.ref[3] : n.ref[2];
-            cur = m == 0 ? pop() : ((bk & 2) ? n23 : n01);
+            const uint32_t word = (bk & 2) ? n.r23 : n.r01;
+            cur = m == 0 ? pop() : (int)(int16_t)(word >> ((bk & 1) << 4));
             if (cur <= -2 && parked < 0) {   // park the nearest leaf at once
                 parked = leaf_of(cur);
                 cur = pop();
