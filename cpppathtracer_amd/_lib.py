@@ -48,6 +48,7 @@ PROTOTYPES = {
     "cpt_get_raw_counters": (_I, [_P, _P]),
     "cpt_get_walk_info": (_I, [_P, _P]),
     "cpt_measure_read_bandwidth": (_I, [_P, _SZ, _I, _P]),
+    "cpt_cap_disk_bound": (_I, [ctypes.c_float, _P]),
     "cpt_last_render_ms": (_I, [_P, _P]),
     "cpt_get_diag_counters": (_I, [_P, _P]),
     "cpt_get_execdiag_counters": (_I, [_P, _P]),

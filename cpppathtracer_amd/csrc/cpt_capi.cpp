@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -145,6 +146,21 @@ void build_host_bvh(HostBvh& b, const std::vector<cpt_object>& objs) {
     b.nodes[0].parent = -1;
 }
 
+// The cap-disk bound of a cylinder leaf (Node::b1, cpt_path.hpp cap_test): the largest float c
+// with  sqrtf(q) < radius  <=>  q <= c  for every float q.  sqrtf is correctly rounded, so
+// sqrtf(q) < r  <=>  sqrtf(q) <= pred(r)  <=>  sqrt(q) < m, m = (pred(r) + r) / 2 (a tie at m
+// is impossible: m has 25 significant bits, so m^2 has at least 49 and is no float)  <=>
+// q < m^2 (exact in double)  <=>  q <= RD(m^2).  radius <= 0 or NaN: never (c = -1).
+float cap_disk_bound(float r) {
+    if (!(r > 0.0f)) return -1.0f;
+    if (r == INFINITY) return FLT_MAX;
+    const double m = ((double)std::nextafter(r, 0.0f) + (double)r) * 0.5;
+    const double x = m * m;
+    float c = (float)x;
+    if ((double)c > x) c = std::nextafter(c, -INFINITY);
+    return c;
+}
+
 // Node contents: internal -> its box; leaf -> the primitive inline (cpt_device.hpp Node).
 Node make_node(const BNode& n, const std::vector<cpt_object>& objs, const std::vector<int>& mat_of_obj) {
     Node g;
@@ -153,6 +169,7 @@ Node make_node(const BNode& n, const std::vector<cpt_object>& objs, const std::v
         g.a0 = o.center.x; g.a1 = o.center.y; g.a2 = o.center.z;
         g.b0 = o.radius; g.b1 = o.y_pos; g.b2 = o.height;
         int type = (o.type >= 0 && o.type <= 2) ? o.type : 3;
+        if (type == CPT_PRIM_CYLINDER) g.b1 = cap_disk_bound(o.radius);   // y_pos is a platform's
         g.code = (mat_of_obj[n.obj] << 2) | type;
     } else {
         g.a0 = n.bmin.x; g.a1 = n.bmin.y; g.a2 = n.bmin.z;
@@ -1572,6 +1589,12 @@ int cpt_math_batch(cpt_ctx* c, int op, const float* a, const float* b, float* ou
     (void)hipFree(db);
     (void)hipFree(dout);
     if (e != hipSuccess) return fail(c, CPT_ERR_HIP, "cpt_math_batch: %s", hipGetErrorString(e));
+    return CPT_OK;
+}
+
+int cpt_cap_disk_bound(float radius, float* out) {
+    if (!out) return CPT_ERR_INVALID_ARG;
+    *out = cap_disk_bound(radius);
     return CPT_OK;
 }
 

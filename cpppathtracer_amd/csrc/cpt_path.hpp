@@ -223,14 +223,17 @@ __device__ __forceinline__ bool platform_test(const Node& pl, const RayK& ray, f
     return false;
 }
 
-// One cylinder cap disk (object.cu:52-77)
-__device__ __forceinline__ bool cap_test(float cx, float cz, float radius, const RayK& ray, float& tmax, int& kind,
+// One cylinder cap disk (object.cu:52-77).  The reference's `sqrtf(q) < radius` is decided as
+// `q <= bound` with the leaf's precomputed bound (Node::b1 of a cylinder leaf, cpt_capi.cpp
+// cap_disk_bound): the same decision for every float q, without the correctly rounded square
+// root.
+__device__ __forceinline__ bool cap_test(float cx, float cz, float bound, const RayK& ray, float& tmax, int& kind,
                                          float ypos) {
     if ((ray.o.y < ypos && ray.d.y > 0.f) || (ray.o.y > ypos && ray.d.y < 0.f)) {
         const float temp = qdiv(ypos - ray.o.y, ray.d.y, ray.yy);
         if (temp < tmax && temp > ray.tmin) {
             const float hx = ray.o.x + temp * ray.d.x, hz = ray.o.z + temp * ray.d.z;
-            if (__builtin_sqrtf((hx - cx) * (hx - cx) + (hz - cz) * (hz - cz)) < radius) {
+            if ((hx - cx) * (hx - cx) + (hz - cz) * (hz - cz) <= bound) {
                 tmax = temp;
                     kind = HK_FACING_Y;
                 return true;
@@ -247,9 +250,9 @@ __device__ __forceinline__ bool cylinder_test(const Node& cy, const RayK& ray, f
     const float ccx = cy.a0, ccy = cy.a1, ccz = cy.a2, r = cy.b0, height = cy.b2;
     bool ret = false;
     const float upper = ccy + height / 2;
-    if (cap_test(ccx, ccz, r, ray, tmax, kind, upper)) ret = true;
+    if (cap_test(ccx, ccz, cy.b1, ray, tmax, kind, upper)) ret = true;
     const float lower = ccy - height / 2;
-    if (cap_test(ccx, ccz, r, ray, tmax, kind, lower)) ret = true;
+    if (cap_test(ccx, ccz, cy.b1, ray, tmax, kind, lower)) ret = true;
     const float dx = ray.d.x, dz = ray.d.z;
     const float cx = ray.o.x - ccx, cz = ray.o.z - ccz;
     const float a = dx * dx + dz * dz;
@@ -493,9 +496,9 @@ __device__ __forceinline__ bool sphere_cyl_test(const Node& nd, const RayK& ray,
     float lower = 0.f, upper = 0.f;
     if (!sph) {
         upper = nd.a1 + nd.b2 / 2;
-        if (cap_test(nd.a0, nd.a2, r, ray, tmax, kind, upper)) ret = true;
+        if (cap_test(nd.a0, nd.a2, nd.b1, ray, tmax, kind, upper)) ret = true;
         lower = nd.a1 - nd.b2 / 2;
-        if (cap_test(nd.a0, nd.a2, r, ray, tmax, kind, lower)) ret = true;
+        if (cap_test(nd.a0, nd.a2, nd.b1, ray, tmax, kind, lower)) ret = true;
     }
     const float cx = ray.o.x - nd.a0, cy = ray.o.y - nd.a1, cz = ray.o.z - nd.a2;
     const float dx = ray.d.x, dy = ray.d.y, dz = ray.d.z;
@@ -760,12 +763,10 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         return (int)*top;
     };
     bool working = true;
+    // Invariant at the top of every iteration: a lane whose next ref is a leaf has a parked leaf
+    // (cur <= -2 implies parked >= 0); the node visit and the leaf round below keep it.
     for (int it = 0;; ++it) {
         stamps::count(9);
-        if (cur <= -2 && parked < 0) {
-            parked = leaf_of(cur);
-            cur = pop();
-        }
         if (cur >= 0) {
             execdiag::lanes(p.stats + 64, 1);
             if (STATS) {
@@ -808,7 +809,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
             }
         }
         working = parked >= 0 || cur != NONE;
-        const bool stopped = parked >= 0 && (cur == NONE || cur <= -2);
+        const bool stopped = parked >= 0 && cur < 0;   // at a second leaf or out of nodes
         const uint64_t w = __ballot(working);
         const bool tail = __popcll(w) <= 8;   // stamps only: the walk's tail (few lanes left)
         stamps::lap(tail ? 11 : 1);
@@ -828,6 +829,10 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
                 limit = walk_limit(tmax);
             }
             parked = -1;
+            if (cur <= -2) {   // the lane stopped at a second leaf: park it
+                parked = leaf_of(cur);
+                cur = pop();
+            }
         }
         stamps::lap(tail ? 12 : 2);
     }

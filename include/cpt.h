@@ -296,6 +296,10 @@ int cpt_reset_display(cpt_ctx* ctx);
  * the box): `iters` grid-stride 16-B-per-lane read passes over a fresh `bytes`-byte buffer
  * (use >> 256 MiB so the Infinity Cache cannot serve it), GB/s from HIP events. */
 int cpt_measure_read_bandwidth(cpt_ctx* ctx, size_t bytes, int iters, float* gbps);
+/* Host-only test hook (no GPU): the cap-disk bound a cylinder leaf carries (cpt_capi.cpp
+ * cap_disk_bound), the largest float c with  sqrtf(q) < radius  <=>  q <= c  for every float
+ * q; the kernels decide the reference's cap test (object.cu:52-77) with it. */
+int cpt_cap_disk_bound(float radius, float* out);
 /* Device-math known-answer surface used by the parity tests: op 0 powf(a,b), 1 sinf(a),
  * 2 cosf(a), 3 asinf(a), 4 atanf(a), 5 (float)pow((double)a, 1.0/(double)b),
  * 6 (float)((double)a / (double)b) [IEEE f64 division], 7 a / b [f32 division],
