@@ -170,6 +170,15 @@ Node make_node(const BNode& n, const std::vector<cpt_object>& objs, const std::v
         g.b0 = o.radius; g.b1 = o.y_pos; g.b2 = o.height;
         int type = (o.type >= 0 && o.type <= 2) ? o.type : 3;
         if (type == CPT_PRIM_CYLINDER) g.b1 = cap_disk_bound(o.radius);   // y_pos is a platform's
+        if (type == CPT_PRIM_SPHERE) {
+            // the root-1 normal's exact quotients (cpt_path.hpp hit_attributes): the correctly
+            // rounded double reciprocal of the radius, its low word in b1 and high word in b2
+            const double inv_r = 1.0 / (double)o.radius;
+            uint32_t w[2];
+            std::memcpy(w, &inv_r, 8);
+            std::memcpy(&g.b1, &w[0], 4);
+            std::memcpy(&g.b2, &w[1], 4);
+        }
         g.code = (mat_of_obj[n.obj] << 2) | type;
     } else {
         g.a0 = n.bmin.x; g.a1 = n.bmin.y; g.a2 = n.bmin.z;
@@ -1217,6 +1226,8 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     p.cam.lens_radius = cam->lens_radius;
     p.cam.width = cam->width;
     p.cam.height = cam->height;
+    p.cam.inv_w = 1.0 / (double)(float)cam->width;
+    p.cam.inv_h = 1.0 / (double)(float)cam->height;
     p.rows = c->d_rows;
     p.n_rows = c->n_rows;
     p.width = c->width;

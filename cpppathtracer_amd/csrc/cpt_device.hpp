@@ -335,13 +335,18 @@ static_assert(sizeof(Node) == 32, "Node is 32 B");
 //   rad   = emit_intensity_ * kd_ (material.cu:36,62,97,141); in a textured material kd_
 //           aliases tex_, so these are the handle's bits, as in the reference's union
 //   inv_alpha = 1.0 / (double)powf(1000, smoothness_) (material.cu:43,69,103)
-// The host stages {att = kd_ bits, rad.x = emit_intensity_} and the kernel completes it.
+//   inv_ior = 1.f / ior_, and for Glass schlick_r0 = ((1 - ior_) / (1 + ior_))^2 in the
+//   reflectivity slot (ray_tracing_math.hpp:65-67, material.cu:114-133): the shader's own
+//   quotients, computed once per material instead of once per hit
+// The host stages {att = kd_ bits, rad.x = emit_intensity_, smoothness} and the kernel
+// completes it.
 struct __attribute__((aligned(16))) Mat {
     float att_x, att_y, att_z;
     int32_t type;
     float rad_x, rad_y, rad_z;
     float ior;
-    float reflectivity, smoothness;
+    union { float reflectivity; float schlick_r0; };   // Mirror: reflectivity_; Glass: r0
+    union { float smoothness; float inv_ior; };        // staged: smoothness_; prepared: 1 / ior
     double inv_alpha;
 };
 static_assert(sizeof(Mat) == 48, "Mat is 48 B");

@@ -25,6 +25,8 @@ struct CamK {
     float top_left[3], horizontal[3], vertical[3];
     float lens_radius;
     int width, height;
+    double inv_w, inv_h;   // 1.0 / (double)(float)width, height: RayGen's x / width, y / height as
+                           // exact quotients (cpt_path.hpp ray_gen)
 };
 
 // Kernel arguments (passed by value: they land in the kernarg segment and are read with

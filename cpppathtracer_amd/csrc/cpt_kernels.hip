@@ -597,6 +597,12 @@ __global__ void k_prepare_materials(Mat* mats, const int32_t* tex_of_mat, const 
     }
     float alpha = dm::powf_(1000.0f, m.smoothness);
     m.inv_alpha = 1.0 / (double)alpha;
+    m.inv_ior = 1.f / m.ior;
+    if (m.type == 3) {   // Glass (the only shader that reads r0; Mirror reads reflectivity)
+        float r0 = (1 - m.ior) / (1 + m.ior);
+        r0 *= r0;
+        m.schlick_r0 = r0;
+    }
     mats[i] = m;
 }
 

@@ -292,10 +292,18 @@ __device__ __forceinline__ Hit hit_attributes(const Node& nd, const RayK& ray, f
     Hit h;
     h.pos = ray.o + t * ray.d;
     const v3 c = mk(nd.a0, nd.a1, nd.a2);
-    if (kind == HK_SPHERE_ROOT1) h.normal = (h.pos - c) / nd.b0;
-    else if (kind == HK_SPHERE_ROOT2) h.normal = normalize(h.pos - c);
-    else if (kind == HK_CYL_SIDE) h.normal = normalize(mk(h.pos.x - c.x, 0.f, h.pos.z - c.z));
-    else h.normal = normalize(mk(0, -ray.d.y, 0));
+    const v3 pc = h.pos - c;
+    if (kind == HK_SPHERE_ROOT1) {
+        // (p - c) / radius, each component the IEEE quotient: qdiv with the sphere leaf's double
+        // reciprocal of its radius (Node::b1/b2, cpt_capi.cpp make_node)
+        const double y = __hiloint2double(__float_as_int(nd.b2), __float_as_int(nd.b1));
+        h.normal = mk(qdiv(pc.x, nd.b0, y), qdiv(pc.y, nd.b0, y), qdiv(pc.z, nd.b0, y));
+    } else {
+        // the other three cases normalize a vector of their own: one normalize for the wave
+        const bool cyl = kind == HK_CYL_SIDE, root2 = kind == HK_SPHERE_ROOT2;
+        const v3 v = mk(root2 || cyl ? pc.x : 0.f, root2 ? pc.y : (cyl ? 0.f : -ray.d.y), root2 || cyl ? pc.z : 0.f);
+        h.normal = normalize(v);
+    }
     return h;
 }
 
@@ -920,10 +928,9 @@ __device__ __forceinline__ v3 lobe(float x_1, float x_2, double inv_alpha) {
     return mk(r * cp, r * sp, z);
 }
 
-// schlick (ray_tracing_math.hpp:65-69), pow(float,int) -> float overload in device code.
-__device__ __forceinline__ float schlick(float cosine, float ref_idx) {
-    float r0 = (1 - ref_idx) / (1 + ref_idx);
-    r0 *= r0;
+// schlick (ray_tracing_math.hpp:65-69), pow(float,int) -> float overload in device code; r0 =
+// ((1 - ref_idx) / (1 + ref_idx))^2 is the material's, prepared once (Mat::schlick_r0).
+__device__ __forceinline__ float schlick(float cosine, float r0) {
     return r0 + (1 - r0) * dm::powf_(1 - cosine, 5.0f);
 }
 
@@ -977,10 +984,10 @@ __device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow&
             cosine = __builtin_sqrtf(1 - m.ior * m.ior * (1 - cosine * cosine));
         } else {
             outward = normal;
-            ni_over_nt = 1.f / m.ior;
+            ni_over_nt = m.inv_ior;   // 1.f / ior, prepared once
             cosine = -dot(in, normal);
         }
-        if (refract(in, outward, ni_over_nt, refracted)) reflect_prob = schlick(cosine, m.ior);
+        if (refract(in, outward, ni_over_nt, refracted)) reflect_prob = schlick(cosine, m.schlick_r0);
         else reflect_prob = 1.0f;
         axis = uniform(rng) < reflect_prob ? reflect(in, normal) : refracted;
     }
@@ -1008,8 +1015,10 @@ __device__ __forceinline__ Ray ray_gen(const CamK& c, int x, int y, Xorwow& rng)
     v3 u = mk(c.u[0], c.u[1], c.u[2]), v = mk(c.v[0], c.v[1], c.v[2]);
     v3 origin = mk(c.origin[0], c.origin[1], c.origin[2]);
     v3 offset = u * rd.x + v * rd.y;
-    float dx = float(x) / float(c.width);
-    float dy = float(y) / float(c.height);
+    // float(x) / float(width): for 1 <= x < width <= 2^24 the quotient is a normal float, which
+    // qdiv_raw with the double reciprocal gets exactly (cpt_device.hpp); x = 0 gives +0
+    float dx = x > 0 ? qdiv_raw(float(x), c.inv_w) : 0.f;
+    float dy = y > 0 ? qdiv_raw(float(y), c.inv_h) : 0.f;
     Ray ray;
     ray.o = origin + offset;
     v3 tl = mk(c.top_left[0], c.top_left[1], c.top_left[2]);
