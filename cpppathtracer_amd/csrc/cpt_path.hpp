@@ -107,9 +107,11 @@ __device__ inline v3 tex2d(const KParams& p, float u, float v) {
 typedef float f2v __attribute__((ext_vector_type(2)));
 
 // Margins of the ordered walk's conservative slab test (slab_pass below): relative to the
-// plane distances, and absolute (the exit offsets carry 2 x WALK_MARGIN_ABS, rounded up).
+// plane distances (folded into the per-ray reciprocals, RayK::inx ...) and absolute (the exit
+// offsets carry 2 x WALK_MARGIN_ABS, rounded up, and 1e-6 for the relative margin's rounding).
 constexpr float WALK_MARGIN_REL = 1e-3f, WALK_MARGIN_ABS = 1e-4f;
-constexpr float SLAB_ABS = 2.0f * WALK_MARGIN_ABS * (1.0f + 2.0f * WALK_MARGIN_REL);
+constexpr float SLAB_SHRINK = 1.0f - WALK_MARGIN_REL, SLAB_GROW = 1.0f + WALK_MARGIN_REL;
+constexpr float SLAB_ABS = 2.0f * WALK_MARGIN_ABS * (1.0f + 2.0f * WALK_MARGIN_REL) * SLAB_GROW + 1e-6f;
 
 struct RayK {
     v3 o, d;
@@ -118,25 +120,28 @@ struct RayK {
                          // yx and yz are filled by with_slab() where an exact slab test runs
     double ya;           // 1/dot(d,d)            (sphere roots, object.cu:15-20)
     double yc;           // 1/(dx*dx + dz*dz)     (cylinder side roots, object.cu:69-79)
-    // The ordered walk's conservative slabs (slab_reject<*, true>, wide_pair): a plane p of axis
-    // a is at t = fma(p, i_a, c_a), with i_a = f32 1/d_a and c_a = -(o_a * i_a) -+ beta_a for
-    // entry (n) and exit (f) planes; beta_a = 2^-20 |o_a * i_a| covers the rounding of the
-    // product and the sum, so an entry plane's t is never above (p - o_a) * i_a before its own
-    // rounding (DESIGN.md §Ordered walk).  The exit offsets also carry the test's absolute
-    // margin.  A skipped axis (|d| < 1e-30) has i_a = 0 and c_a = -+2e30: no constraint, which
-    // only widens.
-    float ix, iy, iz;
+    // The ordered walk's conservative slabs (slab_reject<*, true>, wide_pair, slab_pass): a plane
+    // p of axis a is entered at t = fma(p, in_a, cn_a) and left at fma(p, if_a, cf_a), with
+    // in_a = i (1 - 1e-3), if_a = i (1 + 1e-3) for the f32 i = 1/d_a (the relative margin: an
+    // entry distance shrinks toward 0 and an exit distance grows by 1e-3 of itself) and
+    // c_a = -(o_a * i_a) -+ beta_a; beta_a = 2^-20 |o_a * i_a| covers the rounding of the product
+    // and the sum, so an entry plane's t is never above (p - o_a) * in_a before its own rounding
+    // (DESIGN.md §Ordered walk).  The exit offsets also carry the absolute margin.  A skipped
+    // axis (|d| < 1e-30) has i = 0 and c = -+2e30: no constraint, which only widens.
+    float inx, iny, inz, ifx, ify, ifz;
     float nx, ny, nz;    // entry offsets
     float fx, fy, fz;    // exit offsets (+ SLAB_ABS)
-    float t3;            // conservative tmin limit: (tmin - 1e-4) * (1 + 2e-3)
+    float t3;            // conservative tmin limit: t3 - 1e-3 |t3|, t3 = (tmin - 1e-4) * (1 + 2e-3)
 };
 
-// Entry / exit offsets of one axis of the conservative slabs (RayK::ix ...).
-__device__ __forceinline__ void slab_axis(float o, float d, float& i, float& cn, float& cf) {
-    i = __builtin_fabsf(d) >= 1e-30f ? rcp_f(d) : 0.0f;
-    const float pr = o * i, beta = __builtin_fabsf(pr) * 0x1p-20f;
-    cn = i != 0.0f ? -pr - beta : -DEFAULT_RAY_TMAX * 2;
-    cf = i != 0.0f ? (-pr + beta) + SLAB_ABS : DEFAULT_RAY_TMAX * 2;
+// Entry / exit reciprocals and offsets of one axis of the conservative slabs (RayK::inx ...).
+__device__ __forceinline__ void slab_axis(float o, float d, float& in, float& if_, float& cn, float& cf) {
+    const float i = __builtin_fabsf(d) >= 1e-30f ? rcp_f(d) : 0.0f;
+    in = i * SLAB_SHRINK;
+    if_ = i * SLAB_GROW;
+    const float pn = o * in, pf = o * if_;
+    cn = i != 0.0f ? -pn - __builtin_fabsf(pn) * 0x1p-20f : -DEFAULT_RAY_TMAX * 2;
+    cf = i != 0.0f ? (-pf + __builtin_fabsf(pf) * 0x1p-20f) + SLAB_ABS : DEFAULT_RAY_TMAX * 2;
 }
 
 __device__ __forceinline__ RayK make_rayk(const Ray& r) {
@@ -149,10 +154,11 @@ __device__ __forceinline__ RayK make_rayk(const Ray& r) {
     k.yz = 0.0;
     k.ya = rcp_d(dot(r.d, r.d));
     k.yc = rcp_d(r.d.x * r.d.x + r.d.z * r.d.z);
-    slab_axis(r.o.x, r.d.x, k.ix, k.nx, k.fx);
-    slab_axis(r.o.y, r.d.y, k.iy, k.ny, k.fy);
-    slab_axis(r.o.z, r.d.z, k.iz, k.nz, k.fz);
-    k.t3 = (r.tmin - 1e-4f) * (1.0f + 2e-3f);
+    slab_axis(r.o.x, r.d.x, k.inx, k.ifx, k.nx, k.fx);
+    slab_axis(r.o.y, r.d.y, k.iny, k.ify, k.ny, k.fy);
+    slab_axis(r.o.z, r.d.z, k.inz, k.ifz, k.nz, k.fz);
+    const float t3 = (r.tmin - 1e-4f) * (1.0f + 2e-3f);
+    k.t3 = t3 - WALK_MARGIN_REL * __builtin_fabsf(t3);
     return k;
 }
 
@@ -332,35 +338,35 @@ struct Counters {
 // §Ordered walk).  The margin dwarfs the reciprocal's few-ulp error.
 // The conservative walk's tmax limit (slab_reject<*, true>'s `tmax` argument).
 __device__ __forceinline__ float walk_limit(float tmax) {
-    return (tmax + WALK_MARGIN_ABS) * (1.0f + 2.0f * WALK_MARGIN_REL);
+    return ((tmax + WALK_MARGIN_ABS) * (1.0f + 2.0f * WALK_MARGIN_REL)) * SLAB_GROW;
 }
 
-// The conservative pass test on a box's entry / exit distances lo = max over axes of the entry
-// planes' fma(p, i, c_n), hi = min of the exit planes' fma(p, i, c_f) (RayK::ix ...; hi carries
-// the absolute margin through c_f).  With lo' = max(lo, t3) and hi' = min(hi, limit) the box
-// passes iff
-//     lo' - 1e-3 |lo'|  <=  hi' + 1e-3 |hi'|.
-// It passes whenever the reference test on the exact quotients (b - o) / d passes with any
-// tmax <= the walk's: that one needs lo <= hi, lo <= tmax and hi >= tmin, and each of the four
-// choices of (lo', hi') then satisfies the inequality with the relative margin to spare for
-// the planes' few-ulp rounding (DESIGN.md §Ordered walk).  lo' is also the child's sort key.
+// The conservative pass test on a box's entry / exit distances: lo = max over axes of the
+// entry planes' fma(p, in, cn), hi = min of the exit planes' fma(p, if, cf) (RayK::inx ...,
+// which carry the relative and absolute margins); the box passes iff
+//     max(lo, t3') <= min(hi, limit')
+// with t3' = t3 - 1e-3 |t3| and limit' = walk_limit(tmax) (both widened the same way).  It
+// passes every box the round-2 test passed (reject iff lo - hi > 1e-3 (|lo| + |hi|) + 2e-4, or
+// lo > (tmax + 1e-4) * 1.002, or hi < (tmin - 1e-4) * 1.002, on unscaled distances): for the
+// distances >= 0 the scaled ones are the old ones times (1 -+ 1e-3), and the few in (t3, 0)
+// differ from that by less than the 1e-6 the exit offsets add (DESIGN.md §Ordered walk).
+// lo' = max(lo, t3') is also the child's sort key.
 __device__ __forceinline__ bool slab_pass(float& lo, float hi, float t3, float limit) {
     lo = __builtin_fmaxf(lo, t3);
-    hi = __builtin_fminf(hi, limit);
-    return __builtin_fmaf(-WALK_MARGIN_REL, __builtin_fabsf(lo), lo) <= __builtin_fmaf(WALK_MARGIN_REL, __builtin_fabsf(hi), hi);
+    return lo <= __builtin_fminf(hi, limit);
 }
 
 template <bool FAST, bool CONS = false>
 __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, float tmax) {
     if (CONS) {
         // The entry plane of an axis is its min plane when 1/d >= 0 (also on a skipped axis).
-        const bool px = ray.ix >= 0.0f, py = ray.iy >= 0.0f, pz = ray.iz >= 0.0f;
-        float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(px ? nd.a0 : nd.b0, ray.ix, ray.nx),
-                                                   __builtin_fmaf(py ? nd.a1 : nd.b1, ray.iy, ray.ny)),
-                                   __builtin_fmaf(pz ? nd.a2 : nd.b2, ray.iz, ray.nz));
-        const float hi = __builtin_fminf(__builtin_fminf(__builtin_fmaf(px ? nd.b0 : nd.a0, ray.ix, ray.fx),
-                                                         __builtin_fmaf(py ? nd.b1 : nd.a1, ray.iy, ray.fy)),
-                                         __builtin_fmaf(pz ? nd.b2 : nd.a2, ray.iz, ray.fz));
+        const bool px = ray.inx >= 0.0f, py = ray.iny >= 0.0f, pz = ray.inz >= 0.0f;
+        float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(px ? nd.a0 : nd.b0, ray.inx, ray.nx),
+                                                   __builtin_fmaf(py ? nd.a1 : nd.b1, ray.iny, ray.ny)),
+                                   __builtin_fmaf(pz ? nd.a2 : nd.b2, ray.inz, ray.nz));
+        const float hi = __builtin_fminf(__builtin_fminf(__builtin_fmaf(px ? nd.b0 : nd.a0, ray.ifx, ray.fx),
+                                                         __builtin_fmaf(py ? nd.b1 : nd.a1, ray.ify, ray.fy)),
+                                         __builtin_fmaf(pz ? nd.b2 : nd.a2, ray.ifz, ray.fz));
         return !slab_pass(lo, hi, ray.t3, tmax);
     }
     float t0x = qdiv_raw(nd.a0 - ray.o.x, ray.yx), t1x = qdiv_raw(nd.b0 - ray.o.x, ray.yx);
@@ -415,10 +421,10 @@ __device__ __forceinline__ bool slab_reject(const Node& nd, const RayK& ray, flo
 // lo and hi are bit for bit those of the min/max form and the decision is the same.
 
 __device__ __forceinline__ bool slab_reject_octant(const Node& nd, const RayK& ray, float limit) {
-    float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(nd.a0, ray.ix, ray.nx), __builtin_fmaf(nd.a1, ray.iy, ray.ny)),
-                               __builtin_fmaf(nd.a2, ray.iz, ray.nz));
-    const float hi = __builtin_fminf(__builtin_fminf(__builtin_fmaf(nd.b0, ray.ix, ray.fx), __builtin_fmaf(nd.b1, ray.iy, ray.fy)),
-                                     __builtin_fmaf(nd.b2, ray.iz, ray.fz));
+    float lo = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(nd.a0, ray.inx, ray.nx), __builtin_fmaf(nd.a1, ray.iny, ray.ny)),
+                               __builtin_fmaf(nd.a2, ray.inz, ray.nz));
+    const float hi = __builtin_fminf(__builtin_fminf(__builtin_fmaf(nd.b0, ray.ifx, ray.fx), __builtin_fmaf(nd.b1, ray.ify, ray.fy)),
+                                     __builtin_fmaf(nd.b2, ray.ifz, ray.fz));
     return !slab_pass(lo, hi, ray.t3, limit);
 }
 
@@ -678,14 +684,14 @@ __device__ __forceinline__ WideNode load_wide_node(const uint4* tree, int n_lds,
 // sort keys (slab_pass's lo').
 __device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], const RayK& ray, float limit,
                                               float& lo_a, float& lo_b) {
-    lo_a = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(e[0].x, ray.ix, ray.nx), __builtin_fmaf(e[1].x, ray.iy, ray.ny)),
-                           __builtin_fmaf(e[2].x, ray.iz, ray.nz));
-    lo_b = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(e[0].y, ray.ix, ray.nx), __builtin_fmaf(e[1].y, ray.iy, ray.ny)),
-                           __builtin_fmaf(e[2].y, ray.iz, ray.nz));
-    const float hi_a = __builtin_fminf(__builtin_fminf(__builtin_fmaf(x[0].x, ray.ix, ray.fx), __builtin_fmaf(x[1].x, ray.iy, ray.fy)),
-                                       __builtin_fmaf(x[2].x, ray.iz, ray.fz));
-    const float hi_b = __builtin_fminf(__builtin_fminf(__builtin_fmaf(x[0].y, ray.ix, ray.fx), __builtin_fmaf(x[1].y, ray.iy, ray.fy)),
-                                       __builtin_fmaf(x[2].y, ray.iz, ray.fz));
+    lo_a = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(e[0].x, ray.inx, ray.nx), __builtin_fmaf(e[1].x, ray.iny, ray.ny)),
+                           __builtin_fmaf(e[2].x, ray.inz, ray.nz));
+    lo_b = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(e[0].y, ray.inx, ray.nx), __builtin_fmaf(e[1].y, ray.iny, ray.ny)),
+                           __builtin_fmaf(e[2].y, ray.inz, ray.nz));
+    const float hi_a = __builtin_fminf(__builtin_fminf(__builtin_fmaf(x[0].x, ray.ifx, ray.fx), __builtin_fmaf(x[1].x, ray.ify, ray.fy)),
+                                       __builtin_fmaf(x[2].x, ray.ifz, ray.fz));
+    const float hi_b = __builtin_fminf(__builtin_fminf(__builtin_fmaf(x[0].y, ray.ifx, ray.fx), __builtin_fmaf(x[1].y, ray.ify, ray.fy)),
+                                       __builtin_fmaf(x[2].y, ray.ifz, ray.fz));
     const bool pa = slab_pass(lo_a, hi_a, ray.t3, limit), pb = slab_pass(lo_b, hi_b, ray.t3, limit);
     return (pa ? 1u : 0u) | (pb ? 2u : 0u);
 }

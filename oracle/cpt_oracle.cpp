@@ -908,31 +908,36 @@ bool slab_pass(const Node& n, const Ray& ray) {                 // bvh.cu:181-20
     return !(local_tmin > local_tmax || local_tmin > ray.tmax || local_tmax < ray.tmin);
 }
 
-// The product's conservative slab (cpt_path.hpp slab_reject<FAST, true> and slab_pass): f32
-// reciprocals i; a plane p is at fma(p, i, c), c = -(o * i) -+ 2^-20 |o * i| for the entry (-)
-// and exit (+, plus SLAB_ABS) plane of the axis (the entry plane is the min plane when
-// i >= 0); skipped axes for |d| < 1e-30 (i = 0, c = -+2e30).  With lo' = max(lo, t3) and
-// hi' = min(hi, (tmax + 1e-4) * 1.002), t3 = (tmin - 1e-4) * 1.002, the box passes iff
-// lo' - 1e-3 |lo'| <= hi' + 1e-3 |hi'|.
+// The product's conservative slab (cpt_path.hpp slab_reject<FAST, true>, slab_pass, RayK): f32
+// reciprocals i = 1/d, scaled to in = i (1 - 1e-3) for entry planes and if = i (1 + 1e-3) for
+// exit planes; a plane p is entered at fma(p, in, cn) and left at fma(p, if, cf), with
+// cn = -(o in) - 2^-20 |o in| and cf = (-(o if) + 2^-20 |o if|) + SLAB_ABS (the entry plane is
+// the min plane when i >= 0); skipped axes for |d| < 1e-30 (i = 0, c = -+2e30).  The box
+// passes iff max(lo, t3') <= min(hi, limit'), t3' = t3 - 1e-3 |t3| with
+// t3 = (tmin - 1e-4) * 1.002, limit' = ((tmax + 1e-4) * 1.002) * 1.001.
 bool slab_pass_conservative(const Bvh::WNode& n, const Ray& ray) {
     const float BIG = DEFAULT_RAY_TMAX * 2;
-    const float REL = 1e-3f, ABS = 1e-4f, SLAB_ABS = 2.0f * ABS * (1.0f + 2.0f * REL);
+    const float REL = 1e-3f, ABS = 1e-4f, SHRINK = 1.0f - REL, GROW = 1.0f + REL;
+    const float SLAB_ABS = 2.0f * ABS * (1.0f + 2.0f * REL) * GROW + 1e-6f;
     const float o[3] = {ray.origin.x, ray.origin.y, ray.origin.z}, d[3] = {ray.dir.x, ray.dir.y, ray.dir.z};
     const float a[3] = {n.bmin.x, n.bmin.y, n.bmin.z}, b[3] = {n.bmax.x, n.bmax.y, n.bmax.z};
     float l[3], h[3];
     for (int k = 0; k < 3; ++k) {
         const float inv = fabsf(d[k]) >= 1e-30f ? 1.0f / d[k] : 0.0f;
-        const float pr = o[k] * inv, beta = fabsf(pr) * 0x1p-20f;
-        const float cn = inv != 0.0f ? -pr - beta : -BIG, cf = inv != 0.0f ? (-pr + beta) + SLAB_ABS : BIG;
-        const bool pos = inv >= 0.0f;
-        l[k] = fmaf(pos ? a[k] : b[k], inv, cn);
-        h[k] = fmaf(pos ? b[k] : a[k], inv, cf);
+        const float in = inv * SHRINK, ig = inv * GROW;
+        const float pn = o[k] * in, pf = o[k] * ig;
+        const float cn = inv != 0.0f ? -pn - fabsf(pn) * 0x1p-20f : -BIG;
+        const float cf = inv != 0.0f ? (-pf + fabsf(pf) * 0x1p-20f) + SLAB_ABS : BIG;
+        const bool pos = in >= 0.0f;
+        l[k] = fmaf(pos ? a[k] : b[k], in, cn);
+        h[k] = fmaf(pos ? b[k] : a[k], ig, cf);
     }
-    const float tlim = (ray.tmax + ABS) * (1.0f + 2.0f * REL);
-    const float t3 = (ray.tmin - 1e-4f) * (1.0f + 2e-3f);
+    const float tlim = ((ray.tmax + ABS) * (1.0f + 2.0f * REL)) * GROW;
+    const float t3r = (ray.tmin - 1e-4f) * (1.0f + 2e-3f);
+    const float t3 = t3r - REL * fabsf(t3r);
     const float lo = fmaxf(fmaxf(fmaxf(l[0], l[1]), l[2]), t3);
-    const float hi = fminf(fminf(fminf(h[0], h[1]), h[2]), tlim);
-    return fmaf(-REL, fabsf(lo), lo) <= fmaf(REL, fabsf(hi), hi);
+    const float hi = fminf(fminf(h[0], h[1]), h[2]);
+    return lo <= fminf(hi, tlim);
 }
 
 bool trace_ray_ordered(const Bvh& bvh, Ray ray, Attr& attr, int& hit_obj, Stats& st) {
