@@ -58,7 +58,8 @@ constexpr double REF_PI = 3.14159265358979323846;
 
 // ------------------------------------------------------------------------------------
 // Deterministic transcendentals.  Double-precision sequences with
-// explicit constants; no FMA contraction.  Identical sequences live in the CPU oracle.
+// explicit constants and explicit fused multiply-adds (no other contraction).  Identical
+// sequences live in the CPU oracle (std::fma).
 // ------------------------------------------------------------------------------------
 namespace dm {
 
@@ -71,6 +72,13 @@ constexpr double PIO2_2 = 6.07710050650619224932e-11;
 constexpr double PIO2_3 = 2.02226624879595063154e-21;
 constexpr double TWO_OVER_PI = 6.36619772367581382433e-01;
 constexpr double PI_2_D = 1.57079632679489655800e+00;
+
+// A double constant materialised in SGPRs where it is used (the empty asm hides its value), so
+// the compiler cannot hoist the polynomials' constants out of the persistent loop into VGPRs.
+__device__ __forceinline__ double kc(double c) {
+    asm volatile("" : "+s"(c));
+    return c;
+}
 
 __device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
 __device__ __forceinline__ double bitsd(uint64_t u) { return __longlong_as_double((long long)u); }
@@ -91,20 +99,20 @@ __device__ inline double log_pos(double x) {
     double s = f / (2.0 + f);
     double s2 = s * s;
     double p = 1.0 / 25.0;
-    p = 1.0 / 23.0 + s2 * p;
-    p = 1.0 / 21.0 + s2 * p;
-    p = 1.0 / 19.0 + s2 * p;
-    p = 1.0 / 17.0 + s2 * p;
-    p = 1.0 / 15.0 + s2 * p;
-    p = 1.0 / 13.0 + s2 * p;
-    p = 1.0 / 11.0 + s2 * p;
-    p = 1.0 / 9.0 + s2 * p;
-    p = 1.0 / 7.0 + s2 * p;
-    p = 1.0 / 5.0 + s2 * p;
-    p = 1.0 / 3.0 + s2 * p;
-    double r = 2.0 * s + 2.0 * s * (s2 * p);
+    p = __builtin_fma(s2, p, kc(1.0 / 23.0));
+    p = __builtin_fma(s2, p, kc(1.0 / 21.0));
+    p = __builtin_fma(s2, p, kc(1.0 / 19.0));
+    p = __builtin_fma(s2, p, kc(1.0 / 17.0));
+    p = __builtin_fma(s2, p, kc(1.0 / 15.0));
+    p = __builtin_fma(s2, p, kc(1.0 / 13.0));
+    p = __builtin_fma(s2, p, kc(1.0 / 11.0));
+    p = __builtin_fma(s2, p, kc(1.0 / 9.0));
+    p = __builtin_fma(s2, p, kc(1.0 / 7.0));
+    p = __builtin_fma(s2, p, kc(1.0 / 5.0));
+    p = __builtin_fma(s2, p, kc(1.0 / 3.0));
+    double r = __builtin_fma(2.0 * s, s2 * p, 2.0 * s);
     double de = (double)e;
-    return de * LN2_HI + (r + de * LN2_LO);
+    return __builtin_fma(de, kc(LN2_HI), __builtin_fma(de, kc(LN2_LO), r));
 }
 
 __device__ inline double log(double x) {
@@ -123,22 +131,22 @@ __device__ inline double exp(double x) {
     if (x != x) return x;
     if (x > 709.782712893384) return __builtin_inf();
     if (x < -745.1332191019412) return 0.0;
-    double k = __builtin_floor(x * INV_LN2 + 0.5);
-    double r = (x - k * LN2_HI) - k * LN2_LO;
+    double k = __builtin_floor(__builtin_fma(x, kc(INV_LN2), 0.5));
+    double r = __builtin_fma(-k, kc(LN2_LO), __builtin_fma(-k, kc(LN2_HI), x));
     double p = 1.0 / 6227020800.0;
-    p = 1.0 / 479001600.0 + r * p;
-    p = 1.0 / 39916800.0 + r * p;
-    p = 1.0 / 3628800.0 + r * p;
-    p = 1.0 / 362880.0 + r * p;
-    p = 1.0 / 40320.0 + r * p;
-    p = 1.0 / 5040.0 + r * p;
-    p = 1.0 / 720.0 + r * p;
-    p = 1.0 / 120.0 + r * p;
-    p = 1.0 / 24.0 + r * p;
-    p = 1.0 / 6.0 + r * p;
-    p = 0.5 + r * p;
-    p = 1.0 + r * p;
-    p = 1.0 + r * p;
+    p = __builtin_fma(r, p, kc(1.0 / 479001600.0));
+    p = __builtin_fma(r, p, kc(1.0 / 39916800.0));
+    p = __builtin_fma(r, p, kc(1.0 / 3628800.0));
+    p = __builtin_fma(r, p, kc(1.0 / 362880.0));
+    p = __builtin_fma(r, p, kc(1.0 / 40320.0));
+    p = __builtin_fma(r, p, kc(1.0 / 5040.0));
+    p = __builtin_fma(r, p, kc(1.0 / 720.0));
+    p = __builtin_fma(r, p, kc(1.0 / 120.0));
+    p = __builtin_fma(r, p, kc(1.0 / 24.0));
+    p = __builtin_fma(r, p, kc(1.0 / 6.0));
+    p = __builtin_fma(r, p, kc(0.5));
+    p = __builtin_fma(r, p, kc(1.0));
+    p = __builtin_fma(r, p, kc(1.0));
     return ldexp_(p, (int)k);
 }
 
@@ -163,35 +171,35 @@ __device__ __forceinline__ float powf_(float x, float y) { return (float)pow((do
 __device__ inline double sin_poly(double r) {
     double r2 = r * r;
     double p = -1.0 / 121645100408832000.0;
-    p = 1.0 / 355687428096000.0 + r2 * p;
-    p = -1.0 / 1307674368000.0 + r2 * p;
-    p = 1.0 / 6227020800.0 + r2 * p;
-    p = -1.0 / 39916800.0 + r2 * p;
-    p = 1.0 / 362880.0 + r2 * p;
-    p = -1.0 / 5040.0 + r2 * p;
-    p = 1.0 / 120.0 + r2 * p;
-    p = -1.0 / 6.0 + r2 * p;
-    return r + r * (r2 * p);
+    p = __builtin_fma(r2, p, kc(1.0 / 355687428096000.0));
+    p = __builtin_fma(r2, p, kc(-1.0 / 1307674368000.0));
+    p = __builtin_fma(r2, p, kc(1.0 / 6227020800.0));
+    p = __builtin_fma(r2, p, kc(-1.0 / 39916800.0));
+    p = __builtin_fma(r2, p, kc(1.0 / 362880.0));
+    p = __builtin_fma(r2, p, kc(-1.0 / 5040.0));
+    p = __builtin_fma(r2, p, kc(1.0 / 120.0));
+    p = __builtin_fma(r2, p, kc(-1.0 / 6.0));
+    return __builtin_fma(r, r2 * p, r);
 }
 
 __device__ inline double cos_poly(double r) {
     double r2 = r * r;
     double p = 1.0 / 2432902008176640000.0;
-    p = -1.0 / 6402373705728000.0 + r2 * p;
-    p = 1.0 / 20922789888000.0 + r2 * p;
-    p = -1.0 / 87178291200.0 + r2 * p;
-    p = 1.0 / 479001600.0 + r2 * p;
-    p = -1.0 / 3628800.0 + r2 * p;
-    p = 1.0 / 40320.0 + r2 * p;
-    p = -1.0 / 720.0 + r2 * p;
-    p = 1.0 / 24.0 + r2 * p;
-    p = -0.5 + r2 * p;
-    return 1.0 + r2 * p;
+    p = __builtin_fma(r2, p, kc(-1.0 / 6402373705728000.0));
+    p = __builtin_fma(r2, p, kc(1.0 / 20922789888000.0));
+    p = __builtin_fma(r2, p, kc(-1.0 / 87178291200.0));
+    p = __builtin_fma(r2, p, kc(1.0 / 479001600.0));
+    p = __builtin_fma(r2, p, kc(-1.0 / 3628800.0));
+    p = __builtin_fma(r2, p, kc(1.0 / 40320.0));
+    p = __builtin_fma(r2, p, kc(-1.0 / 720.0));
+    p = __builtin_fma(r2, p, kc(1.0 / 24.0));
+    p = __builtin_fma(r2, p, kc(-0.5));
+    return __builtin_fma(r2, p, 1.0);
 }
 
 __device__ __forceinline__ double reduce(double x, int* q) {
-    double k = __builtin_floor(x * TWO_OVER_PI + 0.5);
-    double r = ((x - k * PIO2_1) - k * PIO2_2) - k * PIO2_3;
+    double k = __builtin_floor(__builtin_fma(x, kc(TWO_OVER_PI), 0.5));
+    double r = __builtin_fma(-k, kc(PIO2_3), __builtin_fma(-k, kc(PIO2_2), __builtin_fma(-k, kc(PIO2_1), x)));
     double km = k - 4.0 * __builtin_floor(k * 0.25);
     *q = (int)km;
     return r;
@@ -247,9 +255,9 @@ __device__ inline double atan(double t) {
     const double lo = r1 ? ATAN_LO0 : r2 ? ATAN_LO1 : r3 ? ATAN_LO2 : ATAN_LO3;
     const double x = num / den;
     const double z = x * x, w = z * z;
-    const double s1 = z * (AT0 + w * (AT2 + w * (AT4 + w * (AT6 + w * (AT8 + w * AT10)))));
-    const double s2 = w * (AT1 + w * (AT3 + w * (AT5 + w * (AT7 + w * AT9))));
-    const double r = r0 ? x - x * (s1 + s2) : hi - ((x * (s1 + s2) - lo) - x);
+    const double s1 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, kc(AT10), kc(AT8)), kc(AT6)), kc(AT4)), kc(AT2)), kc(AT0));
+    const double s2 = w * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, kc(AT9), kc(AT7)), kc(AT5)), kc(AT3)), kc(AT1));
+    const double r = r0 ? __builtin_fma(-x, s1 + s2, x) : hi - (__builtin_fma(x, s1 + s2, -lo) - x);
     return sgn * r;
 }
 

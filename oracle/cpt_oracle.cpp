@@ -107,7 +107,8 @@ inline f3 reflect(f3 i, f3 n) { return sub(i, mul(mul(2.0f, n), dot(n, i))); }  
 // ray_tracing_math.hpp:68).  libdevice is not available, so the reference semantics are
 // defined here as: evaluate in double with these exact operation sequences (error well
 // under 1e-15 relative), then round as the C++ expression does.  The HIP kernels implement
-// the identical sequences; with FMA contraction off on both sides the results are equal
+// the identical sequences: the polynomial steps are explicit fused multiply-adds (std::fma
+// here, v_fma_f64 there) and FMA contraction is off everywhere else, so the results are equal
 // bit for bit.  Accuracy vs glibc is checked by tests/test_oracle_math.py.
 // ---------------------------------------------------------------------------------------
 inline uint64_t dbits(double x) { uint64_t u; std::memcpy(&u, &x, 8); return u; }
@@ -139,20 +140,20 @@ double dm_log(double x) {
     double s2 = s * s;
     // 2*atanh(s) = 2s(1 + s2/3 + s2^2/5 + ...), |s| <= 0.1716, 12 terms
     double p = 1.0 / 25.0;
-    p = 1.0 / 23.0 + s2 * p;
-    p = 1.0 / 21.0 + s2 * p;
-    p = 1.0 / 19.0 + s2 * p;
-    p = 1.0 / 17.0 + s2 * p;
-    p = 1.0 / 15.0 + s2 * p;
-    p = 1.0 / 13.0 + s2 * p;
-    p = 1.0 / 11.0 + s2 * p;
-    p = 1.0 / 9.0 + s2 * p;
-    p = 1.0 / 7.0 + s2 * p;
-    p = 1.0 / 5.0 + s2 * p;
-    p = 1.0 / 3.0 + s2 * p;
-    double r = 2.0 * s + 2.0 * s * (s2 * p);
+    p = std::fma(s2, p, 1.0 / 23.0);
+    p = std::fma(s2, p, 1.0 / 21.0);
+    p = std::fma(s2, p, 1.0 / 19.0);
+    p = std::fma(s2, p, 1.0 / 17.0);
+    p = std::fma(s2, p, 1.0 / 15.0);
+    p = std::fma(s2, p, 1.0 / 13.0);
+    p = std::fma(s2, p, 1.0 / 11.0);
+    p = std::fma(s2, p, 1.0 / 9.0);
+    p = std::fma(s2, p, 1.0 / 7.0);
+    p = std::fma(s2, p, 1.0 / 5.0);
+    p = std::fma(s2, p, 1.0 / 3.0);
+    double r = std::fma(2.0 * s, s2 * p, 2.0 * s);
     double de = (double)e;
-    return de * LN2_HI + (r + de * LN2_LO);
+    return std::fma(de, LN2_HI, std::fma(de, LN2_LO, r));
 }
 
 double dm_ldexp(double x, int k) {
@@ -167,23 +168,23 @@ double dm_exp(double x) {
     if (x != x) return x;
     if (x > 709.782712893384) return INFINITY;
     if (x < -745.1332191019412) return 0.0;
-    double k = floor(x * INV_LN2 + 0.5);
-    double r = (x - k * LN2_HI) - k * LN2_LO;   // |r| <= 0.3466
+    double k = floor(std::fma(x, INV_LN2, 0.5));
+    double r = std::fma(-k, LN2_LO, std::fma(-k, LN2_HI, x));   // |r| <= 0.3466
     // Taylor to r^13
     double p = 1.0 / 6227020800.0;              // 1/13!
-    p = 1.0 / 479001600.0 + r * p;              // 1/12!
-    p = 1.0 / 39916800.0 + r * p;
-    p = 1.0 / 3628800.0 + r * p;
-    p = 1.0 / 362880.0 + r * p;
-    p = 1.0 / 40320.0 + r * p;
-    p = 1.0 / 5040.0 + r * p;
-    p = 1.0 / 720.0 + r * p;
-    p = 1.0 / 120.0 + r * p;
-    p = 1.0 / 24.0 + r * p;
-    p = 1.0 / 6.0 + r * p;
-    p = 0.5 + r * p;
-    p = 1.0 + r * p;
-    p = 1.0 + r * p;
+    p = std::fma(r, p, 1.0 / 479001600.0);              // 1/12!
+    p = std::fma(r, p, 1.0 / 39916800.0);
+    p = std::fma(r, p, 1.0 / 3628800.0);
+    p = std::fma(r, p, 1.0 / 362880.0);
+    p = std::fma(r, p, 1.0 / 40320.0);
+    p = std::fma(r, p, 1.0 / 5040.0);
+    p = std::fma(r, p, 1.0 / 720.0);
+    p = std::fma(r, p, 1.0 / 120.0);
+    p = std::fma(r, p, 1.0 / 24.0);
+    p = std::fma(r, p, 1.0 / 6.0);
+    p = std::fma(r, p, 0.5);
+    p = std::fma(r, p, 1.0);
+    p = std::fma(r, p, 1.0);
     return dm_ldexp(p, (int)k);
 }
 
@@ -215,36 +216,36 @@ const double TWO_OVER_PI = 6.36619772367581382433e-01;
 double dm_sin_poly(double r) {   // |r| <= pi/4, Taylor to r^19
     double r2 = r * r;
     double p = -1.0 / 121645100408832000.0;     // -1/19!
-    p = 1.0 / 355687428096000.0 + r2 * p;       // 1/17!
-    p = -1.0 / 1307674368000.0 + r2 * p;        // -1/15!
-    p = 1.0 / 6227020800.0 + r2 * p;            // 1/13!
-    p = -1.0 / 39916800.0 + r2 * p;             // -1/11!
-    p = 1.0 / 362880.0 + r2 * p;
-    p = -1.0 / 5040.0 + r2 * p;
-    p = 1.0 / 120.0 + r2 * p;
-    p = -1.0 / 6.0 + r2 * p;
-    return r + r * (r2 * p);
+    p = std::fma(r2, p, 1.0 / 355687428096000.0);       // 1/17!
+    p = std::fma(r2, p, -1.0 / 1307674368000.0);        // -1/15!
+    p = std::fma(r2, p, 1.0 / 6227020800.0);            // 1/13!
+    p = std::fma(r2, p, -1.0 / 39916800.0);             // -1/11!
+    p = std::fma(r2, p, 1.0 / 362880.0);
+    p = std::fma(r2, p, -1.0 / 5040.0);
+    p = std::fma(r2, p, 1.0 / 120.0);
+    p = std::fma(r2, p, -1.0 / 6.0);
+    return std::fma(r, r2 * p, r);
 }
 
 double dm_cos_poly(double r) {   // |r| <= pi/4, Taylor to r^20
     double r2 = r * r;
     double p = 1.0 / 2432902008176640000.0;     // 1/20!
-    p = -1.0 / 6402373705728000.0 + r2 * p;     // -1/18!
-    p = 1.0 / 20922789888000.0 + r2 * p;        // 1/16!
-    p = -1.0 / 87178291200.0 + r2 * p;          // -1/14!
-    p = 1.0 / 479001600.0 + r2 * p;             // 1/12!
-    p = -1.0 / 3628800.0 + r2 * p;
-    p = 1.0 / 40320.0 + r2 * p;
-    p = -1.0 / 720.0 + r2 * p;
-    p = 1.0 / 24.0 + r2 * p;
-    p = -0.5 + r2 * p;
-    return 1.0 + r2 * p;
+    p = std::fma(r2, p, -1.0 / 6402373705728000.0);     // -1/18!
+    p = std::fma(r2, p, 1.0 / 20922789888000.0);        // 1/16!
+    p = std::fma(r2, p, -1.0 / 87178291200.0);          // -1/14!
+    p = std::fma(r2, p, 1.0 / 479001600.0);             // 1/12!
+    p = std::fma(r2, p, -1.0 / 3628800.0);
+    p = std::fma(r2, p, 1.0 / 40320.0);
+    p = std::fma(r2, p, -1.0 / 720.0);
+    p = std::fma(r2, p, 1.0 / 24.0);
+    p = std::fma(r2, p, -0.5);
+    return std::fma(r2, p, 1.0);
 }
 
 // Shared range reduction; returns quadrant in *q.
 double dm_reduce(double x, int* q) {
-    double k = floor(x * TWO_OVER_PI + 0.5);
-    double r = ((x - k * PIO2_1) - k * PIO2_2) - k * PIO2_3;
+    double k = floor(std::fma(x, TWO_OVER_PI, 0.5));
+    double r = std::fma(-k, PIO2_3, std::fma(-k, PIO2_2, std::fma(-k, PIO2_1, x)));
     double km = k - 4.0 * floor(k * 0.25);     // k mod 4 in [0,4)
     *q = (int)km;
     return r;
@@ -310,9 +311,9 @@ double dm_atan(double t) {
     const double lo = r1 ? ATAN_LO0 : r2 ? ATAN_LO1 : r3 ? ATAN_LO2 : ATAN_LO3;
     const double x = num / den;
     const double z = x * x, w = z * z;
-    const double s1 = z * (AT0 + w * (AT2 + w * (AT4 + w * (AT6 + w * (AT8 + w * AT10)))));
-    const double s2 = w * (AT1 + w * (AT3 + w * (AT5 + w * (AT7 + w * AT9))));
-    const double r = r0 ? x - x * (s1 + s2) : hi - ((x * (s1 + s2) - lo) - x);
+    const double s1 = z * std::fma(w, std::fma(w, std::fma(w, std::fma(w, std::fma(w, AT10, AT8), AT6), AT4), AT2), AT0);
+    const double s2 = w * std::fma(w, std::fma(w, std::fma(w, std::fma(w, AT9, AT7), AT5), AT3), AT1);
+    const double r = r0 ? std::fma(-x, s1 + s2, x) : hi - (std::fma(x, s1 + s2, -lo) - x);
     return sgn * r;
 }
 
