@@ -168,6 +168,15 @@ __device__ inline double pow(double x, double y) {
 
 __device__ __forceinline__ float powf_(float x, float y) { return (float)pow((double)x, (double)y); }
 
+// pow(x, 5) of schlick (ray_tracing_math.hpp:68, the integer exponent): x^2 is exact in double,
+// then two rounded products -- a few ulps of double from the exact power, like pow's exp(5 log x),
+// at a fraction of its cost.  The oracle's dm_pow5f is the same three products.
+__device__ __forceinline__ float pow5f(float xf) {
+    const double x = (double)xf;
+    const double x2 = x * x;
+    return (float)(x2 * x2 * x);
+}
+
 __device__ inline double sin_poly(double r) {
     double r2 = r * r;
     double p = -1.0 / 121645100408832000.0;

@@ -823,6 +823,7 @@ __global__ void k_math_batch(int op, const float* a, const float* b, float* out,
         case 6: r = (float)((double)x / (double)y); break;
         case 7: r = x / y; break;
         case 8: r = __builtin_sqrtf(x); break;
+        case 9: r = dm::pow5f(x); break;
         default: r = __builtin_nanf("");
     }
     out[i] = r;

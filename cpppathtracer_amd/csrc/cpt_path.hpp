@@ -934,10 +934,11 @@ __device__ __forceinline__ v3 lobe(float x_1, float x_2, double inv_alpha) {
     return mk(r * cp, r * sp, z);
 }
 
-// schlick (ray_tracing_math.hpp:65-69), pow(float,int) -> float overload in device code; r0 =
-// ((1 - ref_idx) / (1 + ref_idx))^2 is the material's, prepared once (Mat::schlick_r0).
+// schlick (ray_tracing_math.hpp:65-69), pow(float,int) -> float overload in device code, as
+// dm::pow5f; r0 = ((1 - ref_idx) / (1 + ref_idx))^2 is the material's, prepared once
+// (Mat::schlick_r0).
 __device__ __forceinline__ float schlick(float cosine, float r0) {
-    return r0 + (1 - r0) * dm::powf_(1 - cosine, 5.0f);
+    return r0 + (1 - r0) * dm::pow5f(1 - cosine);
 }
 
 // refract (ray_tracing_math.hpp:71-80), discriminant through double (1.0 literal).

@@ -303,7 +303,7 @@ int cpt_cap_disk_bound(float radius, float* out);
 /* Device-math known-answer surface used by the parity tests: op 0 powf(a,b), 1 sinf(a),
  * 2 cosf(a), 3 asinf(a), 4 atanf(a), 5 (float)pow((double)a, 1.0/(double)b),
  * 6 (float)((double)a / (double)b) [IEEE f64 division], 7 a / b [f32 division],
- * 8 sqrtf(a). */
+ * 8 sqrtf(a), 9 pow(a, 5) as schlick computes it (dm::pow5f). */
 int cpt_math_batch(cpt_ctx* ctx, int op, const float* a, const float* b, float* out, size_t n);
 /* Device self-test of the exact-quotient kernel helper against the hardware IEEE f32 divide
  * over n hashed operand pairs (which: 0 all bit patterns, 1 slab-like ranges, 2 mid ranges).

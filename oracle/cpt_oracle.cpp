@@ -207,6 +207,14 @@ double dm_pow(double x, double y) {
 
 float dm_powf(float x, float y) { return (float)dm_pow((double)x, (double)y); }
 
+// pow(x, 5) of schlick (ray_tracing_math.hpp:68, an integer exponent): x^2 exact in double, then
+// two rounded products; the device's dm::pow5f is the same sequence.
+float dm_pow5f(float xf) {
+    const double x = (double)xf;
+    const double x2 = x * x;
+    return (float)(x2 * x2 * x);
+}
+
 // pi/2 split (fdlibm constants): PIO2_1 has 33 significant bits.
 const double PIO2_1 = 1.57079632673412561417e+00;
 const double PIO2_2 = 6.07710050650619224932e-11;
@@ -1023,7 +1031,7 @@ f3 to_world(f3 a, f3 N) {
 float schlick(float cosine, float ref_idx) {
     float r0 = (1 - ref_idx) / (1 + ref_idx);
     r0 *= r0;
-    return r0 + (1 - r0) * dm_powf(1 - cosine, 5.0f);
+    return r0 + (1 - r0) * dm_pow5f(1 - cosine);
 }
 
 // refract (ray_tracing_math.hpp:71-80): discriminant in double (1.0 literal), stored float.
@@ -1339,6 +1347,7 @@ void or_math_batch(int op, const float* a, const float* b, float* out, long n) {
             case 3: out[i] = dm_asinf(a[i]); break;
             case 4: out[i] = dm_atanf(a[i]); break;
             case 5: out[i] = (float)dm_pow((double)a[i], 1.0 / (double)b[i]); break;
+            case 9: out[i] = dm_pow5f(a[i]); break;
             default: out[i] = NAN;
         }
     }

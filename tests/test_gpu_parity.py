@@ -29,6 +29,14 @@ def test_unary_math_bitexact(gpu, oracle_mod, op):
     np.testing.assert_array_equal(g.view(np.uint32), o.view(np.uint32))
 
 
+def test_pow5_bitexact(gpu, oracle_mod):
+    # schlick's (1 - cosine)^5 (op 9): GPU and oracle evaluate the same three double products
+    x = np.concatenate([(RNG.random(400000) * 2).astype(np.float32),
+                        ((RNG.random(100000) - 0.5) * 1e3).astype(np.float32),
+                        np.array([0, -0.0, 1, 2, 1e-30, 1e-45, np.inf, -np.inf, np.nan, 3.4e38], np.float32)])
+    np.testing.assert_array_equal(gpu.math_batch(9, x).view(np.uint32), oracle_mod.math_batch(9, x).view(np.uint32))
+
+
 @pytest.mark.parametrize("op", [0, 5])
 def test_binary_pow_bitexact(gpu, oracle_mod, op):
     a = np.concatenate([RNG.random(200000).astype(np.float32) + np.float32(2 ** -33),

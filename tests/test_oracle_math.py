@@ -75,3 +75,13 @@ def test_powf(oracle_mod):
 def test_pow_special(oracle_mod, x, y, want):
     assert oracle_mod.lib().or_pow(x, y) == pytest.approx(want, rel=1e-15, abs=0)
     assert np.isnan(oracle_mod.lib().or_pow(-2.0, 0.5))
+
+
+def test_pow5_schlick(oracle_mod):
+    # (1 - cosine)^5 in schlick (ray_tracing_math.hpp:68): cosine in [-1, 1], and the specials
+    x = (RNG.random(200000) * 2).astype(np.float32)
+    _check(oracle_mod.math_batch(9, x), np.power(x.astype(np.float64), 5))
+    edge = np.array([0.0, 1.0, 2.0, 1e-30, 3e7, np.inf], np.float32)
+    with np.errstate(over="ignore"):
+        np.testing.assert_array_equal(oracle_mod.math_batch(9, edge), np.power(edge.astype(np.float64), 5).astype(np.float32))
+    assert np.isnan(oracle_mod.math_batch(9, np.array([np.nan], np.float32))).all()
