@@ -374,8 +374,10 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             {
                 const bool ends = !hit || !(depth + 1 < max_depth);
                 const bool need_now = (pend && ends) || (!hit && L.left == 1);
+                // (32-bit scalar counts: SALU compares, cpt_path.hpp wave_count)
                 const bool flush = DEFER_MISS_ROUND == 0 || retiring || __ballot(need_now) != 0 ||
-                                   __popcll(__ballot(pend || !hit)) * 64 >= DEFER_MISS_ROUND * __popcll(__ballot(1));
+                                   wave_count(__ballot(pend || !hit)) * 64u >=
+                                       (uint32_t)DEFER_MISS_ROUND * wave_count(__builtin_amdgcn_read_exec());
                 if (flush) {
                     // One sky fetch per lane that needs one: the pending (older) direction, else
                     // this miss.  A lane holding both fetches the pending one here; its new miss

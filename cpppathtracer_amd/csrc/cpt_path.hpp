@@ -624,6 +624,13 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
 // ======================================================================================
 constexpr int WIDE_LANES = 256;   // block size of the kernels without the LDS image
 
+// Number of set bits of a wave-uniform mask as a 32-bit value (two 32-bit popcounts: the
+// compiler then compares it with SALU s_cmp_*_u32; a 64-bit popcount it compares with VALU
+// v_cmp_*_u64).  (Not inline asm: s_bcnt1 writes SCC, which an asm statement cannot declare.)
+__device__ __forceinline__ uint32_t wave_count(uint64_t m) {
+    return (uint32_t)__builtin_popcount((uint32_t)m) + (uint32_t)__builtin_popcount((uint32_t)(m >> 32));
+}
+
 typedef __attribute__((address_space(3))) int16_t lds_i16;
 
 // The compact image's first LDS_TREE_NODES nodes are staged in LDS (k_megakernel<..., LDST>,
@@ -667,9 +674,16 @@ template <bool HYB>
 __device__ __forceinline__ WideNode load_wide_node(const uint4* tree, int n_lds, __amdgpu_buffer_rsrc_t rsrc,
                                                    uint32_t image_off, int cur, int sx, int sy, int sz) {
     if (!HYB || __builtin_expect(cur < n_lds, 1)) {
-        // cur < 2^15: a 24-bit multiply (full rate; v_mul_lo_u32 is quarter rate)
-        const uint4* q = (const uint4*)((const char*)tree + __umul24((uint32_t)cur, 112u));
-        return wide_node([&](int k) { return q[k]; }, sx, sy, sz);
+        // cur < 2^15: a 24-bit multiply-add (full rate; v_mul_lo_u32 is quarter rate, and the
+        // compiler turns __umul24 of a value it cannot bound back into one)
+        // (`tree` is the block's LDS copy: its LDS address is 32 bits)
+        typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(3))) const v4u_t lds_v4u;
+        typedef __attribute__((address_space(3))) const uint4 lds_u4;
+        uint32_t a;
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(a) : "v"(cur), "s"(112u), "v"((uint32_t)(uintptr_t)(lds_u4*)tree));
+        lds_v4u* const q = (lds_v4u*)(uintptr_t)a;
+        return wide_node([&](int k) { const v4u_t v = q[k]; return make_uint4(v.x, v.y, v.z, v.w); }, sx, sy, sz);
     }
     const uint32_t off = image_off + (uint32_t)cur * 112u;
     return wide_node(
@@ -776,7 +790,6 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         top -= BLK;
         return (int)*top;
     };
-    bool working = true;
     // Invariant at the top of every iteration: a lane whose next ref is a leaf has a parked leaf
     // (cur <= -2 implies parked >= 0); the node visit and the leaf round below keep it.
     for (int it = 0;; ++it) {
@@ -813,7 +826,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
 #pragma unroll
             for (int k = 3; k >= 0; --k) {
                 *top = (int16_t)n.ref[k];
-                top += ((pm >> k) & 1u) * BLK;
+                top += __builtin_amdgcn_ubfe(pm, (uint32_t)k, 1u) * BLK;
             }
             const uint32_t word = (bk & 2) ? n.r23 : n.r01;
             cur = m == 0 ? pop() : (int)(int16_t)(word >> ((bk & 1) << 4));
@@ -822,15 +835,22 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
                 cur = pop();
             }
         }
-        working = parked >= 0 || cur != NONE;
-        const bool stopped = parked >= 0 && cur < 0;   // at a second leaf or out of nodes
-        const uint64_t w = __ballot(working);
-        const bool tail = __popcll(w) <= 8;   // stamps only: the walk's tail (few lanes left)
+        // (one ballot per compare, combined as masks: a ballot of anything but a single compare
+        // -- __ballot's int argument, a named bool, an || -- is materialised in a VGPR and
+        // compared back into a mask)
+        const uint64_t has_parked = __builtin_amdgcn_ballot_w64(parked >= 0);
+        const uint64_t w = has_parked | __builtin_amdgcn_ballot_w64(cur != NONE);
+        const uint64_t stopped = has_parked & __builtin_amdgcn_ballot_w64(cur < 0);   // at a second leaf or out of nodes
+        // wave-uniform counts as 32-bit SGPR values: SALU compares (the compiler otherwise
+        // compares the 64-bit popcount with VALU v_cmp_*_u64)
+        const uint32_t n_w = wave_count(w);
+        const bool tail = n_w <= 8u;   // stamps only: the walk's tail (few lanes left)
         stamps::lap(tail ? 11 : 1);
         if (tail) stamps::count(13);
         if (!w) break;
-        if (__popcll(w) <= suspend_at && __popcll(participants & ~w) >= SUSPEND_MIN_DONE && it > 0) break;
-        if (__popcll(__ballot(stopped)) * 64 >= SPEC_LEAF_ROUND * __popcll(w) && parked >= 0) {
+        if (n_w <= (uint32_t)suspend_at && wave_count(participants & ~w) >= (uint32_t)SUSPEND_MIN_DONE && it > 0)
+            break;
+        if (wave_count(stopped) * 64u >= (uint32_t)SPEC_LEAF_ROUND * n_w && parked >= 0) {
             stamps::count(10);
             execdiag::lanes(p.stats + 64, 2);
             if (STATS) cnt.prims++;
@@ -850,6 +870,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         }
         stamps::lap(tail ? 12 : 2);
     }
+    const bool working = parked >= 0 || cur != NONE;
     ws.active = working;
     if (working) return 2;   // suspended
     if (best < 0) return 0;
