@@ -792,65 +792,78 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     };
     // Invariant at the top of every iteration: a lane whose next ref is a leaf has a parked leaf
     // (cur <= -2 implies parked >= 0); the node visit and the leaf round below keep it.
-    for (int it = 0;; ++it) {
-        stamps::count(9);
-        if (cur >= 0) {
-            execdiag::lanes(p.stats + 64, 1);
-            if (STATS) {
-                cnt.nodes++;
-                cnt.gnodes += HYB && cur >= n_lds ? 1u : 0u;
-            }
-            const WideNode n = load_wide_node<HYB>(tree, n_lds, rsrc, image_off, cur, sx, sy, sz);
-            const f2v e01[3] = {n.e[0][0], n.e[1][0], n.e[2][0]}, x01[3] = {n.x[0][0], n.x[1][0], n.x[2][0]};
-            const f2v e23[3] = {n.e[0][1], n.e[1][1], n.e[2][1]}, x23[3] = {n.x[0][1], n.x[1][1], n.x[2][1]};
-            float lo[4];
-            const uint32_t m = wide_pair(e01, x01, ray, limit, lo[0], lo[1]) |
-                               (wide_pair(e23, x23, ray, limit, lo[2], lo[3]) << 2);
-            // The hit child walked next is the one with the nearest entry distance (first slot
-            // on ties): the minimum of sort keys made of the distance's bits with the slot in
-            // the two low bits (integer order is the float order for the distances >= 0; the
-            // few negative ones, of boxes the ray starts in, come first, and ties within 4 ulps
-            // go to the first slot -- the order only steers the walk, the hits do not depend
-            // on it).  The other hits are pushed (slot 3 first) without branches: every slot
-            // is written at the top, and the top moves past it only when it is pushed (the
-            // host bounds the depth, so a write at an unmoved top stays inside the lane's
-            // stack).
-            int key = 0x7fffffff;
+    // The node visits run in an inner loop that leaves for a leaf round (or ends the walk), so
+    // the walk's tmax / limit / best are invariant in it: the compiler then keeps them in place
+    // instead of copying them around the leaf round's branch in every node iteration.
+    int it = 0;
+    for (;;) {
+        bool leaf_round = false;
+        for (;; ++it) {
+            stamps::count(9);
+            if (cur >= 0) {
+                execdiag::lanes(p.stats + 64, 1);
+                if (STATS) {
+                    cnt.nodes++;
+                    cnt.gnodes += HYB && cur >= n_lds ? 1u : 0u;
+                }
+                const WideNode n = load_wide_node<HYB>(tree, n_lds, rsrc, image_off, cur, sx, sy, sz);
+                const f2v e01[3] = {n.e[0][0], n.e[1][0], n.e[2][0]}, x01[3] = {n.x[0][0], n.x[1][0], n.x[2][0]};
+                const f2v e23[3] = {n.e[0][1], n.e[1][1], n.e[2][1]}, x23[3] = {n.x[0][1], n.x[1][1], n.x[2][1]};
+                float lo[4];
+                const uint32_t m = wide_pair(e01, x01, ray, limit, lo[0], lo[1]) |
+                                   (wide_pair(e23, x23, ray, limit, lo[2], lo[3]) << 2);
+                // The hit child walked next is the one with the nearest entry distance (first
+                // slot on ties): the minimum of sort keys made of the distance's bits with the
+                // slot in the two low bits (integer order is the float order for the distances
+                // >= 0; the few negative ones, of boxes the ray starts in, come first, and ties
+                // within 4 ulps go to the first slot -- the order only steers the walk, the hits
+                // do not depend on it).  The other hits are pushed (slot 3 first) without
+                // branches: every slot is written at the top, and the top moves past it only
+                // when it is pushed (the host bounds the depth, so a write at an unmoved top
+                // stays inside the lane's stack).
+                int key = 0x7fffffff;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int kk = (__float_as_int(lo[k]) & ~3) | k;
-                key = ((m >> k) & 1u) && kk < key ? kk : key;
-            }
-            const int bk = key & 3;
-            const uint32_t pm = m & ~(1u << bk);   // the hits pushed
+                for (int k = 0; k < 4; ++k) {
+                    const int kk = (__float_as_int(lo[k]) & ~3) | k;
+                    key = ((m >> k) & 1u) && kk < key ? kk : key;
+                }
+                const int bk = key & 3;
+                const uint32_t pm = m & ~(1u << bk);   // the hits pushed
 #pragma unroll
-            for (int k = 3; k >= 0; --k) {
-                *top = (int16_t)n.ref[k];
-                top += __builtin_amdgcn_ubfe(pm, (uint32_t)k, 1u) * BLK;
+                for (int k = 3; k >= 0; --k) {
+                    *top = (int16_t)n.ref[k];
+                    top += __builtin_amdgcn_ubfe(pm, (uint32_t)k, 1u) * BLK;
+                }
+                const uint32_t word = (bk & 2) ? n.r23 : n.r01;
+                cur = m == 0 ? pop() : (int)(int16_t)(word >> ((bk & 1) << 4));
+                if (cur <= -2 && parked < 0) {   // park the nearest leaf at once
+                    parked = leaf_of(cur);
+                    cur = pop();
+                }
             }
-            const uint32_t word = (bk & 2) ? n.r23 : n.r01;
-            cur = m == 0 ? pop() : (int)(int16_t)(word >> ((bk & 1) << 4));
-            if (cur <= -2 && parked < 0) {   // park the nearest leaf at once
-                parked = leaf_of(cur);
-                cur = pop();
+            // (one ballot per compare, combined as masks: a ballot of anything but a single
+            // compare -- __ballot's int argument, a named bool, an || -- is materialised in a
+            // VGPR and compared back into a mask)
+            const uint64_t has_parked = __builtin_amdgcn_ballot_w64(parked >= 0);
+            const uint64_t w = has_parked | __builtin_amdgcn_ballot_w64(cur != NONE);
+            const uint64_t stopped = has_parked & __builtin_amdgcn_ballot_w64(cur < 0);   // at a second leaf or out of nodes
+            // wave-uniform counts as 32-bit SGPR values: SALU compares (the compiler otherwise
+            // compares the 64-bit popcount with VALU v_cmp_*_u64)
+            const uint32_t n_w = wave_count(w);
+            const bool tail = n_w <= 8u;   // stamps only: the walk's tail (few lanes left)
+            stamps::lap(tail ? 11 : 1);
+            if (tail) stamps::count(13);
+            if (!w) break;
+            if (n_w <= (uint32_t)suspend_at && wave_count(participants & ~w) >= (uint32_t)SUSPEND_MIN_DONE && it > 0)
+                break;
+            if (wave_count(stopped) * 64u >= (uint32_t)SPEC_LEAF_ROUND * n_w) {
+                leaf_round = true;
+                ++it;
+                break;
             }
         }
-        // (one ballot per compare, combined as masks: a ballot of anything but a single compare
-        // -- __ballot's int argument, a named bool, an || -- is materialised in a VGPR and
-        // compared back into a mask)
-        const uint64_t has_parked = __builtin_amdgcn_ballot_w64(parked >= 0);
-        const uint64_t w = has_parked | __builtin_amdgcn_ballot_w64(cur != NONE);
-        const uint64_t stopped = has_parked & __builtin_amdgcn_ballot_w64(cur < 0);   // at a second leaf or out of nodes
-        // wave-uniform counts as 32-bit SGPR values: SALU compares (the compiler otherwise
-        // compares the 64-bit popcount with VALU v_cmp_*_u64)
-        const uint32_t n_w = wave_count(w);
-        const bool tail = n_w <= 8u;   // stamps only: the walk's tail (few lanes left)
-        stamps::lap(tail ? 11 : 1);
-        if (tail) stamps::count(13);
-        if (!w) break;
-        if (n_w <= (uint32_t)suspend_at && wave_count(participants & ~w) >= (uint32_t)SUSPEND_MIN_DONE && it > 0)
-            break;
-        if (wave_count(stopped) * 64u >= (uint32_t)SPEC_LEAF_ROUND * n_w && parked >= 0) {
+        if (!leaf_round) break;   // the walk ended or is suspended
+        if (parked >= 0) {
             stamps::count(10);
             execdiag::lanes(p.stats + 64, 2);
             if (STATS) cnt.prims++;
@@ -868,7 +881,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
                 cur = pop();
             }
         }
-        stamps::lap(tail ? 12 : 2);
+        stamps::lap(2);
     }
     const bool working = parked >= 0 || cur != NONE;
     ws.active = working;
