@@ -120,6 +120,7 @@ struct RayK {
                          // yx and yz are filled by with_slab() where an exact slab test runs
     double ya;           // 1/dot(d,d)            (sphere roots, object.cu:15-20)
     double yc;           // 1/(dx*dx + dz*dz)     (cylinder side roots, object.cu:69-79)
+    float aa, ac;        // dot(d,d) and dx*dx + dz*dz themselves: the quadratics' `a` (per ray)
     // The ordered walk's conservative slabs (slab_reject<*, true>, wide_pair, slab_pass): a plane
     // p of axis a is entered at t = fma(p, in_a, cn_a) and left at fma(p, if_a, cf_a), with
     // in_a = i (1 - 1e-3), if_a = i (1 + 1e-3) for the f32 i = 1/d_a (the relative margin: an
@@ -152,8 +153,10 @@ __device__ __forceinline__ RayK make_rayk(const Ray& r) {
     k.yx = 0.0;   // with_slab()
     k.yy = rcp_d(r.d.y);
     k.yz = 0.0;
-    k.ya = rcp_d(dot(r.d, r.d));
-    k.yc = rcp_d(r.d.x * r.d.x + r.d.z * r.d.z);
+    k.aa = dot(r.d, r.d);
+    k.ac = r.d.x * r.d.x + r.d.z * r.d.z;
+    k.ya = rcp_d(k.aa);
+    k.yc = rcp_d(k.ac);
     slab_axis(r.o.x, r.d.x, k.inx, k.ifx, k.nx, k.fx);
     slab_axis(r.o.y, r.d.y, k.iny, k.ify, k.ny, k.fy);
     slab_axis(r.o.z, r.d.z, k.inz, k.ifz, k.nz, k.fz);
@@ -518,7 +521,9 @@ __device__ __forceinline__ bool sphere_cyl_test(const Node& nd, const RayK& ray,
     const float dx = ray.d.x, dy = ray.d.y, dz = ray.d.z;
     const float bx = cx * dx, ax = dx * dx, qx = cx * cx;
     const float b = (sph ? bx + cy * dy : bx) + cz * dz;
-    const float a = (sph ? ax + dy * dy : ax) + dz * dz;
+    // (dx*dx + dy*dy) + dz*dz or dx*dx + dz*dz: the ray's own, computed once (RayK::aa / ac)
+    const float a = sph ? ray.aa : ray.ac;
+    (void)ax;
     const float c = ((sph ? qx + cy * cy : qx) + cz * cz) - r * r;
     const float disc = b * b - a * c;
     if (!(disc > 0.f)) return ret;
