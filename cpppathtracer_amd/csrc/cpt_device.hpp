@@ -42,6 +42,27 @@ __device__ __forceinline__ v3 normalize(v3 v) {                                 
     float inv = rcp_f(__builtin_sqrtf(dot(v, v)));   // host-path rsqrtf = 1/sqrtf (:78-81)
     return v * inv;
 }
+
+// sqrtf(x), correctly rounded, for x = +-0, |x| >= 2^-96, inf or NaN: the compiler's own IEEE
+// sequence (v_sqrt_f32, then the candidate +-1 ulp chosen by the signs of the two fma
+// residuals) without the steps that serve only |x| < 2^-96 (the 2^32 pre-scale and 2^-16
+// post-scale) and +-0 / +inf (the final class select: the residual steps already return
+// v_sqrt_f32's +-0 / +inf unchanged); checked for every pattern of that domain on the device
+// (test_sqrt_nn_exhaustive).  Callers pass 0 or quantities far from 2^-96: 1 - z*z of floats
+// z <= 1 (0, >= 2^-24, or <= -2^-24), squared lengths of near-unit vectors.
+__device__ __forceinline__ float sqrt_nn_raw(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
+    const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
+    const float r = rm <= 0.0f ? sm : s;
+    return rp > 0.0f ? sp : r;
+}
+__device__ __forceinline__ float sqrt_nn(float x) { return sqrt_nn_raw(x); }
+// normalize() of a vector whose squared length is 0 or >= 2^-96 (a unit vector up to rounding)
+__device__ __forceinline__ v3 normalize_u(v3 v) {
+    float inv = rcp_f(sqrt_nn(dot(v, v)));
+    return v * inv;
+}
 __device__ __forceinline__ v3 cross(v3 a, v3 b) {                                               // :1436-1439
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }

@@ -428,7 +428,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 dep_acc += DEFAULT_RAY_TMAX;           // TraceRay took the ray by value (a18)
             }
             first = false;
-            ray.d = normalize(sh.bounce);
+            ray.d = normalize_u(sh.bounce);
             ray.tmin = BOUNCE_RAY_TMIN;
             ray.tmax = DEFAULT_RAY_TMAX;
             depth++;
@@ -566,6 +566,13 @@ __global__ void k_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned l
             const float s = __builtin_sqrtf(d), rs_ref = 1.0f / s, rs = rcp_f(s);
             same = (!dom || __float_as_uint(r_ref) == __float_as_uint(r) || (r_ref != r_ref && r != r)) &&
                    (__float_as_uint(rs_ref) == __float_as_uint(rs) || (rs_ref != rs_ref && rs != rs));
+        } else if (which == 5) {   // sqrt_nn over its domain: +-0, |x| >= 2^-96, inf, NaN
+            a = 1.0f;
+            d = __uint_as_float((uint32_t)i);
+            const uint32_t ex = ((uint32_t)i >> 23) & 0xffu;
+            const bool dom = ex >= 31u || ((uint32_t)i & 0x7fffffffu) == 0u;
+            const float r_ref = __builtin_sqrtf(d), r = sqrt_nn_raw(d);
+            same = !dom || __float_as_uint(r_ref) == __float_as_uint(r) || (r_ref != r_ref && r != r);
         } else {
             const float q_ref = a / d;
             const float q = qdiv(a, d, rcp_d(d));

@@ -953,10 +953,10 @@ struct Shade { v3 radiance, attenuation, bounce; };
 __device__ __forceinline__ v3 to_world(v3 a, v3 N) {
     v3 B, C;
     if (__builtin_fabsf(N.x) > __builtin_fabsf(N.y)) {
-        float invLen = rcp_f(__builtin_sqrtf(N.x * N.x + N.z * N.z));
+        float invLen = rcp_f(sqrt_nn(N.x * N.x + N.z * N.z));
         C = mk(N.z * invLen, 0.0f, -N.x * invLen);
     } else {
-        float invLen = rcp_f(__builtin_sqrtf(N.y * N.y + N.z * N.z));
+        float invLen = rcp_f(sqrt_nn(N.y * N.y + N.z * N.z));
         C = mk(0.f, N.z * invLen, -N.y * invLen);
     }
     B = cross(C, N);
@@ -966,7 +966,7 @@ __device__ __forceinline__ v3 to_world(v3 a, v3 N) {
 // z = pow(x1, inv_alpha) (double pow), r = sqrtf(1 - z^2), phi = (float)(2*M_PI*x2).
 __device__ __forceinline__ v3 lobe(float x_1, float x_2, double inv_alpha) {
     float z = (float)dm::pow((double)x_1, inv_alpha);
-    float r = __builtin_sqrtf(1.0f - z * z);
+    float r = sqrt_nn(1.0f - z * z);
     float phi = (float)(2 * REF_PI * (double)x_2);
     float sp, cp;
     dm::sincosf_(phi, &sp, &cp);
@@ -982,11 +982,11 @@ __device__ __forceinline__ float schlick(float cosine, float r0) {
 
 // refract (ray_tracing_math.hpp:71-80), discriminant through double (1.0 literal).
 __device__ __forceinline__ bool refract(v3 v, v3 n, float ni_over_nt, v3& refracted) {
-    v3 uv = normalize(v);
+    v3 uv = normalize_u(v);
     float dt = dot(uv, n);
     float discriminant = (float)(1.0 - (double)(ni_over_nt * ni_over_nt * (1 - dt * dt)));
     if (discriminant > 0) {
-        refracted = normalize(ni_over_nt * (uv - n * dt) - n * __builtin_sqrtf(discriminant));
+        refracted = normalize_u(ni_over_nt * (uv - n * dt) - n * sqrt_nn(discriminant));
         return true;
     }
     return false;
@@ -1022,12 +1022,12 @@ __device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow&
         if (diag) execdiag::lanes(diag, 5);
         v3 outward, refracted = mk1(0.0f);
         float ni_over_nt, reflect_prob, cosine;
-        const v3 in = normalize(in_dir);
+        const v3 in = normalize_u(in_dir);
         if (dot(in, normal) > 0) {
             outward = -normal;
             ni_over_nt = m.ior;
             cosine = dot(in, normal);
-            cosine = __builtin_sqrtf(1 - m.ior * m.ior * (1 - cosine * cosine));
+            cosine = sqrt_nn(1 - m.ior * m.ior * (1 - cosine * cosine));
         } else {
             outward = normal;
             ni_over_nt = m.inv_ior;   // 1.f / ior, prepared once
@@ -1048,7 +1048,7 @@ __device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow&
 
 // Miss (path_tracer.cu:117-122)
 __device__ __forceinline__ v3 miss_radiance(const KParams& p, v3 dir) {
-    v3 d = normalize(dir);
+    v3 d = normalize_u(dir);
     float v = (float)(dm::div_pi(dm::asinf_(d.z)) + 0.5);     // (double)asinf / REF_PI + 0.5
     float u = (float)dm::div_pi(dm::atanf_(d.y / d.x) / 2);    // (double)(atanf / 2) / REF_PI
     return tex2d(p, u, v);

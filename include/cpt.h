@@ -310,6 +310,8 @@ int cpt_math_batch(cpt_ctx* ctx, int op, const float* a, const float* b, float* 
  * which = 3: the f64 reciprocal helper rcp_d(d) against the IEEE 1.0 / (double)d for the first
  * n float bit patterns d (n = 2^32: all of them); which = 4: the f32 reciprocal helper rcp_f on
  * its domain (2^-126 <= |d| < 2^126, 0, inf, NaN) and rcp_f(sqrtf(d)) for every pattern.
+ * which = 5: the f32 square-root helper sqrt_nn against sqrtf on its domain (+-0,
+ * |x| >= 2^-96, inf, NaN).
  * out[0] receives the mismatch count (0 expected), out[1..out_len) up to out_len-1 failing
  * pairs as (a bits << 32 | d bits). */
 int cpt_selftest_qdiv(cpt_ctx* ctx, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len);

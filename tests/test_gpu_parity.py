@@ -88,6 +88,15 @@ def test_rcp_exhaustive(gpu):
     assert cnt == 0, [float(d) for _, d in pairs]
 
 
+def test_sqrt_nn_exhaustive(gpu):
+    """sqrt_nn (v_sqrt_f32 + the +-1 ulp residual correction without the tiny-argument scaling,
+    cpt_device.hpp) == the IEEE sqrtf for every float pattern of its domain: +-0, |x| >= 2^-96,
+    inf, NaN (the BSDF's 1 - z*z and squared lengths of near-unit vectors).  Outside it: v_sqrt_f32
+    gives a negative subnormal's square root as -0 where sqrtf gives NaN."""
+    cnt, pairs = gpu.selftest_qdiv(5, 1 << 32)
+    assert cnt == 0, [float(d) for _, d in pairs]
+
+
 # ------------------------------------------------------------------------------- rng
 @pytest.mark.parametrize("w,rows", [(64, list(range(64))), (3840, [0, 1, 7, 1079, 2159]),
                                     (333, [5, 3, 200, 3])])
