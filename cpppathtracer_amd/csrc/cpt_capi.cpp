@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdarg>
@@ -340,6 +341,18 @@ struct cpt_ctx {
     Mat* d_mats = nullptr;
     size_t cap_nodes = 0, cap_mats = 0;
     bool scene_set = false;
+    // device refit (cpt_update_objects): the plan of both trees (ids: reference tree, then walk
+    // tree), parents, heights, each object's walk-tree leaf, the boxes as built
+    std::vector<cpt::RefitNode> refit_plan;
+    std::vector<int32_t> refit_parent, refit_height, refit_walk_leaf;
+    std::vector<cpt::Box6> refit_boxes;
+    std::vector<uint8_t> refit_mark;   // scratch of an update batch (all zero between batches)
+    int refit_n_ref = 0;
+    cpt::RefitNode* d_refit_plan = nullptr;
+    cpt::Box6* d_refit_boxes = nullptr;
+    void* d_refit_work = nullptr;   // an update batch: RefitLeaf records, then the dirty node ids
+    size_t cap_refit_plan = 0, cap_refit_boxes = 0, cap_refit_work = 0;
+    float last_update_ms = 0.f;     // host wall time of the last cpt_update_objects[_rebuild]
 
     // material textures (cpt_bind_texture)
     struct Texture { uint64_t handle; uint32_t* d_texels; int w, h, cols, addr, filter; };
@@ -592,7 +605,7 @@ int build(HostBvh& t, const std::vector<cpt_object>& O, std::vector<int>& idx, i
 constexpr int WIDE_STACK = CPT_WSTACK;
 
 int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int n_bvh, int n_unb,
-                   std::vector<Node>& out, int* n_leaves_out) {
+                   std::vector<Node>& out, int* n_leaves_out, std::vector<int>& slot_of, std::vector<int>& leaf_of) {
     std::vector<int> wbin;                      // binary node of each wide node
     std::vector<std::vector<int>> kids;         // its children (binary node ids)
     std::vector<int> wide_of(w.nodes.size(), -1);
@@ -719,8 +732,13 @@ int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int
                 std::memcpy(&q[(2 * a + 1) * 4 + k], &h3[a], 4);
             }
             q[24 + (k >> 1)] |= (uint32_t)(uint16_t)(int16_t)r << (16 * (k & 1));
+            if (k < (int)ord.size()) slot_of[ord[k]] = id * 4 + k;
         }
     }
+    // the device refit's map (binary walk node -> leaf array index; the platforms are its head)
+    leaf_of = li_of;
+    for (size_t b = 0; b < w.nodes.size(); ++b)
+        if (w.nodes[b].is_object && leaf_of[b] < 0 && pos0[b] >= 0 && pos0[b] < n_unb) leaf_of[b] = pos0[b];
     return n_wide;
 }
 
@@ -730,27 +748,73 @@ int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, s
 
 // The reference order followed by the eight octant orders of the walk tree (one array,
 // n_walk nodes each: the unbounded leaves, then the tree).
+void build_refit_plan(cpt_ctx* c, const HostBvh& w, const std::vector<int> (&pos)[8], const std::vector<int>& slot_of,
+                      const std::vector<int>& leaf_of);
+
 void linearise_all(cpt_ctx* c) {
     c->lin.clear();
     c->n_walk = 0;
     c->n_wide = 0;
     c->n_unb = 0;
+    c->refit_plan.clear();
     c->lin.reserve(9 * c->bvh.nodes.size());
     linearise(c->bvh, c->objs, c->mat_of_obj, c->lin, c->pos_of_node, -1, nullptr);
     c->n_bvh = (int)c->lin.size();
     if (c->n_bvh == 0) return;
     HostBvh w;
-    std::vector<int> unbounded, rank, pos, pos0;
+    std::vector<int> unbounded, rank, pos[8];
     const int root = build_walk_tree(c, w, unbounded, rank);
-    for (int o = 0; o < 8; ++o) {
-        linearise(w, c->objs, c->mat_of_obj, c->lin, pos, o, &rank, root, unbounded);
-        if (o == 0) pos0 = pos;
-    }
+    for (int o = 0; o < 8; ++o) linearise(w, c->objs, c->mat_of_obj, c->lin, pos[o], o, &rank, root, unbounded);
     c->n_walk = (int)(c->lin.size() - c->n_bvh) / 8;
     c->n_unb = (int)unbounded.size();
     c->n_leaves = 0;
+    std::vector<int> slot_of(w.nodes.size(), -1), leaf_of(w.nodes.size(), -1);
     if (root >= 0 && !w.nodes[root].is_object)
-        c->n_wide = linearise_wide(w, root, pos0, c->n_bvh, c->n_unb, c->lin, &c->n_leaves);
+        c->n_wide = linearise_wide(w, root, pos[0], c->n_bvh, c->n_unb, c->lin, &c->n_leaves, slot_of, leaf_of);
+    build_refit_plan(c, w, pos, slot_of, leaf_of);
+}
+
+// The device refit's plan (cpt_internal.hpp RefitNode): every node of both trees with the
+// positions of its copies, its parent and its height (leaves 0), and each object's two leaves.
+void build_refit_plan(cpt_ctx* c, const HostBvh& w, const std::vector<int> (&pos)[8], const std::vector<int>& slot_of,
+                      const std::vector<int>& leaf_of) {
+    const int nr = (int)c->bvh.nodes.size(), nw = (int)w.nodes.size();
+    c->refit_n_ref = nr;
+    c->refit_plan.assign(nr + nw, cpt::RefitNode{});
+    c->refit_parent.assign(nr + nw, -1);
+    c->refit_height.assign(nr + nw, 0);
+    c->refit_boxes.assign(nr + nw, cpt::Box6{});
+    c->refit_walk_leaf.assign(c->objs.size(), -1);
+    c->refit_mark.assign(nr + nw, 0);
+    for (int i = 0; i < nr + nw; ++i) {
+        const bool ref = i < nr;
+        const BNode& n = ref ? c->bvh.nodes[i] : w.nodes[i - nr];
+        cpt::RefitNode& r = c->refit_plan[i];
+        const int off = ref ? 0 : nr;
+        r.left = n.is_object ? -1 : n.left + off;
+        r.right = n.is_object ? -1 : n.right + off;
+        r.slot = ref ? -1 : slot_of[i - nr];
+        r.leaf = ref || c->n_wide == 0 ? -1 : leaf_of[i - nr];
+        for (int o = 0; o < 8; ++o) r.pos[o] = -1;
+        if (ref) r.pos[0] = c->pos_of_node[i];
+        else
+            for (int o = 0; o < 8; ++o)
+                r.pos[o] = pos[o][i - nr] < 0 ? -1 : c->n_bvh + o * c->n_walk + pos[o][i - nr];
+        c->refit_boxes[i] = cpt::Box6{{n.bmin.x, n.bmin.y, n.bmin.z}, {n.bmax.x, n.bmax.y, n.bmax.z}};
+        if (!n.is_object) {
+            c->refit_parent[r.left] = i;
+            c->refit_parent[r.right] = i;
+        } else if (!ref) {
+            c->refit_walk_leaf[n.obj] = i;
+        }
+    }
+    // heights, children first: both builders number a parent before its children (bvh.cu:31-90
+    // divide, sah::build)
+    for (int i = nr + nw - 1; i >= 0; --i) {
+        const cpt::RefitNode& r = c->refit_plan[i];
+        if (r.left >= 0)
+            c->refit_height[i] = 1 + std::max(c->refit_height[r.left], c->refit_height[r.right]);
+    }
 }
 
 int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, std::vector<int>& rank) {
@@ -794,6 +858,8 @@ int sync_checked(cpt_ctx* c) {
     return check_device_error(c);
 }
 
+int upload_materials(cpt_ctx* c);
+
 int upload_scene(cpt_ctx* c) {
     if (c->lin.size() * sizeof(Node) > (size_t)INT32_MAX)   // the walk's buffer descriptor range
         return fail(c, CPT_ERR_UNSUPPORTED, "scene too large: %zu BVH nodes in all orders (max %zu)", c->lin.size(),
@@ -805,6 +871,25 @@ int upload_scene(cpt_ctx* c) {
     hipStream_t s = c->stream();
     if (!c->lin.empty())
         HIP_TRY(c, hipMemcpyAsync(c->d_nodes, c->lin.data(), c->lin.size() * sizeof(Node), hipMemcpyHostToDevice, s));
+    if (!c->refit_plan.empty()) {   // the device refit's plan and the boxes as built
+        if ((rc = ensure(c, &c->d_refit_plan, &c->cap_refit_plan, c->refit_plan.size())) != CPT_OK) return rc;
+        if ((rc = ensure(c, &c->d_refit_boxes, &c->cap_refit_boxes, c->refit_boxes.size())) != CPT_OK) return rc;
+        HIP_TRY(c, hipMemcpyAsync(c->d_refit_plan, c->refit_plan.data(), c->refit_plan.size() * sizeof(cpt::RefitNode),
+                                  hipMemcpyHostToDevice, s));
+        HIP_TRY(c, hipMemcpyAsync(c->d_refit_boxes, c->refit_boxes.data(), c->refit_boxes.size() * sizeof(cpt::Box6),
+                                  hipMemcpyHostToDevice, s));
+    }
+    if ((rc = upload_materials(c)) != CPT_OK) return rc;
+    HIP_TRY(c, hipStreamSynchronize(s));
+    c->scene_set = true;
+    return CPT_OK;
+}
+
+// The deduplicated materials (and the descriptors of the textures they use), completed on the
+// device by k_prepare_materials.
+int upload_materials(cpt_ctx* c) {
+    int rc;
+    hipStream_t s = c->stream();
     if (!c->mats_h.empty()) {
         // textured materials: resolve their handles against the bound textures
         std::vector<int32_t> tex_of_mat(c->mats_h.size(), -1);
@@ -836,9 +921,69 @@ int upload_scene(cpt_ctx* c) {
         HIP_TRY(c, cpt::launch_prepare_materials(c->d_mats, any ? c->d_tex_of_mat : nullptr, any ? c->d_texdescs : nullptr,
                                                  (int)c->mats_h.size(), s));
     }
-    HIP_TRY(c, hipStreamSynchronize(s));
-    c->scene_set = true;
     return CPT_OK;
+}
+
+// SceneBVH::UpdateObject for a batch, on the device (cpt_kernels.hip k_refit_*): the updated
+// objects are already in c->objs (and the host's reference tree is refit, for
+// cpt_scene_bvh_export).  The host names the updated leaves and the union of their ancestors in
+// both trees, height by height -- O(updates x depth), independent of the scene size -- and the
+// device rewrites every copy: the reference order, the eight octant orders, the 4-wide image and
+// leaf array.  Same topology as built (the reference never rebuilds either); the walk tree keeps
+// its SAH structure, so the ordered walk stays exact (any tree of conservative boxes is) while
+// its efficiency may drift after large motions (cpt_update_objects_rebuild re-optimises).
+int device_refit(cpt_ctx* c, int n, const int* indices, bool mats_changed) {
+    std::vector<int> uniq(indices, indices + n);
+    std::sort(uniq.begin(), uniq.end());
+    uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
+    const int nr = c->refit_n_ref;
+    std::vector<cpt::RefitLeaf> recs(uniq.size());
+    std::vector<int32_t> dirty;
+    std::vector<uint8_t>& mark = c->refit_mark;
+    mark.resize(c->refit_plan.size(), 0);
+    for (size_t k = 0; k < uniq.size(); ++k) {
+        const int o = uniq[k];
+        cpt::RefitLeaf& r = recs[k];
+        r.ref_id = c->bvh.leaf_of_object[o];
+        r.walk_id = c->refit_walk_leaf[o];
+        r.prim = make_node(c->bvh.nodes[r.ref_id], c->objs, c->mat_of_obj);
+        const F3 lo = aabb_min(c->objs[o]), hi = aabb_max(c->objs[o]);
+        r.box = cpt::Box6{{lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}};
+        for (int id : {r.ref_id, r.walk_id})
+            for (int p = id < 0 ? -1 : c->refit_parent[id]; p >= 0 && !mark[p]; p = c->refit_parent[p]) {
+                mark[p] = 1;
+                dirty.push_back(p);
+            }
+    }
+    for (int32_t d : dirty) mark[d] = 0;
+    std::stable_sort(dirty.begin(), dirty.end(),
+                     [&](int32_t a, int32_t b) { return c->refit_height[a] < c->refit_height[b]; });
+    std::vector<int32_t> level_end;
+    for (size_t i = 0; i < dirty.size(); ++i)
+        if (i + 1 == dirty.size() || c->refit_height[dirty[i + 1]] != c->refit_height[dirty[i]])
+            level_end.push_back((int32_t)(i + 1));
+    const size_t rec_bytes = recs.size() * sizeof(cpt::RefitLeaf);
+    std::vector<uint8_t> work(rec_bytes + dirty.size() * sizeof(int32_t));
+    std::memcpy(work.data(), recs.data(), rec_bytes);
+    if (!dirty.empty()) std::memcpy(work.data() + rec_bytes, dirty.data(), dirty.size() * sizeof(int32_t));
+    HIP_TRY(c, hipSetDevice(c->device));
+    int rc;
+    uint8_t* d_work = nullptr;
+    if ((rc = ensure(c, reinterpret_cast<uint8_t**>(&c->d_refit_work), &c->cap_refit_work, work.size())) != CPT_OK)
+        return rc;
+    d_work = static_cast<uint8_t*>(c->d_refit_work);
+    hipStream_t s = c->stream();
+    HIP_TRY(c, hipMemcpyAsync(d_work, work.data(), work.size(), hipMemcpyHostToDevice, s));
+    const size_t image_base = (size_t)c->n_bvh + 8 * (size_t)c->n_walk;
+    uint32_t* image = c->n_wide > 0 ? reinterpret_cast<uint32_t*>(c->d_nodes + image_base) : nullptr;
+    Node* leaves = c->n_wide > 0 ? c->d_nodes + image_base + ((size_t)c->n_wide * 7 + 1) / 2 : nullptr;
+    HIP_TRY(c, cpt::launch_refit(reinterpret_cast<const cpt::RefitLeaf*>(d_work), (int)recs.size(),
+                                 reinterpret_cast<const int32_t*>(d_work + rec_bytes), level_end.data(),
+                                 (int)level_end.size(), nr, c->d_refit_plan, c->d_refit_boxes, c->d_nodes, image, leaves,
+                                 s));
+    if (mats_changed && (rc = upload_materials(c)) != CPT_OK) return rc;
+    // the staging vector must outlive the copy; the render after an update sees the new scene
+    return sync_checked(c);
 }
 
 }  // namespace
@@ -910,6 +1055,9 @@ int cpt_destroy(cpt_ctx* c) {
     free_frame(c);
     (void)hipFree(c->d_nodes);
     (void)hipFree(c->d_mats);
+    (void)hipFree(c->d_refit_plan);
+    (void)hipFree(c->d_refit_boxes);
+    (void)hipFree(c->d_refit_work);
     (void)hipFree(c->d_env);
     for (auto& t : c->textures) (void)hipFree(t.d_texels);
     (void)hipFree(c->d_texdescs);
@@ -989,13 +1137,19 @@ int cpt_set_scene(cpt_ctx* c, const cpt_object* objs, int n) {
 
 // SceneBVH::UpdateObject (bvh.cu:122-157): replace the leaf's object, refit the ancestors
 // (MIN/MAX of the two children per axis), re-upload.
-int cpt_update_objects(cpt_ctx* c, int n, const int* indices, const cpt_object* objs) {
+static int update_objects(cpt_ctx* c, int n, const int* indices, const cpt_object* objs, bool rebuild) {
     if (!c || n < 0 || (n > 0 && (!indices || !objs))) return CPT_ERR_INVALID_ARG;
     if (!c->scene_set) return fail(c, CPT_ERR_STATE, "cpt_update_objects: cpt_set_scene first");
     for (int k = 0; k < n; ++k)
         if (indices[k] < 0 || indices[k] >= (int)c->objs.size())
             return fail(c, CPT_ERR_INVALID_ARG, "cpt_update_objects: index %d out of range", indices[k]);
     if (n == 0) return CPT_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    // a primitive becoming or ceasing to be a platform changes the walk tree's leaf set: rebuild
+    for (int k = 0; k < n && !rebuild; ++k)
+        if ((c->objs[indices[k]].type == CPT_PRIM_PLATFORM) != (objs[k].type == CPT_PRIM_PLATFORM)) rebuild = true;
+    if (c->refit_plan.empty()) rebuild = true;
+    const size_t n_mats = c->mats_h.size();
     // SceneBVH::UpdateObject (bvh.cu:144-157): the leaf takes the object, its ancestors'
     // boxes become the union of their children's.  The refit is a function of the leaves
     // only, so a batch refits once and rebuilds the walk orders and uploads once.
@@ -1018,8 +1172,31 @@ int cpt_update_objects(cpt_ctx* c, int n, const int* indices, const cpt_object* 
             ni = nd.parent;
         }
     }
-    linearise_all(c);   // same topology, new boxes and leaf contents in all nine orders
-    return upload_scene(c);
+    int rc;
+    if (rebuild) {
+        // the reference tree keeps its topology (refit above); the walk tree is rebuilt from the
+        // current objects, then all nine orders are re-linearised and uploaded
+        linearise_all(c);
+        rc = upload_scene(c);
+    } else {
+        rc = device_refit(c, n, indices, c->mats_h.size() != n_mats);
+    }
+    c->last_update_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+int cpt_update_objects(cpt_ctx* c, int n, const int* indices, const cpt_object* objs) {
+    return update_objects(c, n, indices, objs, false);
+}
+
+int cpt_update_objects_rebuild(cpt_ctx* c, int n, const int* indices, const cpt_object* objs) {
+    return update_objects(c, n, indices, objs, true);
+}
+
+int cpt_last_update_ms(cpt_ctx* c, float* ms) {
+    if (!c || !ms) return CPT_ERR_INVALID_ARG;
+    *ms = c->last_update_ms;
+    return CPT_OK;
 }
 
 int cpt_update_object(cpt_ctx* c, int index, const cpt_object* obj) {

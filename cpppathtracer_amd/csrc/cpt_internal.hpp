@@ -100,6 +100,32 @@ struct WfState {
     uint32_t* counts;     // [0], [1]: queue sizes; [3]: ident size
 };
 
+// Device refit of cpt_update_objects (SceneBVH::UpdateObject, bvh.cu:122-157, on the GPU).  The
+// reference tree's nodes and the walk tree's nodes are numbered together ("refit ids": the
+// reference tree's BNodes first, then the walk tree's); each records where its copies live in
+// the node buffer.  The topology is fixed until the next cpt_set_scene.
+struct RefitNode {
+    int32_t left, right;    // children (refit ids); a leaf has left = -1
+    int32_t slot;           // 4-wide image slot holding this node's box (wide id * 4 + k), or -1
+    int32_t leaf;           // index in the wide tree's leaf array (walk-tree leaves), or -1
+    int32_t pos[8];         // node-buffer index of each copy: the reference order (pos[0]) or the
+                            // octant orders 0..7 of the walk tree (octant form); -1: none
+};
+struct Box6 { float lo[3], hi[3]; };
+// One updated object: its inline primitive (Node::miss is not written: each copy keeps its own)
+// and its box (Object::GetAABBMin/Max), for its leaf in each tree.
+struct RefitLeaf {
+    Node prim;
+    Box6 box;
+    int32_t ref_id, walk_id;
+};
+// The leaves, then the dirty internal nodes height by height (children before parents): one
+// launch of k_refit_leaves, one of k_refit_nodes per height.  n_ref: reference-tree ids are
+// [0, n_ref); `image` / `leaves` are the wide tree's compact image and leaf array (nullptr: none).
+hipError_t launch_refit(const RefitLeaf* leaves_in, int n_leaves, const int32_t* dirty, const int32_t* level_end,
+                        int n_levels, int n_ref, const RefitNode* nodes_plan, Box6* boxes, Node* nodes, uint32_t* image,
+                        Node* leaves, hipStream_t stream);
+
 hipError_t launch_megakernel(const KParams& p, bool stats, bool aux, hipStream_t stream);
 hipError_t launch_wavefront(const KParams& p, WfState& w, bool stats, bool aux, hipStream_t stream, int* launches);
 hipError_t wavefront_build_ident(const KParams& p, WfState& w, hipStream_t stream);

@@ -939,6 +939,104 @@ hipError_t launch_tile_schedule(const KParams& p0, int passes, void* scratch, si
                                                         stream);
 }
 
+// ======================================================================================
+// Device refit (SceneBVH::UpdateObject / UpdateSceneBVH, bvh.cu:122-157).  The reference refits
+// the updated leaf's ancestors on the host and copies the whole node array back to the GPU;
+// here the host only names the updated leaves and their dirty ancestors (cpt_capi.cpp
+// device_refit) and the boxes are recomputed where the nodes live, for both trees at once:
+// the reference order, the walk tree's eight octant orders, its 4-wide image and leaf array.
+// One thread per node; a launch per height, so a node's children are final before it runs.
+// ======================================================================================
+__device__ __forceinline__ float refit_min(float a, float b) { return a < b ? a : b; }   // MIN_ (ray_tracing_math.hpp:19-21)
+__device__ __forceinline__ float refit_max(float a, float b) { return a > b ? a : b; }   // MAX_ (:15-17)
+
+// A node's inline primitive into one of its copies (each copy keeps its own `miss`).
+__device__ __forceinline__ void refit_put_prim(Node* n, const Node& v) {
+    n->a0 = v.a0; n->a1 = v.a1; n->a2 = v.a2;
+    n->b0 = v.b0; n->b1 = v.b1; n->b2 = v.b2;
+    n->code = v.code;
+}
+
+// An internal node's box into one of its copies: octant form for the walk tree's octant
+// orders (cpt_capi.cpp linearise: the planes a ray of the octant enters through in a).
+__device__ __forceinline__ void refit_put_box(Node* n, const Box6& b, int oct) {
+    const bool sx = oct & 1, sy = oct & 2, sz = oct & 4;
+    n->a0 = sx ? b.hi[0] : b.lo[0]; n->b0 = sx ? b.lo[0] : b.hi[0];
+    n->a1 = sy ? b.hi[1] : b.lo[1]; n->b1 = sy ? b.lo[1] : b.hi[1];
+    n->a2 = sz ? b.hi[2] : b.lo[2]; n->b2 = sz ? b.lo[2] : b.hi[2];
+}
+
+// A slot of the 4-wide image (7 x 16 B per node: [min x][max x][min y][max y][min z][max z] of
+// the four slots, then the refs; cpt_capi.cpp linearise_wide).
+__device__ __forceinline__ void refit_put_slot(uint32_t* image, int slot, const Box6& b) {
+    uint32_t* q = image + (size_t)(slot >> 2) * 28;
+    const int k = slot & 3;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        q[(2 * a) * 4 + k] = __float_as_uint(b.lo[a]);
+        q[(2 * a + 1) * 4 + k] = __float_as_uint(b.hi[a]);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_refit_leaves(const RefitLeaf* __restrict__ in, int n,
+                                                      const RefitNode* __restrict__ plan, Box6* boxes, Node* nodes,
+                                                      uint32_t* image, Node* leaves) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const RefitLeaf r = in[i];
+    boxes[r.ref_id] = r.box;
+    refit_put_prim(nodes + plan[r.ref_id].pos[0], r.prim);
+    if (r.walk_id < 0) return;
+    boxes[r.walk_id] = r.box;
+    const RefitNode w = plan[r.walk_id];
+#pragma unroll
+    for (int o = 0; o < 8; ++o)
+        if (w.pos[o] >= 0) refit_put_prim(nodes + w.pos[o], r.prim);
+    if (w.leaf >= 0 && leaves) refit_put_prim(leaves + w.leaf, r.prim);
+    if (w.slot >= 0 && image) refit_put_slot(image, w.slot, r.box);
+}
+
+__global__ void __launch_bounds__(256) k_refit_nodes(const int32_t* __restrict__ ids, int n, int n_ref,
+                                                     const RefitNode* __restrict__ plan, Box6* boxes, Node* nodes,
+                                                     uint32_t* image) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int id = ids[i];
+    const RefitNode r = plan[id];
+    const Box6 L = boxes[r.left], R = boxes[r.right];
+    Box6 b;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {   // UPDATE_AABB_FOR_CUR_NODE (bvh.cu:130-139): MAX_/MIN_(left, right)
+        b.hi[a] = refit_max(L.hi[a], R.hi[a]);
+        b.lo[a] = refit_min(L.lo[a], R.lo[a]);
+    }
+    boxes[id] = b;
+    if (id < n_ref) {
+        refit_put_box(nodes + r.pos[0], b, 0);
+    } else {
+#pragma unroll
+        for (int o = 0; o < 8; ++o) refit_put_box(nodes + r.pos[o], b, o);
+    }
+    if (r.slot >= 0 && image) refit_put_slot(image, r.slot, b);
+}
+
+hipError_t launch_refit(const RefitLeaf* leaves_in, int n_leaves, const int32_t* dirty, const int32_t* level_end,
+                        int n_levels, int n_ref, const RefitNode* plan, Box6* boxes, Node* nodes, uint32_t* image,
+                        Node* leaves, hipStream_t stream) {
+    if (n_leaves > 0)
+        hipLaunchKernelGGL(k_refit_leaves, dim3((n_leaves + 255) / 256), dim3(256), 0, stream, leaves_in, n_leaves, plan,
+                           boxes, nodes, image, leaves);
+    int begin = 0;
+    for (int l = 0; l < n_levels; ++l) {
+        const int n = level_end[l] - begin;
+        if (n > 0)
+            hipLaunchKernelGGL(k_refit_nodes, dim3((n + 255) / 256), dim3(256), 0, stream, dirty + begin, n, n_ref, plan,
+                               boxes, nodes, image);
+        begin = level_end[l];
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_prepare_materials(Mat* mats, const int32_t* tex_of_mat, const TexDesc* texs, int n,
                                     hipStream_t stream) {
     if (n <= 0) return hipSuccess;

@@ -81,6 +81,20 @@ class Renderer:
         o = np.array(obj, dtype=OBJECT_DTYPE, copy=True)
         self._check(self._L.cpt_update_object(self._ctx, index, _p(o)))
 
+    def update_objects(self, indices, objs, rebuild=False):
+        """SceneBVH::UpdateObject for a batch: refit on the device (cpt_update_objects), or with
+        the ordered walk's tree rebuilt on the host (rebuild=True, cpt_update_objects_rebuild)."""
+        idx = np.ascontiguousarray(indices, dtype=np.int32)
+        o = np.ascontiguousarray(objs, dtype=OBJECT_DTYPE)
+        assert o.shape == idx.shape
+        fn = self._L.cpt_update_objects_rebuild if rebuild else self._L.cpt_update_objects
+        self._check(fn(self._ctx, int(idx.size), _p(idx), _p(o)))
+
+    def last_update_ms(self) -> float:
+        ms = ctypes.c_float(0)
+        self._check(self._L.cpt_last_update_ms(self._ctx, ctypes.byref(ms)))
+        return float(ms.value)
+
     def bvh_export(self):
         n = ctypes.c_int(0)
         self._check(self._L.cpt_scene_bvh_export(self._ctx, None, None, 0, ctypes.byref(n)))

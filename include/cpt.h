@@ -186,10 +186,20 @@ int cpt_camera_get_copy(cpt_camera* cam);
 int cpt_set_scene(cpt_ctx* ctx, const cpt_object* objs, int n_objs);
 /* Replace object `index` (AddObject order) and refit the ancestors' boxes. */
 int cpt_update_object(cpt_ctx* ctx, int index, const cpt_object* obj);
-/* The same for n objects at once (one refit pass, one walk-order rebuild, one upload); the
- * refit is a function of the leaves only, so the result equals n single updates in any order
- * (SceneBVH::UpdateObject, bvh.cu:122-157). */
+/* The same for n objects at once (SceneBVH::UpdateObject, bvh.cu:122-157), refit on the GPU:
+ * the host names the updated leaves and their ancestors (O(n x depth)), kernels rewrite the
+ * boxes bottom-up in every device copy of both trees (reference order, walk orders, 4-wide
+ * image); topology as built.  The refit is a function of the leaves only, so the result equals
+ * n single updates in any order (a repeated index: the last object wins).  Returns after the
+ * device copies are updated.  An edit that turns an object into a platform or back rebuilds
+ * like cpt_update_objects_rebuild. */
 int cpt_update_objects(cpt_ctx* ctx, int n, const int* indices, const cpt_object* objs);
+/* The same edits, with the ordered walk's SAH tree rebuilt from the edited objects on the host
+ * and all orders re-linearised and uploaded (the reference order is refit either way): restores
+ * the walk tree's quality after large motions.  Same images. */
+int cpt_update_objects_rebuild(cpt_ctx* ctx, int n, const int* indices, const cpt_object* objs);
+/* Host wall time of the last cpt_update_objects[_rebuild] call, ms. */
+int cpt_last_update_ms(cpt_ctx* ctx, float* ms);
 /* Exports the BVH in the reference's node order (Divide creation order): per node
  * boxes[6] = {min xyz, max xyz}, links[4] = {is_object, left, right, object index}. */
 int cpt_scene_bvh_export(cpt_ctx* ctx, float* boxes, int32_t* links, int capacity, int* n_nodes);

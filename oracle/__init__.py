@@ -83,6 +83,8 @@ def lib():
         L.or_render.restype = i32
         L.or_render_edited.argtypes = [P, i32, P, P, i32, P, P, i32, i32, i32, P, i32, i32, i32, P, P, P, i32]
         L.or_render_edited.restype = i32
+        L.or_render_edited_ex.argtypes = [P, i32, P, P, i32, P, P, i32, i32, i32, P, i32, i32, i32, P, P, P, i32, i32]
+        L.or_render_edited_ex.restype = i32
         L.or_bind_texture.argtypes = [u64, P, i32, i32, i32, i32, i32]
         L.or_bind_texture.restype = None
         L.or_clear_textures.argtypes = []
@@ -233,9 +235,11 @@ def set_walk(ordered: bool):
     lib().or_set_walk(1 if ordered else 0)
 
 
-def render_edited(objs, edits, cam, env, rows, spp, max_depth, rng, threads=1):
+def render_edited(objs, edits, cam, env, rows, spp, max_depth, rng, threads=1, walk_rebuild=False):
     """render() on the BVH of `objs` after SceneBVH::UpdateObject edits [(index, new_object), ...]
-    (refit, same topology, bvh.cu:122-157).  Returns (accum, stats)."""
+    (refit, same topology, bvh.cu:122-157).  The diagnostic ordered walk's own tree is refit the
+    same way (cpt_update_objects), or rebuilt from the edited objects with walk_rebuild
+    (cpt_update_objects_rebuild).  Returns (accum, stats)."""
     objs = np.ascontiguousarray(objs)
     cam = np.ascontiguousarray(cam)
     rows = np.ascontiguousarray(rows, dtype=np.int32)
@@ -247,8 +251,9 @@ def render_edited(objs, edits, cam, env, rows, spp, max_depth, rng, threads=1):
     stats = np.zeros(5, dtype=np.uint64)
     env_ptr = _ptr(env.rgba) if env is not None else None
     ew, eh, ec = (env.width, env.height, env.valid_cols) if env is not None else (1, 1, 0)
-    rc = lib().or_render_edited(_ptr(objs), len(objs), _ptr(idx), _ptr(new), idx.size, _ptr(cam), env_ptr, ew, eh, ec,
-                                _ptr(rows), rows.size, spp, max_depth, _ptr(rng), _ptr(accum), _ptr(stats), threads)
+    rc = lib().or_render_edited_ex(_ptr(objs), len(objs), _ptr(idx), _ptr(new), idx.size, _ptr(cam), env_ptr, ew, eh,
+                                   ec, _ptr(rows), rows.size, spp, max_depth, _ptr(rng), _ptr(accum), _ptr(stats),
+                                   threads, int(bool(walk_rebuild)))
     if rc != 0:
         raise ValueError(f"or_render_edited failed: {rc}")
     return accum, dict(zip(("segments", "nodes", "prims", "hits", "misses"), (int(x) for x in stats)))

@@ -1504,10 +1504,15 @@ int or_render(const void* objs, int n_objs, const void* camera, const uint8_t* e
 // (bvh.cu:122-157): edit k replaces object edit_idx[k] by edit_objs[k], then refits the
 // leaf's box and every ancestor's box (MIN/MAX of its two children) up to the root.  The
 // topology (and so the traversal order) stays the one of the original build.
-int or_render_edited(const void* objs, int n_objs, const int32_t* edit_idx, const void* edit_objs, int n_edits,
-                     const void* camera, const uint8_t* env_rgba, int env_w, int env_h, int env_valid_cols,
-                     const int32_t* rows, int n_rows, int spp, int max_depth, uint32_t* rng_planar, float* accum,
-                     uint64_t* stats5, int nthreads) {
+// The diagnostic ordered walk's tree: walk_rebuild = 0 refits it the same way (the walk leaf
+// takes the object's new box, its ancestors the MIN/MAX of their two children, left first:
+// libcpt's device refit, cpt_kernels.hip k_refit_nodes); 1 rebuilds it from the edited objects
+// (cpt_update_objects_rebuild).  A platform edit that changes whether the object is a platform
+// always rebuilds (the walk tree holds only the bounded primitives).
+int or_render_edited_ex(const void* objs, int n_objs, const int32_t* edit_idx, const void* edit_objs, int n_edits,
+                        const void* camera, const uint8_t* env_rgba, int env_w, int env_h, int env_valid_cols,
+                        const int32_t* rows, int n_rows, int spp, int max_depth, uint32_t* rng_planar, float* accum,
+                        uint64_t* stats5, int nthreads, int walk_rebuild) {
     if (max_depth < 0 || max_depth > (int)MAX_RECURSION_DEPTH_SET) return -1;
     std::vector<Object> cur(reinterpret_cast<const Object*>(objs), reinterpret_cast<const Object*>(objs) + n_objs);
     Bvh bvh;
@@ -1518,11 +1523,30 @@ int or_render_edited(const void* objs, int n_objs, const int32_t* edit_idx, cons
         if (n.is_object) leaf_of[n.obj] = (int)i;
         else { parent[n.left] = (int)i; parent[n.right] = (int)i; }
     }
+    std::vector<int> wparent(bvh.walk.size(), -1), wleaf_of(n_objs, -1);
+    for (size_t i = 0; i < bvh.walk.size(); ++i) {
+        const Bvh::WNode& n = bvh.walk[i];
+        if (n.obj >= 0) wleaf_of[n.obj] = (int)i;
+        else { wparent[n.left] = (int)i; wparent[n.right] = (int)i; }
+    }
     const Object* E = reinterpret_cast<const Object*>(edit_objs);
     for (int k = 0; k < n_edits; ++k) {
         int o = edit_idx[k];
         if (o < 0 || o >= n_objs) return -2;
+        if ((cur[o].type == PRIM_PLATFORM) != (E[k].type == PRIM_PLATFORM)) walk_rebuild = 1;
         cur[o] = E[k];
+        for (int wi = wleaf_of[o]; wi != -1; wi = wparent[wi]) {   // the walk tree, refit alike
+            Bvh::WNode& n = bvh.walk[wi];
+            if (n.obj >= 0) {
+                n.bmax = aabb_max(cur[n.obj]);
+                n.bmin = aabb_min(cur[n.obj]);
+            } else {
+                const Bvh::WNode& L = bvh.walk[n.left];
+                const Bvh::WNode& R = bvh.walk[n.right];
+                n.bmax = mk(MAX_(L.bmax.x, R.bmax.x), MAX_(L.bmax.y, R.bmax.y), MAX_(L.bmax.z, R.bmax.z));
+                n.bmin = mk(MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z));
+            }
+        }
         for (int ni = leaf_of[o]; ni != -1; ni = parent[ni]) {      // UpdateSceneBVH (bvh.cu:122-141)
             Node& n = bvh.nodes[ni];
             if (n.is_object) {
@@ -1536,9 +1560,17 @@ int or_render_edited(const void* objs, int n_objs, const int32_t* edit_idx, cons
             }
         }
     }
-    build_walk_tree(bvh);   // diagnostic ordered walk: splice the refit tree
+    if (walk_rebuild) build_walk_tree(bvh);
     return render_with(bvh, camera, env_rgba, env_w, env_h, env_valid_cols, rows, n_rows, spp, max_depth, rng_planar,
                        accum, nullptr, nullptr, stats5, 0, nthreads);
+}
+
+int or_render_edited(const void* objs, int n_objs, const int32_t* edit_idx, const void* edit_objs, int n_edits,
+                     const void* camera, const uint8_t* env_rgba, int env_w, int env_h, int env_valid_cols,
+                     const int32_t* rows, int n_rows, int spp, int max_depth, uint32_t* rng_planar, float* accum,
+                     uint64_t* stats5, int nthreads) {
+    return or_render_edited_ex(objs, n_objs, edit_idx, edit_objs, n_edits, camera, env_rgba, env_w, env_h,
+                               env_valid_cols, rows, n_rows, spp, max_depth, rng_planar, accum, stats5, nthreads, 0);
 }
 
 // Denoising + Mix (path_tracer.cu:177-254) for a full W x H frame.  radiance = accum rgb /
