@@ -1150,9 +1150,10 @@ static int update_objects(cpt_ctx* c, int n, const int* indices, const cpt_objec
         if ((c->objs[indices[k]].type == CPT_PRIM_PLATFORM) != (objs[k].type == CPT_PRIM_PLATFORM)) rebuild = true;
     if (c->refit_plan.empty()) rebuild = true;
     const size_t n_mats = c->mats_h.size();
-    // SceneBVH::UpdateObject (bvh.cu:144-157): the leaf takes the object, its ancestors'
-    // boxes become the union of their children's.  The refit is a function of the leaves
-    // only, so a batch refits once and rebuilds the walk orders and uploads once.
+    // SceneBVH::UpdateObject (bvh.cu:144-157) on the host's reference tree (cpt_scene_bvh_export
+    // reads it): the leaf takes the object, its ancestors' boxes become the union of their
+    // children's.  The refit is a function of the leaves only, so the device copies are refit
+    // once per batch below (device_refit), or rebuilt and uploaded once.
     for (int k = 0; k < n; ++k) {
         const int index = indices[k];
         c->objs[index] = objs[k];

@@ -4,7 +4,7 @@
 //   cpt_headless [--scene s3|s4|s1000] [--width W] [--height H] [--spp N] [--depth D] [--seed S]
 //                [--out radiance.bin] [--dispatch K --bgra frame.bin] [--pfm image.pfm]
 //                [--texture file.ppm|file.cptex] [--dump-scene objects.bin] [--devices N]
-//                [--objects N]
+//                [--objects N] [--animate K]
 //
 // --devices N row-tiles the image over N contexts (PathTracer::SetDevices: device i % visible
 // devices, so N > the GPU count puts several tiles on one GPU) and gathers each pass's tiles
@@ -16,6 +16,10 @@
 // --texture makes the floor, the Glass and the Metal sphere of s4 textured materials
 // (Material::have_tex_/tex_, material.h:21-25) sampling that file (AddTexByFile defaults).
 //
+// --animate K renders K more frames after the first (spp each, not accumulated; the RNG streams
+// continue), moving every 10th object (indices 1, 11, 21, ...) by +0.75 in x before each one
+// through SceneBVH::UpdateObject (a device refit of both trees), and prints each frame's time.
+// --out then holds the last frame.
 // --out writes the raw accumulator mean as float32 rgb (row-major); --dispatch runs K passes
 // through the asynchronous DispatchRay pipeline (1 spp + denoise + mix per pass, callback on
 // the render thread) and writes the last BGRA8 frame to --bgra.
@@ -31,6 +35,13 @@
 #include "cpppathtracer/path_tracer.h"
 
 namespace {
+
+std::vector<Object*> g_objects;   // AddObject order (--animate edits them)
+
+void add(PathTracer& tracer, Object* o) {
+    g_objects.push_back(o);
+    tracer.AddObject(o);
+}
 
 Object* make_sphere(const Material& m, float3 c, float r) {
     Object* o = new Object();
@@ -102,7 +113,7 @@ void add_s1000(PathTracer& tracer, uint32_t seed = 20250124u, int n = 1000) {
         }
     }
     Object* floor = make_object(PrimitiveType::Platform, mats[0], make_float3(0, -10000.f, 0), 10000.f, 0.f);
-    tracer.AddObject(floor);
+    add(tracer, floor);
     for (int k = 0; k < n; ++k) {
         const float z = -550.0f + 1.1f * (float)k;
         const int rnd = (int)(rng.random() * 2048.0f) % 2;
@@ -110,11 +121,11 @@ void add_s1000(PathTracer& tracer, uint32_t seed = 20250124u, int n = 1000) {
         const float r = rng.random() * 15.0f + 1.0f;
         if (rnd == 0) {
             const float x = rng.random() * 300.0f - 150.0f;
-            tracer.AddObject(make_object(PrimitiveType::Sphere, mat, make_float3(x, r, z), r, 0.f));
+            add(tracer, make_object(PrimitiveType::Sphere, mat, make_float3(x, r, z), r, 0.f));
         } else {
             const float h = r / 2.0f + rng.random() * 20.0f;
             const float x = rng.random() * 300.0f - 150.0f;
-            tracer.AddObject(make_object(PrimitiveType::Cylinder, mat, make_float3(x, h / 2.0f, z), r, h));
+            add(tracer, make_object(PrimitiveType::Cylinder, mat, make_float3(x, h / 2.0f, z), r, h));
         }
     }
 }
@@ -134,7 +145,7 @@ void on_frame(uint8_t* data, int width, int height, void* param) {
 
 int main(int argc, char** argv) {
     std::string scene = "s4", out, bgra_out, pfm, texture, dump_scene;
-    int W = 64, H = 36, spp = 2, depth = 8, dispatch = 0, devices = 1, n_objects = 1000;
+    int W = 64, H = 36, spp = 2, depth = 8, dispatch = 0, devices = 1, n_objects = 1000, animate = 0;
     unsigned long long seed = 1234;
     for (int i = 1; i + 1 < argc; i += 2) {
         std::string k = argv[i], v = argv[i + 1];
@@ -152,6 +163,7 @@ int main(int argc, char** argv) {
         else if (k == "--dump-scene") dump_scene = v;
         else if (k == "--devices") devices = std::stoi(v);
         else if (k == "--objects") n_objects = std::stoi(v);
+        else if (k == "--animate") animate = std::stoi(v);
         else { fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
     }
 
@@ -167,9 +179,9 @@ int main(int argc, char** argv) {
     if (scene == "s1000") {
         add_s1000(tracer, 20250124u, n_objects);
     } else if (scene == "s3") {
-        tracer.AddObject(make_sphere(make_material(MaterialType::Diffuse, make_float3(0.8f, 0.3f, 0.3f)), make_float3(-35.f, 15.f, 0.f), 15.f));
-        tracer.AddObject(make_sphere(make_material(MaterialType::Diffuse, make_float3(0.3f, 0.8f, 0.3f)), make_float3(0.f, 15.f, 0.f), 15.f));
-        tracer.AddObject(make_sphere(make_material(MaterialType::Diffuse, make_float3(0.3f, 0.3f, 0.8f)), make_float3(35.f, 15.f, 0.f), 15.f));
+        add(tracer, make_sphere(make_material(MaterialType::Diffuse, make_float3(0.8f, 0.3f, 0.3f)), make_float3(-35.f, 15.f, 0.f), 15.f));
+        add(tracer, make_sphere(make_material(MaterialType::Diffuse, make_float3(0.3f, 0.8f, 0.3f)), make_float3(0.f, 15.f, 0.f), 15.f));
+        add(tracer, make_sphere(make_material(MaterialType::Diffuse, make_float3(0.3f, 0.3f, 0.8f)), make_float3(35.f, 15.f, 0.f), 15.f));
     } else {
         PocaTexture tex = 0;
         if (!texture.empty()) {
@@ -188,10 +200,10 @@ int main(int argc, char** argv) {
         floor->y_pos_ = 0.f;
         floor->center_ = make_float3(0, -10000.f, 0);
         floor->radius_ = 10000.f;
-        tracer.AddObject(floor);
-        tracer.AddObject(make_sphere(textured(make_material(MaterialType::Glass, make_float3(1.f), 1.5f, 4.f)), make_float3(-35.f, 15.f, 0.f), 15.f));
-        tracer.AddObject(make_sphere(textured(make_material(MaterialType::Metal, make_float3(0.8f, 0.6f, 0.2f), 0.f, 2.5f)), make_float3(0.f, 15.f, 0.f), 15.f));
-        tracer.AddObject(make_sphere(make_material(MaterialType::Mirror, make_float3(0.9f), 0.f, 3.f, 0.6f), make_float3(35.f, 15.f, 0.f), 15.f));
+        add(tracer, floor);
+        add(tracer, make_sphere(textured(make_material(MaterialType::Glass, make_float3(1.f), 1.5f, 4.f)), make_float3(-35.f, 15.f, 0.f), 15.f));
+        add(tracer, make_sphere(textured(make_material(MaterialType::Metal, make_float3(0.8f, 0.6f, 0.2f), 0.f, 2.5f)), make_float3(0.f, 15.f, 0.f), 15.f));
+        add(tracer, make_sphere(make_material(MaterialType::Mirror, make_float3(0.9f), 0.f, 3.f, 0.6f), make_float3(35.f, 15.f, 0.f), 15.f));
     }
 
     if (!dump_scene.empty()) {
@@ -228,6 +240,18 @@ int main(int argc, char** argv) {
     }
 
     if (!tracer.Render(spp, false)) { fprintf(stderr, "Render: %s\n", tracer.LastError().c_str()); return 1; }
+    for (int f = 1; f <= animate; ++f) {
+        const auto t0 = std::chrono::steady_clock::now();
+        int moved = 0;
+        for (size_t i = 1; i < g_objects.size(); i += 10) {
+            g_objects[i]->center_.x += 0.75f;
+            SceneBVH::UpdateObject(g_objects[i]);
+            ++moved;
+        }
+        if (!tracer.Render(spp, false)) { fprintf(stderr, "Render: %s\n", tracer.LastError().c_str()); return 1; }
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        printf("frame %d: %d objects moved, update + render %.3f ms\n", f, moved, ms);
+    }
     std::vector<float> rgb;
     if (!tracer.ReadRadiance(rgb)) { fprintf(stderr, "ReadRadiance: %s\n", tracer.LastError().c_str()); return 1; }
     double mean = 0;

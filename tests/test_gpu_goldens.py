@@ -84,6 +84,38 @@ def test_cpp_api_render_matches_oracle(oracle_mod, sky, tmp_path, scene, W, H, s
     np.testing.assert_array_equal(rgb.view(np.uint32), want.astype(np.float32).view(np.uint32))
 
 
+def test_cpp_api_animated_refit(oracle_mod, sky, tmp_path):
+    """A dynamic scene through the C++ API: after the first frame, every 10th object moves by
+    +0.75 in x before each of 3 more frames (SceneBVH::UpdateObject -> device refit).  The last
+    frame equals the oracle's render of the refit BVH (bvh.cu:122-157) with the RNG streams
+    carried across the frames."""
+    W, H, spp, depth, K = 48, 27, 2, 16, 3
+    out = tmp_path / "rad.bin"
+    r = subprocess.run([_headless(), "--scene", "s1000", "--width", str(W), "--height", str(H), "--spp", str(spp),
+                        "--depth", str(depth), "--seed", "1234", "--animate", str(K), "--out", str(out)],
+                       cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert f"frame {K}:" in r.stdout, r.stdout
+    objs = scenes.scene_s1000()
+    cam = oracle_mod.camera_get_copy(scenes.camera_for(W, H))
+    rows = np.arange(H, dtype=np.int32)
+    rng = oracle_mod.init_rng(1234, W, rows)
+    acc, _, _, _ = oracle_mod.render(objs, cam, sky, rows, spp, depth, rng, threads=8)
+    moved = np.arange(1, len(objs), 10)
+    x = objs["center"][moved, 0].astype(np.float32).copy()
+    for _ in range(K):
+        x = (x + np.float32(0.75)).astype(np.float32)
+        edits = []
+        for i, xi in zip(moved, x):
+            o = objs[int(i)].copy()
+            o["center"][0] = xi
+            edits.append((int(i), o))
+        acc, _ = oracle_mod.render_edited(objs, edits, cam, sky, rows, spp, depth, rng, threads=8)
+    want = acc[:, :3] / acc[:, 3:4]
+    rgb = np.fromfile(out, dtype=np.float32).reshape(H * W, 3)
+    np.testing.assert_array_equal(rgb.view(np.uint32), want.astype(np.float32).view(np.uint32))
+
+
 def test_cpp_api_dispatch_pipeline(oracle_mod, sky, tmp_path):
     """InitPipeline + DispatchRay x3: GetCopy at thread start (idx 1), then 1 spp + denoise +
     mix per dispatch with idx 2, 3, 4 (path_tracer.cu:256-306) — same bytes as the oracle."""
