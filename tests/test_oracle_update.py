@@ -72,3 +72,35 @@ def test_diagnostic_ordered_walk_same_image(oracle_mod, sky):
     np.testing.assert_array_equal(a1.view(np.uint32), a2.view(np.uint32))
     np.testing.assert_array_equal(r1, r2)
     assert s1["segments"] == s2["segments"] and s1["nodes"] != s2["nodes"]
+
+
+def test_refit_walk_tree_same_image_as_rebuilt(oracle_mod, sky):
+    """The ordered walk on a refit walk tree (libcpt's device refit, cpt_update_objects) and on
+    one rebuilt from the edited objects (cpt_update_objects_rebuild) find the same closest hits
+    as the reference walk: same image and RNG end states; the refit tree's node counts are its
+    own (a worse tree after large moves, never a different hit)."""
+    _, cam, rows = _setup(oracle_mod, 40, 24)
+    objs = scenes.scene_s1000()
+    W = int(cam["width"])
+    rng = np.random.default_rng(5)
+    edits = []
+    for i in rng.choice(np.flatnonzero(objs["type"] != 1), size=200, replace=False):
+        o = objs[int(i)].copy()
+        o["center"][0] += np.float32(rng.uniform(-80, 80))
+        o["radius"] *= np.float32(rng.uniform(0.5, 1.5))
+        edits.append((int(i), o))
+    r0 = oracle_mod.init_rng(4, W, rows, threads=4)
+    a0, s0 = oracle_mod.render_edited(objs, edits, cam, sky, rows, 2, 8, r0, threads=4)
+    out = []
+    oracle_mod.set_walk(True)
+    try:
+        for rebuild in (False, True):
+            r = oracle_mod.init_rng(4, W, rows, threads=4)
+            a, s = oracle_mod.render_edited(objs, edits, cam, sky, rows, 2, 8, r, threads=4, walk_rebuild=rebuild)
+            np.testing.assert_array_equal(a.view(np.uint32), a0.view(np.uint32))
+            np.testing.assert_array_equal(r, r0)
+            assert s["segments"] == s0["segments"] and s["hits"] == s0["hits"]
+            out.append(s)
+    finally:
+        oracle_mod.set_walk(False)
+    assert out[0]["nodes"] != out[1]["nodes"]   # two different walk trees
