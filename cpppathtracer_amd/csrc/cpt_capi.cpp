@@ -350,7 +350,7 @@ struct cpt_ctx {
     int refit_n_ref = 0;
     cpt::RefitNode* d_refit_plan = nullptr;
     cpt::Box6* d_refit_boxes = nullptr;
-    void* d_refit_work = nullptr;   // an update batch: RefitLeaf records, then the dirty node ids
+    uint8_t* d_refit_work = nullptr;   // an update batch: RefitLeaf records, then the dirty node ids
     size_t cap_refit_plan = 0, cap_refit_boxes = 0, cap_refit_work = 0;
     float last_update_ms = 0.f;     // host wall time of the last cpt_update_objects[_rebuild]
 
@@ -968,10 +968,8 @@ int device_refit(cpt_ctx* c, int n, const int* indices, bool mats_changed) {
     if (!dirty.empty()) std::memcpy(work.data() + rec_bytes, dirty.data(), dirty.size() * sizeof(int32_t));
     HIP_TRY(c, hipSetDevice(c->device));
     int rc;
-    uint8_t* d_work = nullptr;
-    if ((rc = ensure(c, reinterpret_cast<uint8_t**>(&c->d_refit_work), &c->cap_refit_work, work.size())) != CPT_OK)
-        return rc;
-    d_work = static_cast<uint8_t*>(c->d_refit_work);
+    if ((rc = ensure(c, &c->d_refit_work, &c->cap_refit_work, work.size())) != CPT_OK) return rc;
+    uint8_t* const d_work = c->d_refit_work;
     hipStream_t s = c->stream();
     HIP_TRY(c, hipMemcpyAsync(d_work, work.data(), work.size(), hipMemcpyHostToDevice, s));
     const size_t image_base = (size_t)c->n_bvh + 8 * (size_t)c->n_walk;
