@@ -84,15 +84,17 @@ def test_cpp_api_render_matches_oracle(oracle_mod, sky, tmp_path, scene, W, H, s
     np.testing.assert_array_equal(rgb.view(np.uint32), want.astype(np.float32).view(np.uint32))
 
 
-def test_cpp_api_animated_refit(oracle_mod, sky, tmp_path):
+@pytest.mark.parametrize("devices", [1, 2])
+def test_cpp_api_animated_refit(oracle_mod, sky, tmp_path, devices):
     """A dynamic scene through the C++ API: after the first frame, every 10th object moves by
-    +0.75 in x before each of 3 more frames (SceneBVH::UpdateObject -> device refit).  The last
-    frame equals the oracle's render of the refit BVH (bvh.cu:122-157) with the RNG streams
-    carried across the frames."""
+    +0.75 in x before each of 3 more frames (SceneBVH::UpdateObject -> device refit, in every
+    context of PathTracer::SetDevices).  The last frame equals the oracle's render of the refit
+    BVH (bvh.cu:122-157) with the RNG streams carried across the frames."""
     W, H, spp, depth, K = 48, 27, 2, 16, 3
     out = tmp_path / "rad.bin"
     r = subprocess.run([_headless(), "--scene", "s1000", "--width", str(W), "--height", str(H), "--spp", str(spp),
-                        "--depth", str(depth), "--seed", "1234", "--animate", str(K), "--out", str(out)],
+                        "--depth", str(depth), "--seed", "1234", "--animate", str(K), "--out", str(out),
+                        "--devices", str(devices)],
                        cwd=REPO, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert f"frame {K}:" in r.stdout, r.stdout
