@@ -12,12 +12,16 @@ Multi-GPU: one process per GPU.  Run under torchrun (WORLD_SIZE set; it must equ
 or give `--gpus N` without a launcher: the parent then starts N ranks through
 `torch.distributed.run` before it touches the GPU, relays rank 0's line and exits with the
 launcher's status.  The image rows are dealt to the ranks in interleaved 8-row blocks (row
-tiling).  Scaling: "weak" (default; the path shards
-into independent row tiles) keeps the pixels per GPU fixed by scaling each axis by sqrt(N)
-(N = 4: 3840x2160, C5's frame); "strong" renders the configuration's image (C4: 1920x1080) at
-every N.  A weak-scaled run with N > 1 also times the configuration's own frame strong-scaled
-over the same ranks and reports it as `strong_scaling` (the north star's 1920x1080 at N GPUs;
-its ceiling is the longest pixel chain).
+tiling).  Scaling: "strong" (default) renders the
+configuration's image (C4: 1920x1080, the metric's resolution; the north star's "1920x1080 at
+1, 2, 4 and 8 GPUs") at every N -- its ceiling is the longest pixel chain, DESIGN.md
+§Multi-GPU; "weak" keeps the pixels per GPU fixed by scaling each axis by sqrt(N) (N = 4:
+3840x2160, C5's frame).  With N > 1 the other mode is timed too over the same ranks and
+reported as a side field (`weak_scaling` / `strong_scaling`).
+
+--dispatch K times the reference's own per-pass loop instead (DispatchRay: 1-spp render +
+Denoising + Mix + BGRA8 to the host, path_tracer.cu:256-306) with one and with several row-tile
+contexts, and prints a separate JSON line (not the headline metric).
 
 Rank 0 prints one JSON line with `roofline` (SURVEY.md §8(d) algorithmic bytes ÷ the kernel's
 HIP-event time, beside the rocprof-measured HBM bytes and VALU issue of a committed profile of
@@ -63,15 +67,22 @@ def parse_args(argv=None):
     ap.add_argument("--schedule", default="cost", choices=["cost", "tiles"],
                     help="megakernel pixel dequeue order: 8x8 tiles heaviest first from a pilot pass "
                          "(CPT_SCHEDULE_COST), or tiles in row-major order")
-    ap.add_argument("--scaling", default="weak", choices=["strong", "weak"],
-                    help="weak: pixels per GPU fixed (image grows by sqrt(N)); strong: the config's image at every N")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (default): the config's image (C4: 1920x1080, the metric's resolution) at every N; "
+                         "weak: pixels per GPU fixed (image grows by sqrt(N))")
     ap.add_argument("--no-strong-check", action="store_true",
-                    help="weak scaling, N > 1: skip the extra strong-scaled timing of the config's own frame")
+                    help="N > 1: skip the extra timing in the other scaling mode (weak-scaled frame, or with "
+                         "--scaling weak the config's own frame strong-scaled)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hbm-probe", action="store_true", help="skip the streaming-read ceiling probe")
     ap.add_argument("--no-count", action="store_true",
                     help="skip the counting passes (roofline byte counts and walk parity): profiling runs only")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target seconds per CPU baseline leg")
+    ap.add_argument("--dispatch", type=int, default=0,
+                    help="K > 0: time K passes of the reference's per-pass DispatchRay loop instead (1 spp + "
+                         "Denoising + Mix + BGRA8 copy; one JSON line, not the headline)")
+    ap.add_argument("--dispatch-contexts", type=int, default=8,
+                    help="--dispatch: also time the loop with this many row-tile contexts + gather (1: skip)")
     ap.add_argument("--profile-json", default=None,
                     help="rocprof summary of this workload (profiles/rocprof_*.json, tools/rocprof_summary.py)")
     return ap.parse_args(argv)
@@ -352,34 +363,45 @@ def run(args):
         t = _all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, avg_kernel_ms_max = t.tolist()
 
-    # Weak scaling, N > 1: the configuration's own frame strong-scaled over the same ranks (each
-    # rank its interleaved 8-row blocks of W0 x H0), 1 untimed + 2 timed frames with the gather.
-    strong = None
-    if world > 1 and args.scaling == "weak" and not args.no_strong_check and (W0, H0) != (W, H):
-        rows0 = tiling.partition_rows(H0, world, rank)
-        cam0 = camera_get_copy(scenes.camera_for(W0, H0))
-        r.set_frame(W0, H0, rows0)
-        r.init_rng(cfg["seed"])
-        gather0 = multigpu.TileGather(W0, H0, world, rank, dev, backend)
-        n_strong = 2
-        for k in range(n_strong + 1):
-            if k == 1:
-                dist.barrier()
-                torch.cuda.synchronize()
-                ts = time.perf_counter()
-            r.render(cam0, spp, depth, path=args.path, ordered=ordered, schedule=schedule, consolidate=consolidate)
-            gather0(r)
-        torch.cuda.synchronize()
-        dist.barrier()
-        ts = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=dev)
-        ts = _all_reduce(ts, op=dist.ReduceOp.MAX).item()
-        strong = {
-            "workload": f"{args.config}: {cfg['scene']} {W0}x{H0} {spp}spp depth {depth}",
-            "n_gpus": world, "steps": n_strong, "ms_per_step": round(ts / n_strong * 1e3, 3),
-            "value": round(W0 * H0 * spp * n_strong / ts / 1e6, 3), "unit": "Mpaths/s",
-            "note": "the configuration's own frame row-tiled over the same ranks (strong scaling); its ceiling is "
-                    "the longest pixel chain (DESIGN.md §Multi-GPU)",
-        }
+    # N > 1: the other scaling mode over the same ranks, 1 untimed + 2 timed frames with the
+    # gather -- strong (the default): the weak-scaled frame (pixels per GPU fixed); weak: the
+    # configuration's own frame strong-scaled (the north star's 1920x1080 at N GPUs, whose
+    # ceiling is the longest pixel chain).
+    other = None
+    if world > 1 and not args.no_strong_check:
+        if args.scaling == "weak":
+            Wx, Hx, mode = W0, H0, "strong"
+        else:
+            (Wx, Hx), mode = tiling.weak_scaled_size(W0, H0, world), "weak"
+        if (Wx, Hx) != (W, H):
+            rows_x = tiling.partition_rows(Hx, world, rank)
+            cam_x = camera_get_copy(scenes.camera_for(Wx, Hx))
+            r.set_frame(Wx, Hx, rows_x)
+            r.init_rng(cfg["seed"])
+            gather_x = multigpu.TileGather(Wx, Hx, world, rank, dev, backend)
+            n_other = 2
+            for k in range(n_other + 1):
+                if k == 1:
+                    dist.barrier()
+                    torch.cuda.synchronize()
+                    ts = time.perf_counter()
+                r.render(cam_x, spp, depth, path=args.path, ordered=ordered, schedule=schedule,
+                         consolidate=consolidate)
+                gather_x(r)
+            torch.cuda.synchronize()
+            dist.barrier()
+            ts = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=dev)
+            ts = _all_reduce(ts, op=dist.ReduceOp.MAX).item()
+            other = {
+                "mode": mode,
+                "workload": f"{args.config}: {cfg['scene']} {Wx}x{Hx} {spp}spp depth {depth}",
+                "n_gpus": world, "steps": n_other, "ms_per_step": round(ts / n_other * 1e3, 3),
+                "value": round(Wx * Hx * spp * n_other / ts / 1e6, 3), "unit": "Mpaths/s",
+                "note": ("the configuration's own frame row-tiled over the same ranks (strong scaling); its ceiling "
+                         "is the longest pixel chain (DESIGN.md §Multi-GPU)" if mode == "strong" else
+                         "the frame scaled by sqrt(N) per axis, so every rank holds the N = 1 pixel count (weak "
+                         "scaling: the path shards into independent row tiles)"),
+            }
 
     if rank == 0:
         paths_total = W * H * spp
@@ -412,8 +434,8 @@ def run(args):
             },
             "rng_init_ms": round(t_init * 1e3, 2),
         }
-        if strong:
-            out["strong_scaling"] = strong
+        if other:
+            out[f"{other.pop('mode')}_scaling"] = other
         if st is not None:
             # Algorithmic bytes of one launch: SURVEY.md 8(d)'s per-unit model x the units the
             # launch processes (the executed walk's own counts; a 4-wide node visit = 112 B),
@@ -493,9 +515,134 @@ def run(args):
         dist.destroy_process_group()
 
 
+# ---------------------------------------------------------------------------------------
+# --dispatch K: the reference's own per-pass loop (PipelineLoop, path_tracer.cu:256-306)
+# ---------------------------------------------------------------------------------------
+DISPLAY_BYTES_PER_PIXEL = 60   # k_denoise_mix: accum 16 + normal 12 + depth 4 + mix 12 read + 12 written + BGRA 4
+
+
+def dispatch_bench(args):
+    """ms per DispatchRay pass: a 1-spp SamplePixel render (radiance + first-hit normal/depth, not
+    accumulated), Denoising + Mix into BGRA8, and the W x H x 4 B copy to the host that the
+    reference's callback receives -- per pass, with each kernel's HIP-event time.  Once with one
+    context (SetDevices(1)), once with `--dispatch-contexts` row-tile contexts gathered into a
+    frame context (SetDevices(n): the contexts share this box's GPU), whose per-pass gather is
+    also timed on its own.  One JSON line; not the headline metric."""
+    import numpy as np
+    import torch
+
+    from cpppathtracer_amd import Renderer, camera_get_copy, scenes, texture_io, tiling
+
+    torch.cuda.set_device(0)
+    cfg = dict(scenes.CONFIGS[args.config])
+    W, H, depth = args.width or cfg["width"], args.height or cfg["height"], cfg["depth"]
+    objs = scenes.SCENES[cfg["scene"]]()
+    sky = texture_io.load_cptex()
+    cam0 = camera_get_copy(scenes.camera_for(W, H))
+    K, warm = args.dispatch, 3
+    host = torch.empty((H, W, 4), dtype=torch.uint8, pin_memory=True).numpy()   # the callback's frame
+    h_eff, w_eff = 16 * (H // 16), 16 * (W // 16)
+
+    def cam_at(idx):   # GetCopy's cur_sample_idx of pass idx (motional_camera.cu:195)
+        c = np.array(cam0, copy=True)
+        c["cur_sample_idx"] = idx
+        return c
+
+    def make(dev_rows=None):
+        r = Renderer(0)
+        r.set_scene(objs)
+        r.set_env(sky)
+        r.set_frame(W, H, dev_rows)
+        r.init_rng(args.seed)
+        return r
+
+    def summary(samples):
+        a = np.array(samples)
+        return {"median": round(float(np.median(a)), 3), "mean": round(float(a.mean()), 3),
+                "min": round(float(a.min()), 3), "max": round(float(a.max()), 3)}
+
+    # ---- one context -------------------------------------------------------------------
+    r = make()
+    wall, rend, disp = [], [], []
+    for k in range(warm + K):
+        idx = k + 1
+        t0 = time.perf_counter()
+        r.render(cam_at(idx), 1, depth, aux=True, ordered=args.walk == "ordered")
+        r.denoise_mix(idx, out=host)   # waits for the frame on the host
+        t1 = time.perf_counter()
+        if k >= warm:
+            wall.append((t1 - t0) * 1e3)
+            rend.append(r.last_render_ms())
+            disp.append(r.last_display_ms())
+    r.close()
+    d_ms = float(np.median(disp))
+    display_bytes = DISPLAY_BYTES_PER_PIXEL * w_eff * h_eff
+    one = {
+        "contexts": 1,
+        "pass_ms": summary(wall),
+        "render_ms": summary(rend),
+        "display_ms": summary(disp),
+        "copy_and_host_ms": round(float(np.median(wall)) - float(np.median(rend)) - d_ms, 3),
+        "display_roofline": {
+            "kernel": "k_denoise_mix", "bound": "hbm", "bytes_per_launch": display_bytes,
+            "achieved": round(display_bytes / (d_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(display_bytes / (d_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "byte_model": f"{DISPLAY_BYTES_PER_PIXEL} B x W'H' ({w_eff}x{h_eff}): accumulator 16 + normal 12 + "
+                          "depth 4 + mix 12 read + 12 written + BGRA8 4",
+        },
+    }
+    # ---- n row-tile contexts + the frame context (SetDevices(n) on this GPU) -------------
+    n = args.dispatch_contexts
+    multi = None
+    if n > 1:
+        tiles = [make(tiling.partition_rows(H, n, t)) for t in range(n)]
+        frame = make()
+        wall, gath = [], []
+        for k in range(warm + K):
+            idx = k + 1
+            t0 = time.perf_counter()
+            for t in tiles:
+                t.render(cam_at(idx), 1, depth, aux=True, ordered=args.walk == "ordered")
+            for t in tiles:
+                frame.gather_rows(t)
+            frame.denoise_mix(idx, out=host)
+            t1 = time.perf_counter()
+            for t in tiles:   # (their errors; their work is done)
+                t.synchronize()
+            # the gather alone: every tile's render finished, then the n gathers and one wait
+            tg = time.perf_counter()
+            for t in tiles:
+                frame.gather_rows(t)
+            frame.synchronize()
+            tg = time.perf_counter() - tg
+            if k >= warm:
+                wall.append((t1 - t0) * 1e3)
+                gath.append(tg * 1e3)
+        multi = {"contexts": n, "pass_ms": summary(wall), "gather_ms": summary(gath),
+                 "note": f"{n} row-tile contexts (interleaved {tiling.BLOCK_ROWS}-row blocks) on one GPU, gathered "
+                         "into a frame context by cpt_gather_rows (events, no host wait), then one display pass"}
+        for t in tiles:
+            t.close()
+        frame.close()
+    out = {
+        "metric": "ms per DispatchRay pass (1 spp SamplePixel + Denoising + Mix + BGRA8 to the host)",
+        "config": {"workload": f"{args.config}: {cfg['scene']} {W}x{H} 1spp depth {depth} per pass",
+                   "width": W, "height": H, "walk": args.walk, "passes": K, "warmup": warm,
+                   "host_buffer": "pinned"},
+        "higher_is_better": False,
+        "single": one,
+    }
+    if multi:
+        out["multi"] = multi
+    print(json.dumps(out), flush=True)
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
+    if args.dispatch:
+        dispatch_bench(args)
+        return
     if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher: start the ranks before anything here touches the GPU
         env = dict(os.environ)

@@ -58,6 +58,7 @@ PROTOTYPES = {
     "cpt_denoise_mix": (_I, [_P, _U32, _P]),
     "cpt_denoise_mix_band": (_I, [_P, _U32, _I, _I, _P]),
     "cpt_copy_bgra_device": (_I, [_P, _P, _SZ]),
+    "cpt_last_display_ms": (_I, [_P, _P]),
     "cpt_reset_display": (_I, [_P]),
     "cpt_math_batch": (_I, [_P, _I, _P, _P, _P, _SZ]),
     "cpt_selftest_qdiv": (_I, [_P, _I, _U64, _U64, _P, _I]),

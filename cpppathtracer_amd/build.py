@@ -16,11 +16,16 @@ SOURCES = [
     os.path.join(CSRC, "cpt_kernels.hip"),
     os.path.join(CSRC, "cpt_wavefront.hip"),
     os.path.join(CSRC, "cpt_capi.cpp"),
+    os.path.join(CSRC, "cpt_scene.cpp"),
+    os.path.join(CSRC, "cpt_host_bvh.cpp"),
+    os.path.join(CSRC, "cpt_host_rng.cpp"),
     os.path.join(CSRC, "cpt_api.cpp"),
 ]
 HEADERS = [
     os.path.join(CSRC, "cpt_device.hpp"),
     os.path.join(CSRC, "cpt_internal.hpp"),
+    os.path.join(CSRC, "cpt_context.hpp"),
+    os.path.join(CSRC, "cpt_host.hpp"),
     os.path.join(CSRC, "cpt_path.hpp"),
     os.path.join(CSRC, "cpt_stamps.hpp"),
     os.path.join(CSRC, "cpt_tuning.hpp"),

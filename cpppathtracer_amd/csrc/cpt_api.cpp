@@ -418,40 +418,33 @@ bool PathTracer::BindTextures(Tile& tile, const std::vector<cpt_object>& objs) {
     return true;
 }
 
-// Brings one context to SceneBVH's state: a new build is uploaded as BuildBVH copied it (the
-// reference's topology), then the objects UpdateObject re-copied since are refit in one batch
-// (bvh.cu:144-157).  The state is read under one lock (SceneBVH::GetState).
-bool PathTracer::SyncTile(Tile& tile) {
-    if (!tile.scene_synced || SceneBVH::Revision() != tile.scene_rev) {
-        uint64_t build = 0, rev = 0;
-        std::vector<cpt_object> built, current;
-        std::vector<uint64_t> updates;
-        const bool rebuild = !tile.scene_synced || SceneBVH::BuildId() != tile.scene_build;
-        SceneBVH::GetState(build, rev, rebuild ? &built : nullptr, current, updates);
-        if (!rebuild && build != tile.scene_build)   // rebuilt between the two reads
-            SceneBVH::GetState(build, rev, &built, current, updates);
-        if (rebuild || build != tile.scene_build) {
+// Brings one context to a snapshot of SceneBVH's state: a new build is uploaded as BuildBVH
+// copied it (the reference's topology), then the objects UpdateObject re-copied since are refit
+// in one batch (bvh.cu:144-157).
+bool PathTracer::SyncTile(Tile& tile, const SceneSnap& snap) {
+    if (!tile.scene_synced || snap.rev != tile.scene_rev) {
+        if (!tile.scene_synced || snap.build != tile.scene_build) {
             tile.bound_textures.clear();
-            if (!BindTextures(tile, built)) return false;
-            if (cpt_set_scene(tile.ctx, built.empty() ? nullptr : built.data(), (int)built.size()) != CPT_OK)
+            if (!BindTextures(tile, snap.built)) return false;
+            if (cpt_set_scene(tile.ctx, snap.built.empty() ? nullptr : snap.built.data(), (int)snap.built.size()) != CPT_OK)
                 return Fail("cpt_set_scene", tile.ctx);
-            tile.scene_build = build;
-            tile.updates_seen.assign(built.size(), 0);
+            tile.scene_build = snap.build;
+            tile.updates_seen.assign(snap.built.size(), 0);
         }
         std::vector<int> idx;
         std::vector<cpt_object> objs;
-        for (size_t i = 0; i < updates.size() && i < tile.updates_seen.size(); ++i)
-            if (updates[i] != tile.updates_seen[i]) {
+        for (size_t i = 0; i < snap.updates.size() && i < tile.updates_seen.size(); ++i)
+            if (snap.updates[i] != tile.updates_seen[i]) {
                 idx.push_back((int)i);
-                objs.push_back(current[i]);
+                objs.push_back(snap.current[i]);
             }
         if (!idx.empty()) {
             if (!BindTextures(tile, objs)) return false;
             if (cpt_update_objects(tile.ctx, (int)idx.size(), idx.data(), objs.data()) != CPT_OK)
                 return Fail("cpt_update_objects", tile.ctx);
         }
-        tile.updates_seen = updates;
-        tile.scene_rev = rev;
+        tile.updates_seen = snap.updates;
+        tile.scene_rev = snap.rev;
         tile.scene_synced = true;
     }
     if (!tile.env_uploaded) {
@@ -465,10 +458,22 @@ bool PathTracer::SyncTile(Tile& tile) {
     return true;
 }
 
+// One snapshot for the whole pass: an UpdateObject from another thread lands either before
+// every tile or after all of them, never between two tiles of one frame.
 bool PathTracer::SyncScene() {
     if (!EnsureContext()) return false;
+    SceneSnap snap;
+    bool need = false;
+    const uint64_t rev = SceneBVH::Revision();
+    for (const Tile& t : tiles_) need = need || !t.scene_synced || t.scene_rev != rev;
+    if (need) {
+        SceneBVH::GetState(snap.build, snap.rev, &snap.built, snap.current, snap.updates);
+    } else {
+        snap.build = tiles_[0].scene_build;
+        snap.rev = tiles_[0].scene_rev;
+    }
     for (Tile& t : tiles_)
-        if (!SyncTile(t)) return false;
+        if (!SyncTile(t, snap)) return false;
     return true;
 }
 
@@ -520,9 +525,12 @@ bool PathTracer::RenderPass(MotionalCamera& cam, int spp, bool accumulate) {
     for (Tile& t : tiles_)
         if (cpt_render(t.ctx, reinterpret_cast<const cpt_camera*>(&cam), spp, (int)max_recursion_depth_, flags) != CPT_OK)
             return Fail("cpt_render", t.ctx);
+    // every gather queues behind its tile's render (events, no host wait); one wait at the end
     for (Tile& t : tiles_)
         if (cpt_gather_rows(frame_, t.ctx) != CPT_OK) return Fail("cpt_gather_rows", frame_);
     if (cpt_synchronize(frame_) != CPT_OK) return Fail("cpt_synchronize", frame_);
+    for (Tile& t : tiles_)   // the tiles' device errors (their work is done by now)
+        if (cpt_synchronize(t.ctx) != CPT_OK) return Fail("cpt_synchronize", t.ctx);
     return true;
 }
 

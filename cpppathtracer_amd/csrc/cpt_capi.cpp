@@ -1,11 +1,11 @@
-// cpt_capi.cpp — implementation of the C-ABI in include/cpt.h.
-//
-// Owns the per-context device memory, builds the reference's median-split BVH on the host
-// (bvh.cu:31-120) and linearises it into the skip-link order the kernels walk, computes the
-// XORWOW jump tables (GF(2) matrix powers), and launches the kernels on one HIP stream.
+// cpt_capi.cpp — implementation of the C-ABI in include/cpt.h: contexts, frames, the RNG init,
+// render launches, the row-tile gather, counters and the display path.  The scene half
+// (upload, material slots, walk trees, device refit) is cpt_scene.cpp; the host BVH builds and
+// the XORWOW tables are cpt_host_bvh.cpp / cpt_host_rng.cpp.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cfloat>
 #include <cmath>
@@ -14,13 +14,10 @@
 #include <cstring>
 #include <mutex>
 #include <new>
-#include <queue>
 #include <string>
-#include <functional>
 #include <vector>
 
-#include "../../include/cpt.h"
-#include "cpt_internal.hpp"
+#include "cpt_context.hpp"
 
 static_assert(sizeof(cpt_material) == 40, "cpt_material must match Material (40 B)");
 static_assert(sizeof(cpt_object) == 72, "cpt_object must match Object (72 B)");
@@ -28,389 +25,15 @@ static_assert(sizeof(cpt_camera) == 136, "cpt_camera must match MotionalCamera (
 static_assert(offsetof(cpt_object, center) == 48, "Object::center_ offset");
 static_assert(offsetof(cpt_material, refractive_index) == 24, "Material::refractive_index_ offset");
 
+using namespace cpt::host;
+using namespace cpt::ctx;
+
 namespace {
-
-using cpt::Mat;
-using cpt::Node;
-using cpt::TexDesc;
-
 std::string g_create_error;
-
-// ------------------------------------------------------------------------------------
-// Host BVH: SceneBVH::Divide (bvh.cu:31-90) and the skip-link linearisation.
-// ------------------------------------------------------------------------------------
-struct F3 { float x, y, z; };
-
-inline float MIN_(float a, float b) { return a < b ? a : b; }   // ray_tracing_math.hpp:19-21
-inline float MAX_(float a, float b) { return a > b ? a : b; }   // ray_tracing_math.hpp:15-17
-inline float ABS_(float a) { return a >= 0 ? a : -a; }          // ray_tracing_math.hpp:23-25
-
-// Object::GetAABBMax / GetAABBMin (object.cu:134-170)
-F3 aabb_max(const cpt_object& o) {
-    const float tol = 2e-5f * 5.f;
-    switch (o.type) {
-        case CPT_PRIM_SPHERE: {
-            float r = ABS_(o.radius);
-            return F3{o.center.x + r, o.center.y + r, o.center.z + r};
-        }
-        case CPT_PRIM_PLATFORM: return F3{1e30f * 5, o.y_pos + tol, 1e30f * 5};
-        case CPT_PRIM_CYLINDER:
-            return F3{o.center.x + ABS_(o.radius), o.center.y + o.height / 2 + tol, o.center.z + ABS_(o.radius)};
-        default: return F3{0, 0, 0};
-    }
-}
-
-F3 aabb_min(const cpt_object& o) {
-    const float tol = 2e-5f * 5.f;
-    switch (o.type) {
-        case CPT_PRIM_SPHERE: {
-            float r = ABS_(o.radius);
-            return F3{o.center.x - r, o.center.y - r, o.center.z - r};
-        }
-        case CPT_PRIM_PLATFORM: return F3{-1e30f * 5, o.y_pos - tol, -1e30f * 5};
-        case CPT_PRIM_CYLINDER:
-            return F3{o.center.x - ABS_(o.radius), o.center.y - o.height / 2 - tol, o.center.z - ABS_(o.radius)};
-        default: return F3{0, 0, 0};
-    }
-}
-
-struct BNode {            // bvh.h:32-38, object stored as an index
-    F3 bmin, bmax;
-    bool is_object;
-    int left, right, obj, parent;
-    int axis;              // split axis of an internal node (its children's centroid order)
-};
-
-struct HostBvh {
-    std::vector<BNode> nodes;          // Divide creation order (reference order)
-    std::vector<int> leaf_of_object;   // object index -> node
-};
-
-int divide(HostBvh& b, const std::vector<cpt_object>& objs, std::vector<int>& idx, int l, int r) {
-    if (l >= r) return -1;
-    int ret = (int)b.nodes.size();
-    b.nodes.push_back(BNode{});
-    F3 lmin = aabb_min(objs[idx[l]]), lmax = aabb_max(objs[idx[l]]);
-    if (l == r - 1) {
-        BNode& n = b.nodes[ret];
-        n.left = n.right = -1;
-        n.bmin = lmin; n.bmax = lmax;
-        n.is_object = true;
-        n.obj = idx[l];
-        b.leaf_of_object[idx[l]] = ret;
-        return ret;
-    }
-    float minx = lmin.x, miny = lmin.y, minz = lmin.z, maxx = lmax.x, maxy = lmax.y, maxz = lmax.z;
-    for (int i = l + 1; i < r; ++i) {
-        F3 a = aabb_min(objs[idx[i]]), c = aabb_max(objs[idx[i]]);
-        minx = MIN_(minx, a.x); miny = MIN_(miny, a.y); minz = MIN_(minz, a.z);
-        maxx = MAX_(maxx, c.x); maxy = MAX_(maxy, c.y); maxz = MAX_(maxz, c.z);
-    }
-    float sx = maxx - minx, sy = maxy - miny, sz = maxz - minz;
-    int axis = (sx >= sy && sx >= sz) ? 0 : (sy >= sz ? 1 : 2);
-    // Centroids precomputed once per split (the reference recomputes them in the comparator);
-    // stable order for equal centroids (std::sort's tie order is implementation-defined).
-    std::vector<std::pair<float, int>> keyed;
-    keyed.reserve(r - l);
-    for (int i = l; i < r; ++i) {
-        F3 a = aabb_min(objs[idx[i]]), c = aabb_max(objs[idx[i]]);
-        float lo = axis == 0 ? a.x : axis == 1 ? a.y : a.z;
-        float hi = axis == 0 ? c.x : axis == 1 ? c.y : c.z;
-        keyed.emplace_back((lo + hi) / 2, idx[i]);
-    }
-    std::stable_sort(keyed.begin(), keyed.end(),
-                     [](const std::pair<float, int>& p, const std::pair<float, int>& q) { return p.first < q.first; });
-    for (int i = l; i < r; ++i) idx[i] = keyed[i - l].second;
-    int mid = (l + r) / 2;
-    int left = divide(b, objs, idx, l, mid);
-    int right = divide(b, objs, idx, mid, r);
-    BNode& n = b.nodes[ret];
-    n.left = left; n.right = right;
-    n.bmin = F3{minx, miny, minz};
-    n.bmax = F3{maxx, maxy, maxz};
-    n.is_object = false;
-    n.obj = -1;
-    n.axis = axis;
-    b.nodes[left].parent = ret;
-    b.nodes[right].parent = ret;
-    return ret;
-}
-
-void build_host_bvh(HostBvh& b, const std::vector<cpt_object>& objs) {
-    b.nodes.clear();
-    b.leaf_of_object.assign(objs.size(), -1);
-    if (objs.empty()) return;
-    b.nodes.reserve(2 * objs.size());
-    std::vector<int> idx(objs.size());
-    for (size_t i = 0; i < objs.size(); ++i) idx[i] = (int)i;
-    divide(b, objs, idx, 0, (int)objs.size());
-    b.nodes[0].parent = -1;
-}
-
-// The cap-disk bound of a cylinder leaf (Node::b1, cpt_path.hpp cap_test): the largest float c
-// with  sqrtf(q) < radius  <=>  q <= c  for every float q.  sqrtf is correctly rounded, so
-// sqrtf(q) < r  <=>  sqrtf(q) <= pred(r)  <=>  sqrt(q) < m, m = (pred(r) + r) / 2 (a tie at m
-// is impossible: m has 25 significant bits, so m^2 has at least 49 and is no float)  <=>
-// q < m^2 (exact in double)  <=>  q <= RD(m^2).  radius <= 0 or NaN: never (c = -1).
-float cap_disk_bound(float r) {
-    if (!(r > 0.0f)) return -1.0f;
-    if (r == INFINITY) return FLT_MAX;
-    const double m = ((double)std::nextafter(r, 0.0f) + (double)r) * 0.5;
-    const double x = m * m;
-    float c = (float)x;
-    if ((double)c > x) c = std::nextafter(c, -INFINITY);
-    return c;
-}
-
-// Node contents: internal -> its box; leaf -> the primitive inline (cpt_device.hpp Node).
-Node make_node(const BNode& n, const std::vector<cpt_object>& objs, const std::vector<int>& mat_of_obj) {
-    Node g;
-    if (n.is_object) {
-        const cpt_object& o = objs[n.obj];
-        g.a0 = o.center.x; g.a1 = o.center.y; g.a2 = o.center.z;
-        g.b0 = o.radius; g.b1 = o.y_pos; g.b2 = o.height;
-        int type = (o.type >= 0 && o.type <= 2) ? o.type : 3;
-        if (type == CPT_PRIM_CYLINDER) g.b1 = cap_disk_bound(o.radius);   // y_pos is a platform's
-        if (type == CPT_PRIM_SPHERE) {
-            // the root-1 normal's exact quotients (cpt_path.hpp hit_attributes): the correctly
-            // rounded double reciprocal of the radius, its low word in b1 and high word in b2
-            const double inv_r = 1.0 / (double)o.radius;
-            uint32_t w[2];
-            std::memcpy(w, &inv_r, 8);
-            std::memcpy(&g.b1, &w[0], 4);
-            std::memcpy(&g.b2, &w[1], 4);
-        }
-        g.code = (mat_of_obj[n.obj] << 2) | type;
-    } else {
-        g.a0 = n.bmin.x; g.a1 = n.bmin.y; g.a2 = n.bmin.z;
-        g.b0 = n.bmax.x; g.b1 = n.bmax.y; g.b2 = n.bmax.z;
-        g.code = -1;
-    }
-    g.miss = -1;
-    return g;
-}
-
-// Right-first preorder = the order the reference's stack DFS pops nodes (left pushed first,
-// bvh.cu:201-202).  Internal nodes: miss = position after the node's subtree.  Leaves: the
-// walk always continues at position + 1, so `miss` carries the leaf's position in this
-// reference order instead (the tie rank of the ordered walk, cpt_path.hpp trace).
-//
-// octant >= 0 builds the near-first order for rays whose direction signs are the octant's
-// bits (bit a set = negative along axis a): at each internal node the child on the near side
-// of its split axis comes first.  ref_pos gives the leaves' reference positions.
-void linearise(const HostBvh& b, const std::vector<cpt_object>& objs, const std::vector<int>& mat_of_obj,
-               std::vector<Node>& out, std::vector<int>& pos_of_node, int octant, const std::vector<int>* ref_pos,
-               int root = 0, const std::vector<int>& prefix = {}) {
-    const size_t base = out.size();
-    pos_of_node.assign(b.nodes.size(), -1);
-    for (int leaf : prefix) {            // unbounded leaves, tested before the tree
-        pos_of_node[leaf] = (int)(out.size() - base);
-        out.push_back(make_node(b.nodes[leaf], objs, mat_of_obj));
-        out.back().miss = (*ref_pos)[leaf];
-    }
-    if (b.nodes.empty() || root < 0) return;
-    struct Frame { int node; int stage; };
-    std::vector<Frame> st;
-    st.push_back({root, 0});
-    while (!st.empty()) {
-        Frame& f = st.back();
-        const BNode& n = b.nodes[f.node];
-        if (f.stage == 0) {
-            pos_of_node[f.node] = (int)(out.size() - base);
-            out.push_back(make_node(n, objs, mat_of_obj));
-            if (n.is_object) {
-                out.back().miss = ref_pos ? (*ref_pos)[f.node] : pos_of_node[f.node];
-                st.pop_back();
-                continue;
-            }
-            if (octant >= 0) {
-                // octant form (cpt_path.hpp slab_reject_octant): a = the planes a ray of this
-                // octant enters through, b = the ones it leaves through (bmax first on an
-                // axis the ray runs down)
-                Node& q = out.back();
-                if (octant & 1) std::swap(q.a0, q.b0);
-                if (octant & 2) std::swap(q.a1, q.b1);
-                if (octant & 4) std::swap(q.a2, q.b2);
-            }
-            f.stage = 1;
-            // the reference pops the right child first; a ray moving +axis meets the left
-            // (lower-centroid) child first
-            const bool right_first = octant < 0 || ((octant >> n.axis) & 1);
-            st.push_back({right_first ? n.right : n.left, 0});
-        } else if (f.stage == 1) {
-            f.stage = 2;
-            const bool right_first = octant < 0 || ((octant >> n.axis) & 1);
-            st.push_back({right_first ? n.left : n.right, 0});
-        } else {
-            out[base + pos_of_node[f.node]].miss = (int)(out.size() - base);
-            st.pop_back();
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------
-// XORWOW jump tables: jumps[t] = A^(2^67 * 2^t), 160x160 over GF(2), column-major
-// (column c = A^k e_c as 5 words), the layout rocRAND uses (rocrand_xorwow.h:51-65).
-// ------------------------------------------------------------------------------------
-struct BitMat { uint32_t m[800]; };
-
-void xorshift_step(uint32_t v[5]) {   // linear part of curand() (d excluded)
-    uint32_t t = v[0] ^ (v[0] >> 2);
-    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
-    v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
-}
-
-void bm_apply(const BitMat& M, const uint32_t in[5], uint32_t out[5]) {
-    uint32_t r[5] = {0, 0, 0, 0, 0};
-    for (int c = 0; c < 160; ++c)
-        if ((in[c >> 5] >> (c & 31)) & 1u)
-            for (int k = 0; k < 5; ++k) r[k] ^= M.m[c * 5 + k];
-    std::memcpy(out, r, sizeof(r));
-}
-
-BitMat bm_square(const BitMat& M) {
-    BitMat R;
-    for (int c = 0; c < 160; ++c) bm_apply(M, &M.m[c * 5], &R.m[c * 5]);
-    return R;
-}
-
-const std::vector<uint32_t>& jump_tables() {
-    static std::vector<uint32_t> tbl;
-    static std::once_flag once;
-    std::call_once(once, [] {
-        BitMat A;
-        for (int c = 0; c < 160; ++c) {
-            uint32_t v[5] = {0, 0, 0, 0, 0};
-            v[c >> 5] = 1u << (c & 31);
-            xorshift_step(v);
-            std::memcpy(&A.m[c * 5], v, 20);
-        }
-        for (int i = 0; i < 67; ++i) A = bm_square(A);
-        tbl.resize(64 * 800);
-        for (int t = 0; t < 64; ++t) {
-            std::memcpy(&tbl[(size_t)t * 800], A.m, sizeof(A.m));
-            A = bm_square(A);
-        }
-    });
-    return tbl;
-}
-
-// curand_init's seed scrambling (curand_kernel.h, CUDA 11.7).
-void curand_seed_state(uint64_t seed, uint32_t out[6]) {
-    uint32_t s0 = (uint32_t)seed ^ 0xaad26b49u;
-    uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
-    uint32_t t0 = 1099087573u * s0;
-    uint32_t t1 = 2591861531u * s1;
-    out[0] = 123456789u + t0;
-    out[1] = 362436069u ^ t0;
-    out[2] = 521288629u + t1;
-    out[3] = 88675123u ^ t1;
-    out[4] = 5783321u + t0;
-    out[5] = 6615241u + t1 + t0;
-}
-
 }  // namespace
 
-// ======================================================================================
-// Context
-// ======================================================================================
-struct cpt_ctx {
-    int device = 0;
-    hipStream_t own_stream = nullptr;
-    hipStream_t user_stream = nullptr;
-    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-    hipEvent_t ev_main = nullptr;   // after the cost schedule's pilot: the dominant kernel(s) only
-    bool have_timing = false;
-    std::string err;
-
-    // scene
-    std::vector<cpt_object> objs;
-    HostBvh bvh;
-    std::vector<Node> lin;             // 9 orders of n_bvh nodes: reference, then octants 0..7
-    std::vector<int> pos_of_node;      // BNode -> position in the reference order
-    int n_bvh = 0;                     // nodes of the reference order
-    int n_walk = 0;                    // nodes of each octant order (walk tree + unbounded leaves)
-    int n_wide = 0;                    // 4-wide walk-tree nodes per octant (0: none, binary walk)
-    int n_unb = 0;                     // unbounded (platform) leaves at the head of each octant order
-    int n_leaves = 0;                  // the wide tree's leaf array (after its compact image)
-    std::vector<Mat> mats_h;           // deduplicated materials (host-staged, see Mat)
-    std::vector<int> mat_have_tex;     // per material slot: textured?
-    std::vector<uint64_t> mat_tex;     // per material slot: texture handle (textured slots)
-    std::vector<int> mat_of_obj;       // object index -> material index
-    Node* d_nodes = nullptr;
-    Mat* d_mats = nullptr;
-    size_t cap_nodes = 0, cap_mats = 0;
-    bool scene_set = false;
-    // device refit (cpt_update_objects): the plan of both trees (ids: reference tree, then walk
-    // tree), parents, heights, each object's walk-tree leaf, the boxes as built
-    std::vector<cpt::RefitNode> refit_plan;
-    std::vector<int32_t> refit_parent, refit_height, refit_walk_leaf;
-    std::vector<cpt::Box6> refit_boxes;
-    std::vector<uint8_t> refit_mark;   // scratch of an update batch (all zero between batches)
-    int refit_n_ref = 0;
-    cpt::RefitNode* d_refit_plan = nullptr;
-    cpt::Box6* d_refit_boxes = nullptr;
-    uint8_t* d_refit_work = nullptr;   // an update batch: RefitLeaf records, then the dirty node ids
-    size_t cap_refit_plan = 0, cap_refit_boxes = 0, cap_refit_work = 0;
-    float last_update_ms = 0.f;     // host wall time of the last cpt_update_objects[_rebuild]
-
-    // material textures (cpt_bind_texture)
-    struct Texture { uint64_t handle; uint32_t* d_texels; int w, h, cols, addr, filter; };
-    std::vector<Texture> textures;
-    TexDesc* d_texdescs = nullptr;
-    int32_t* d_tex_of_mat = nullptr;
-    size_t cap_texdescs = 0, cap_tex_of_mat = 0;
-
-    // environment
-    uint32_t* d_env = nullptr;
-    int env_w = 1, env_h = 1, env_cols = 0;
-    size_t cap_env = 0;
-
-    // frame
-    int width = 0, height = 0, n_rows = 0;
-    std::vector<int32_t> rows_h;
-    int32_t* d_rows = nullptr;
-    uint32_t* d_rng = nullptr;
-    float4* d_accum = nullptr;
-    float* d_normal = nullptr;
-    float* d_depth = nullptr;
-    bool frame_set = false, rng_set = false;
-
-    // rng init
-    uint32_t* d_jumps = nullptr;
-    uint32_t* d_scratch_w = nullptr;
-    uint32_t* d_scratch_m = nullptr;
-
-    unsigned long long* d_stats = nullptr;
-    uint32_t* d_work = nullptr;
-    void* d_sched = nullptr;     // cost schedule: pilot tile costs + sort scratch
-    size_t cap_sched = 0;
-    uint32_t* d_tile_order = nullptr;
-    size_t cap_tile_order = 0;
-    uint4* d_resume = nullptr;          // tail consolidation: handed-over chains (5 x uint4 each)
-    size_t cap_resume = 0;
-    cpt::WfState wf{};           // wavefront path state (allocated on first use)
-    bool wf_ready = false;
-    float* d_mix = nullptr;      // display running mean (Mix), rgb per pixel of the display band
-    uint8_t* d_bgra = nullptr;   // display frame (band rows)
-    int band_y0 = -1, band_y1 = -1;   // display band the buffers hold
-    float last_kernel_ms = 0.f;
-    int last_launches = 0;
-    // row-tile gather (cpt_gather_rows): a source's rows staged on this device, and the frame
-    // row each goes to
-    float4* d_gather = nullptr;
-    size_t cap_gather = 0;
-    int32_t* d_gather_map = nullptr;
-    size_t cap_gather_map = 0;
-    std::vector<int32_t> gather_map_h;
-    // consolidation test hooks (cpt_set_debug_consolidation)
-    uint32_t dbg = 0;
-    int keeper_spin_log2 = 0, publish_wait_log2 = 0;
-
-    hipStream_t stream() const { return user_stream ? user_stream : own_stream; }
-};
-
-namespace {
+namespace cpt {
+namespace ctx {
 
 int fail(cpt_ctx* c, int code, const char* fmt, ...) {
     char buf[512];
@@ -421,24 +44,6 @@ int fail(cpt_ctx* c, int code, const char* fmt, ...) {
     if (c) c->err = buf;
     else g_create_error = buf;
     return code;
-}
-
-#define HIP_TRY(ctx, expr)                                                                             \
-    do {                                                                                               \
-        hipError_t e_ = (expr);                                                                        \
-        if (e_ != hipSuccess)                                                                          \
-            return fail((ctx), e_ == hipErrorOutOfMemory ? CPT_ERR_OUT_OF_MEMORY : CPT_ERR_HIP,        \
-                        "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__);           \
-    } while (0)
-
-template <typename T>
-int ensure(cpt_ctx* c, T** ptr, size_t* cap, size_t count) {
-    if (*ptr && *cap >= count) return CPT_OK;
-    if (*ptr) { (void)hipFree(*ptr); *ptr = nullptr; *cap = 0; }
-    if (count == 0) return CPT_OK;
-    HIP_TRY(c, hipMalloc((void**)ptr, count * sizeof(T)));
-    *cap = count;
-    return CPT_OK;
 }
 
 void free_frame(cpt_ctx* c) {
@@ -471,380 +76,17 @@ void free_frame(cpt_ctx* c) {
     c->frame_set = c->rng_set = false;
 }
 
-// Host staging of a Mat (cpt_device.hpp): att = kd_ (the union's bits: the handle's for a
-// textured material), rad.x = emit_intensity_; k_prepare_materials completes it.
-Mat to_mat(const cpt_material& m) {
-    Mat g;
-    std::memset(&g, 0, sizeof(g));
-    g.att_x = m.u.kd.x; g.att_y = m.u.kd.y; g.att_z = m.u.kd.z;
-    g.type = m.type;
-    g.rad_x = m.emit_intensity;
-    g.ior = m.refractive_index;
-    g.reflectivity = m.reflectivity;
-    g.smoothness = m.smoothness;
-    g.inv_alpha = 0.0;
-    return g;
-}
-
-int material_slot(cpt_ctx* c, const cpt_material& m) {
-    Mat g = to_mat(m);
-    const int tex = m.have_tex ? 1 : 0;
-    for (size_t i = 0; i < c->mats_h.size(); ++i)
-        if (std::memcmp(&c->mats_h[i], &g, sizeof(Mat)) == 0 && c->mat_have_tex[i] == tex &&
-            (!tex || c->mat_tex[i] == m.u.tex))
-            return (int)i;
-    c->mats_h.push_back(g);
-    c->mat_have_tex.push_back(tex);
-    c->mat_tex.push_back(tex ? m.u.tex : 0);
-    return (int)c->mats_h.size() - 1;
-}
-
-// Walk tree of the ordered walk (CPT_TRAVERSAL_ORDERED, DESIGN.md §Ordered walk): a binned
-// SAH tree over the bounded primitives, one primitive per leaf.  Platforms (+-5e30 boxes) stay
-// out of it: the walk tests them first.  The tree only decides which primitives a ray tests;
-// the closest hit is the reference's (rank tie rule, conservative slab test, winner
-// certificate in cpt_path.hpp).
-namespace sah {
-constexpr int NB = 16;
-inline float comp(const F3& v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
-inline F3 fmin3(const F3& a, const F3& b) { return F3{MIN_(a.x, b.x), MIN_(a.y, b.y), MIN_(a.z, b.z)}; }
-inline F3 fmax3(const F3& a, const F3& b) { return F3{MAX_(a.x, b.x), MAX_(a.y, b.y), MAX_(a.z, b.z)}; }
-inline float area(const F3& lo, const F3& hi) {
-    const float dx = hi.x - lo.x, dy = hi.y - lo.y, dz = hi.z - lo.z;
-    return 2.f * (dx * dy + dy * dz + dz * dx);
-}
-inline int bin_of(float c, float e0, float e1) { return std::min(NB - 1, (int)((c - e0) / (e1 - e0) * NB)); }
-
-int leaf(HostBvh& t, const std::vector<cpt_object>& O, int o) {
-    BNode n{};
-    n.bmin = aabb_min(O[o]);
-    n.bmax = aabb_max(O[o]);
-    n.is_object = true;
-    n.left = n.right = -1;
-    n.obj = o;
-    n.parent = -1;
-    t.nodes.push_back(n);
-    return (int)t.nodes.size() - 1;
-}
-
-int build(HostBvh& t, const std::vector<cpt_object>& O, std::vector<int>& idx, int l, int r) {
-    if (r - l == 1) return leaf(t, O, idx[l]);
-    F3 lo = aabb_min(O[idx[l]]), hi = aabb_max(O[idx[l]]);
-    F3 clo{1e30f, 1e30f, 1e30f}, chi{-1e30f, -1e30f, -1e30f};
-    std::vector<float> cen(3 * (r - l));
-    for (int i = l; i < r; ++i) {
-        const F3 a = aabb_min(O[idx[i]]), b = aabb_max(O[idx[i]]);
-        lo = fmin3(lo, a);
-        hi = fmax3(hi, b);
-        const F3 c{(a.x + b.x) * .5f, (a.y + b.y) * .5f, (a.z + b.z) * .5f};
-        cen[3 * (i - l)] = c.x; cen[3 * (i - l) + 1] = c.y; cen[3 * (i - l) + 2] = c.z;
-        clo = fmin3(clo, c);
-        chi = fmax3(chi, c);
-    }
-    float best = 3.0e38f;
-    int best_axis = -1, best_bin = -1;
-    for (int axis = 0; axis < 3; ++axis) {
-        const float e0 = comp(clo, axis), e1 = comp(chi, axis);
-        if (!(e1 > e0)) continue;
-        int cnt[NB] = {0};
-        F3 blo[NB], bhi[NB];
-        for (int b = 0; b < NB; ++b) { blo[b] = F3{1e30f, 1e30f, 1e30f}; bhi[b] = F3{-1e30f, -1e30f, -1e30f}; }
-        for (int i = l; i < r; ++i) {
-            const int b = bin_of(cen[3 * (i - l) + axis], e0, e1);
-            cnt[b]++;
-            blo[b] = fmin3(blo[b], aabb_min(O[idx[i]]));
-            bhi[b] = fmax3(bhi[b], aabb_max(O[idx[i]]));
-        }
-        for (int sp = 1; sp < NB; ++sp) {
-            int nl = 0, nr = 0;
-            F3 llo{1e30f, 1e30f, 1e30f}, lhi{-1e30f, -1e30f, -1e30f}, rlo = llo, rhi = lhi;
-            for (int b = 0; b < sp; ++b) if (cnt[b]) { nl += cnt[b]; llo = fmin3(llo, blo[b]); lhi = fmax3(lhi, bhi[b]); }
-            for (int b = sp; b < NB; ++b) if (cnt[b]) { nr += cnt[b]; rlo = fmin3(rlo, blo[b]); rhi = fmax3(rhi, bhi[b]); }
-            if (!nl || !nr) continue;
-            const float cost = area(llo, lhi) * nl + area(rlo, rhi) * nr;
-            if (cost < best) { best = cost; best_axis = axis; best_bin = sp; }
-        }
-    }
-    int axis, mid;
-    if (best_axis < 0) {
-        // all centroids coincide: split the list in half (stable order)
-        axis = 0;
-        mid = (l + r) / 2;
-    } else {
-        axis = best_axis;
-        const float e0 = comp(clo, axis), e1 = comp(chi, axis);
-        std::vector<int> lhs, rhs;
-        for (int i = l; i < r; ++i)
-            (bin_of(cen[3 * (i - l) + axis], e0, e1) < best_bin ? lhs : rhs).push_back(idx[i]);
-        std::copy(lhs.begin(), lhs.end(), idx.begin() + l);
-        std::copy(rhs.begin(), rhs.end(), idx.begin() + l + (int)lhs.size());
-        mid = l + (int)lhs.size();
-    }
-    const int me = (int)t.nodes.size();
-    t.nodes.push_back(BNode{});
-    const int L = build(t, O, idx, l, mid), R = build(t, O, idx, mid, r);
-    BNode& n = t.nodes[me];
-    n.bmin = lo; n.bmax = hi;
-    n.is_object = false;
-    n.left = L; n.right = R; n.obj = -1; n.parent = -1; n.axis = axis;
-    t.nodes[L].parent = me;
-    t.nodes[R].parent = me;
-    return me;
-}
-}  // namespace sah
-
-// ------------------------------------------------------------------------------------
-// 4-wide walk tree (DESIGN.md §Wide walk).  The binary SAH walk tree is collapsed into
-// nodes of up to four children: starting from a node's two children, the internal child
-// with the largest box is replaced by its own two children until there are four (or only
-// leaves).  Appended to `out` (after the eight binary octant orders): the compact image,
-// 7 x 16 B per node (layout below), then the leaf array.  Nodes are numbered largest box
-// first (root 0).  Returns n_wide, or 0 when the device walk's stack (WIDE_STACK entries per
-// lane, cpt_path.hpp) could overflow on this tree or a ref would not fit 15 bits.
-// ------------------------------------------------------------------------------------
-constexpr int WIDE_STACK = CPT_WSTACK;
-
-int linearise_wide(const HostBvh& w, int root, const std::vector<int>& pos0, int n_bvh, int n_unb,
-                   std::vector<Node>& out, int* n_leaves_out, std::vector<int>& slot_of, std::vector<int>& leaf_of) {
-    std::vector<int> wbin;                      // binary node of each wide node
-    std::vector<std::vector<int>> kids;         // its children (binary node ids)
-    std::vector<int> wide_of(w.nodes.size(), -1);
-    auto area = [&](int b) {
-        const BNode& n = w.nodes[b];
-        const float dx = n.bmax.x - n.bmin.x, dy = n.bmax.y - n.bmin.y, dz = n.bmax.z - n.bmin.z;
-        return dx * dy + dy * dz + dz * dx;
-    };
-    int max_push = 0;
-    std::function<void(int, int)> make = [&](int b, int pushed) {
-        const int id = (int)wbin.size();
-        wbin.push_back(b);
-        wide_of[b] = id;
-        std::vector<int> ch = {w.nodes[b].left, w.nodes[b].right};
-        while (ch.size() < 4) {
-            int best = -1;
-            float ba = -1.f;
-            for (size_t k = 0; k < ch.size(); ++k)
-                if (!w.nodes[ch[k]].is_object && area(ch[k]) > ba) { ba = area(ch[k]); best = (int)k; }
-            if (best < 0) break;
-            const int x = ch[best];
-            ch.erase(ch.begin() + best);
-            ch.insert(ch.begin() + best, {w.nodes[x].left, w.nodes[x].right});
-        }
-        kids.push_back(ch);
-        // a lane entering this node keeps one hit child and pushes the others
-        pushed += (int)ch.size() - 1;
-        max_push = std::max(max_push, pushed);
-        for (int x : ch)
-            if (!w.nodes[x].is_object) make(x, pushed);
-    };
-    make(root, n_unb);   // the walk starts with the root and the platforms on the stack
-    if (max_push + 1 > WIDE_STACK) return 0;
-    const int n_wide = (int)wbin.size();
-    // The leaf array after the compact image: the platforms (the head of every octant order),
-    // then the walk tree's leaves in the order the wide nodes, in preorder, first reference
-    // them (a subtree's leaves share cache lines); Node copies of octant 0's inline leaves.
-    // The compact image refers to leaf i as ~(i + 1) (<= -2, apart from the empty slot's -1).
-    std::vector<int> li_of(w.nodes.size(), -1), leaf_pos;
-    for (int k = 0; k < n_unb; ++k) leaf_pos.push_back(k);
-    for (int id = 0; id < n_wide; ++id)
-        for (int x : kids[id])
-            if (w.nodes[x].is_object && li_of[x] < 0) {
-                li_of[x] = (int)leaf_pos.size();
-                leaf_pos.push_back(pos0[x]);
-            }
-    if ((int)leaf_pos.size() > 32765) return 0;
-    // The ids are preorder (make's recursion order), which keeps a subtree's nodes and leaves
-    // together in memory.  A tree larger than the LDS image is renumbered so that its first
-    // LDS_TREE_NODES ids -- the part the device stages in LDS -- are its top: the nodes a
-    // best-first expansion from the root by surface area (which a random ray hits in
-    // proportion to) reaches first, each after its parent; those first, then the rest, each
-    // part in preorder.
-    if (n_wide > cpt::LDS_TREE_NODES) {
-        std::vector<char> top(n_wide, 0);
-        std::priority_queue<std::pair<float, int>, std::vector<std::pair<float, int>>, std::greater<>> pq;
-        pq.emplace(-area(wbin[0]), 0);
-        for (int taken = 0; !pq.empty() && taken < cpt::LDS_TREE_NODES; ++taken) {
-            const int id = pq.top().second;
-            pq.pop();
-            top[id] = 1;
-            for (int x : kids[id])
-                if (!w.nodes[x].is_object) pq.emplace(-area(x), wide_of[x]);
-        }
-        std::vector<int> order;   // new id -> old id: the top in preorder, then the rest
-        order.reserve(n_wide);
-        for (int part = 1; part >= 0; --part)
-            for (int id = 0; id < n_wide; ++id)
-                if (top[id] == part) order.push_back(id);
-        std::vector<int> new_id(n_wide);
-        for (int k = 0; k < n_wide; ++k) new_id[order[k]] = k;
-        std::vector<int> wbin2(n_wide);
-        std::vector<std::vector<int>> kids2(n_wide);
-        for (int k = 0; k < n_wide; ++k) {
-            wbin2[k] = wbin[order[k]];
-            kids2[k] = kids[order[k]];
-        }
-        wbin.swap(wbin2);
-        kids.swap(kids2);
-        for (int& x : wide_of)
-            if (x >= 0) x = new_id[x];
-    }
-    // the device stack holds 16-bit refs: wide node ids and ~(leaf position) within 15 bits
-    if (n_wide > 32767) return 0;
-    for (int p : pos0)
-        if (p > 32766) return 0;
-    const size_t base = out.size();
-    const size_t n_compact = (size_t)(n_wide * 7 + 1) / 2;
-    out.resize(base + n_compact + leaf_pos.size());
-    for (size_t i = 0; i < leaf_pos.size(); ++i) out[base + n_compact + i] = out[(size_t)n_bvh + leaf_pos[i]];
-    *n_leaves_out = (int)leaf_pos.size();
-    // The compact image (cpt_path.hpp trace_wide; its first LDS_TREE_NODES nodes are staged in
-    // LDS): 7 x 16 B per node, one copy for every direction octant --
-    //   [min x][max x][min y][max y][min z][max z] of the four slots, then
-    //   {refs of slots 0..3 as int16, 8 B zero}.
-    // A lane reads its entry planes at min or max by the sign of its direction, i.e. the planes
-    // its octant enters through, and orders the hit children by their entry distances.  The
-    // slots are in the order of the binary splits between the node and its children (left
-    // first); an empty slot has an inverted box that every ray rejects.
-    uint32_t* compact = reinterpret_cast<uint32_t*>(&out[base]);
-    std::memset(compact, 0, n_compact * sizeof(Node));
-    for (int id = 0; id < n_wide; ++id) {
-        const std::vector<int>& ch = kids[id];
-        std::vector<int> ord;
-        std::function<void(int)> rec = [&](int x) {
-            if (std::find(ch.begin(), ch.end(), x) != ch.end()) { ord.push_back(x); return; }
-            rec(w.nodes[x].left);
-            rec(w.nodes[x].right);
-        };
-        rec(wbin[id]);
-        uint32_t* q = compact + (size_t)id * 28;
-        for (int k = 0; k < 4; ++k) {
-            F3 lo{1e30f, 1e30f, 1e30f}, hi{-1e30f, -1e30f, -1e30f};
-            int32_t r = -1;
-            if (k < (int)ord.size()) {
-                const BNode& n = w.nodes[ord[k]];
-                lo = n.bmin;
-                hi = n.bmax;
-                r = n.is_object ? ~(li_of[ord[k]] + 1) : wide_of[ord[k]];
-            }
-            const float l3[3] = {lo.x, lo.y, lo.z}, h3[3] = {hi.x, hi.y, hi.z};
-            for (int a = 0; a < 3; ++a) {
-                std::memcpy(&q[(2 * a) * 4 + k], &l3[a], 4);
-                std::memcpy(&q[(2 * a + 1) * 4 + k], &h3[a], 4);
-            }
-            q[24 + (k >> 1)] |= (uint32_t)(uint16_t)(int16_t)r << (16 * (k & 1));
-            if (k < (int)ord.size()) slot_of[ord[k]] = id * 4 + k;
-        }
-    }
-    // the device refit's map (binary walk node -> leaf array index; the platforms are its head)
-    leaf_of = li_of;
-    for (size_t b = 0; b < w.nodes.size(); ++b)
-        if (w.nodes[b].is_object && leaf_of[b] < 0 && pos0[b] >= 0 && pos0[b] < n_unb) leaf_of[b] = pos0[b];
-    return n_wide;
-}
-
-// Returns the walk tree's root (-1: no bounded primitive); `unbounded` = its platform leaves
-// by reference rank; `rank` = the reference rank of every walk-tree leaf.
-int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, std::vector<int>& rank);
-
-// The reference order followed by the eight octant orders of the walk tree (one array,
-// n_walk nodes each: the unbounded leaves, then the tree).
-void build_refit_plan(cpt_ctx* c, const HostBvh& w, const std::vector<int> (&pos)[8], const std::vector<int>& slot_of,
-                      const std::vector<int>& leaf_of);
-
-void linearise_all(cpt_ctx* c) {
-    c->lin.clear();
-    c->n_walk = 0;
-    c->n_wide = 0;
-    c->n_unb = 0;
-    c->refit_plan.clear();
-    c->lin.reserve(9 * c->bvh.nodes.size());
-    linearise(c->bvh, c->objs, c->mat_of_obj, c->lin, c->pos_of_node, -1, nullptr);
-    c->n_bvh = (int)c->lin.size();
-    if (c->n_bvh == 0) return;
-    HostBvh w;
-    std::vector<int> unbounded, rank, pos[8];
-    const int root = build_walk_tree(c, w, unbounded, rank);
-    for (int o = 0; o < 8; ++o) linearise(w, c->objs, c->mat_of_obj, c->lin, pos[o], o, &rank, root, unbounded);
-    c->n_walk = (int)(c->lin.size() - c->n_bvh) / 8;
-    c->n_unb = (int)unbounded.size();
-    c->n_leaves = 0;
-    std::vector<int> slot_of(w.nodes.size(), -1), leaf_of(w.nodes.size(), -1);
-    if (root >= 0 && !w.nodes[root].is_object)
-        c->n_wide = linearise_wide(w, root, pos[0], c->n_bvh, c->n_unb, c->lin, &c->n_leaves, slot_of, leaf_of);
-    build_refit_plan(c, w, pos, slot_of, leaf_of);
-}
-
-// The device refit's plan (cpt_internal.hpp RefitNode): every node of both trees with the
-// positions of its copies, its parent and its height (leaves 0), and each object's two leaves.
-void build_refit_plan(cpt_ctx* c, const HostBvh& w, const std::vector<int> (&pos)[8], const std::vector<int>& slot_of,
-                      const std::vector<int>& leaf_of) {
-    const int nr = (int)c->bvh.nodes.size(), nw = (int)w.nodes.size();
-    c->refit_n_ref = nr;
-    c->refit_plan.assign(nr + nw, cpt::RefitNode{});
-    c->refit_parent.assign(nr + nw, -1);
-    c->refit_height.assign(nr + nw, 0);
-    c->refit_boxes.assign(nr + nw, cpt::Box6{});
-    c->refit_walk_leaf.assign(c->objs.size(), -1);
-    c->refit_mark.assign(nr + nw, 0);
-    for (int i = 0; i < nr + nw; ++i) {
-        const bool ref = i < nr;
-        const BNode& n = ref ? c->bvh.nodes[i] : w.nodes[i - nr];
-        cpt::RefitNode& r = c->refit_plan[i];
-        const int off = ref ? 0 : nr;
-        r.left = n.is_object ? -1 : n.left + off;
-        r.right = n.is_object ? -1 : n.right + off;
-        r.slot = ref ? -1 : slot_of[i - nr];
-        r.leaf = ref || c->n_wide == 0 ? -1 : leaf_of[i - nr];
-        for (int o = 0; o < 8; ++o) r.pos[o] = -1;
-        if (ref) r.pos[0] = c->pos_of_node[i];
-        else
-            for (int o = 0; o < 8; ++o)
-                r.pos[o] = pos[o][i - nr] < 0 ? -1 : c->n_bvh + o * c->n_walk + pos[o][i - nr];
-        c->refit_boxes[i] = cpt::Box6{{n.bmin.x, n.bmin.y, n.bmin.z}, {n.bmax.x, n.bmax.y, n.bmax.z}};
-        if (!n.is_object) {
-            c->refit_parent[r.left] = i;
-            c->refit_parent[r.right] = i;
-        } else if (!ref) {
-            c->refit_walk_leaf[n.obj] = i;
-        }
-    }
-    // heights, children first: both builders number a parent before its children (bvh.cu:31-90
-    // divide, sah::build)
-    for (int i = nr + nw - 1; i >= 0; --i) {
-        const cpt::RefitNode& r = c->refit_plan[i];
-        if (r.left >= 0)
-            c->refit_height[i] = 1 + std::max(c->refit_height[r.left], c->refit_height[r.right]);
-    }
-}
-
-int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, std::vector<int>& rank) {
-    const std::vector<cpt_object>& O = c->objs;
-    w.nodes.clear();
-    w.leaf_of_object.assign(O.size(), -1);
-    unbounded.clear();
-    std::vector<int> idx;
-    std::vector<std::pair<int, int>> flat;   // (reference rank, object) of the platforms
-    for (size_t o = 0; o < O.size(); ++o) {
-        const int ref_rank = c->pos_of_node[c->bvh.leaf_of_object[o]];
-        if (O[o].type == CPT_PRIM_PLATFORM) flat.emplace_back(ref_rank, (int)o);
-        else idx.push_back((int)o);
-    }
-    std::sort(flat.begin(), flat.end());
-    for (const auto& f : flat) unbounded.push_back(sah::leaf(w, O, f.second));
-    const int root = idx.empty() ? -1 : sah::build(w, O, idx, 0, (int)idx.size());
-    rank.assign(w.nodes.size(), -1);
-    for (size_t i = 0; i < w.nodes.size(); ++i)
-        if (w.nodes[i].is_object) rank[i] = c->pos_of_node[c->bvh.leaf_of_object[w.nodes[i].obj]];
-    return root;
-}
-
 // The kernels' sticky error word (KParams::error, CPT_DEVERR_*): read after the context's
 // stream has drained; a set word is cleared and reported once, like a sticky HIP error.
+// Both the read and the clear run on the context's own stream (a blocking hipMemcpy would
+// synchronise with the legacy default stream and so with other streams' work, e.g. collectives).
 int check_device_error(cpt_ctx* c) {
     uint32_t v = 0;
-    HIP_TRY(c, hipMemcpy(&v, c->d_work + 4, sizeof(v), hipMemcpyDeviceToHost));
+    hipStream_t s = c->stream();
+    HIP_TRY(c, hipMemcpyAsync(&v, c->d_work + 4, sizeof(v), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
     if (v == 0) return CPT_OK;
-    HIP_TRY(c, hipMemset(c->d_work + 4, 0, sizeof(v)));
+    HIP_TRY(c, hipMemsetAsync(c->d_work + 4, 0, sizeof(v), s));
     return fail(c, CPT_ERR_DEVICE, "device error 0x%x:%s%s%s", v,
                 (v & cpt::CPT_DEVERR_KEEPER_TIMEOUT) ? " a keeper wave gave up with chains still live (pixels left unfinished);" : "",
                 (v & cpt::CPT_DEVERR_PUBLISH_TIMEOUT) ? " a handed-over chain was never published (its pixel was not written);" : "",
@@ -858,133 +100,8 @@ int sync_checked(cpt_ctx* c) {
     return check_device_error(c);
 }
 
-int upload_materials(cpt_ctx* c);
-
-int upload_scene(cpt_ctx* c) {
-    if (c->lin.size() * sizeof(Node) > (size_t)INT32_MAX)   // the walk's buffer descriptor range
-        return fail(c, CPT_ERR_UNSUPPORTED, "scene too large: %zu BVH nodes in all orders (max %zu)", c->lin.size(),
-                    (size_t)INT32_MAX / sizeof(Node));
-    HIP_TRY(c, hipSetDevice(c->device));
-    int rc;
-    if ((rc = ensure(c, &c->d_nodes, &c->cap_nodes, std::max<size_t>(1, c->lin.size()))) != CPT_OK) return rc;
-    if ((rc = ensure(c, &c->d_mats, &c->cap_mats, std::max<size_t>(1, c->mats_h.size()))) != CPT_OK) return rc;
-    hipStream_t s = c->stream();
-    if (!c->lin.empty())
-        HIP_TRY(c, hipMemcpyAsync(c->d_nodes, c->lin.data(), c->lin.size() * sizeof(Node), hipMemcpyHostToDevice, s));
-    if (!c->refit_plan.empty()) {   // the device refit's plan and the boxes as built
-        if ((rc = ensure(c, &c->d_refit_plan, &c->cap_refit_plan, c->refit_plan.size())) != CPT_OK) return rc;
-        if ((rc = ensure(c, &c->d_refit_boxes, &c->cap_refit_boxes, c->refit_boxes.size())) != CPT_OK) return rc;
-        HIP_TRY(c, hipMemcpyAsync(c->d_refit_plan, c->refit_plan.data(), c->refit_plan.size() * sizeof(cpt::RefitNode),
-                                  hipMemcpyHostToDevice, s));
-        HIP_TRY(c, hipMemcpyAsync(c->d_refit_boxes, c->refit_boxes.data(), c->refit_boxes.size() * sizeof(cpt::Box6),
-                                  hipMemcpyHostToDevice, s));
-    }
-    if ((rc = upload_materials(c)) != CPT_OK) return rc;
-    HIP_TRY(c, hipStreamSynchronize(s));
-    c->scene_set = true;
-    return CPT_OK;
-}
-
-// The deduplicated materials (and the descriptors of the textures they use), completed on the
-// device by k_prepare_materials.
-int upload_materials(cpt_ctx* c) {
-    int rc;
-    hipStream_t s = c->stream();
-    if (!c->mats_h.empty()) {
-        // textured materials: resolve their handles against the bound textures
-        std::vector<int32_t> tex_of_mat(c->mats_h.size(), -1);
-        bool any = false;
-        for (size_t i = 0; i < c->mats_h.size(); ++i) {
-            if (!c->mat_have_tex[i]) continue;
-            for (size_t t = 0; t < c->textures.size(); ++t)
-                if (c->textures[t].handle == c->mat_tex[i]) tex_of_mat[i] = (int32_t)t;
-            if (tex_of_mat[i] < 0)
-                return fail(c, CPT_ERR_INVALID_ARG, "textured material uses handle %llu, which is not bound (cpt_bind_texture)",
-                            (unsigned long long)c->mat_tex[i]);
-            any = true;
-        }
-        if (any) {
-            std::vector<TexDesc> descs(c->textures.size());
-            for (size_t t = 0; t < descs.size(); ++t) {
-                const auto& x = c->textures[t];
-                descs[t] = TexDesc{x.d_texels, x.w, x.h, x.cols, x.addr, x.filter, 0};
-            }
-            if ((rc = ensure(c, &c->d_texdescs, &c->cap_texdescs, descs.size())) != CPT_OK) return rc;
-            if ((rc = ensure(c, &c->d_tex_of_mat, &c->cap_tex_of_mat, tex_of_mat.size())) != CPT_OK) return rc;
-            HIP_TRY(c, hipMemcpyAsync(c->d_texdescs, descs.data(), descs.size() * sizeof(TexDesc), hipMemcpyHostToDevice, s));
-            HIP_TRY(c, hipMemcpyAsync(c->d_tex_of_mat, tex_of_mat.data(), tex_of_mat.size() * sizeof(int32_t),
-                                      hipMemcpyHostToDevice, s));
-            // the staging vectors must outlive the async copies
-            HIP_TRY(c, hipStreamSynchronize(s));
-        }
-        HIP_TRY(c, hipMemcpyAsync(c->d_mats, c->mats_h.data(), c->mats_h.size() * sizeof(Mat), hipMemcpyHostToDevice, s));
-        HIP_TRY(c, cpt::launch_prepare_materials(c->d_mats, any ? c->d_tex_of_mat : nullptr, any ? c->d_texdescs : nullptr,
-                                                 (int)c->mats_h.size(), s));
-    }
-    return CPT_OK;
-}
-
-// SceneBVH::UpdateObject for a batch, on the device (cpt_kernels.hip k_refit_*): the updated
-// objects are already in c->objs (and the host's reference tree is refit, for
-// cpt_scene_bvh_export).  The host names the updated leaves and the union of their ancestors in
-// both trees, height by height -- O(updates x depth), independent of the scene size -- and the
-// device rewrites every copy: the reference order, the eight octant orders, the 4-wide image and
-// leaf array.  Same topology as built (the reference never rebuilds either); the walk tree keeps
-// its SAH structure, so the ordered walk stays exact (any tree of conservative boxes is) while
-// its efficiency may drift after large motions (cpt_update_objects_rebuild re-optimises).
-int device_refit(cpt_ctx* c, int n, const int* indices, bool mats_changed) {
-    std::vector<int> uniq(indices, indices + n);
-    std::sort(uniq.begin(), uniq.end());
-    uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
-    const int nr = c->refit_n_ref;
-    std::vector<cpt::RefitLeaf> recs(uniq.size());
-    std::vector<int32_t> dirty;
-    std::vector<uint8_t>& mark = c->refit_mark;
-    mark.resize(c->refit_plan.size(), 0);
-    for (size_t k = 0; k < uniq.size(); ++k) {
-        const int o = uniq[k];
-        cpt::RefitLeaf& r = recs[k];
-        r.ref_id = c->bvh.leaf_of_object[o];
-        r.walk_id = c->refit_walk_leaf[o];
-        r.prim = make_node(c->bvh.nodes[r.ref_id], c->objs, c->mat_of_obj);
-        const F3 lo = aabb_min(c->objs[o]), hi = aabb_max(c->objs[o]);
-        r.box = cpt::Box6{{lo.x, lo.y, lo.z}, {hi.x, hi.y, hi.z}};
-        for (int id : {r.ref_id, r.walk_id})
-            for (int p = id < 0 ? -1 : c->refit_parent[id]; p >= 0 && !mark[p]; p = c->refit_parent[p]) {
-                mark[p] = 1;
-                dirty.push_back(p);
-            }
-    }
-    for (int32_t d : dirty) mark[d] = 0;
-    std::stable_sort(dirty.begin(), dirty.end(),
-                     [&](int32_t a, int32_t b) { return c->refit_height[a] < c->refit_height[b]; });
-    std::vector<int32_t> level_end;
-    for (size_t i = 0; i < dirty.size(); ++i)
-        if (i + 1 == dirty.size() || c->refit_height[dirty[i + 1]] != c->refit_height[dirty[i]])
-            level_end.push_back((int32_t)(i + 1));
-    const size_t rec_bytes = recs.size() * sizeof(cpt::RefitLeaf);
-    std::vector<uint8_t> work(rec_bytes + dirty.size() * sizeof(int32_t));
-    std::memcpy(work.data(), recs.data(), rec_bytes);
-    if (!dirty.empty()) std::memcpy(work.data() + rec_bytes, dirty.data(), dirty.size() * sizeof(int32_t));
-    HIP_TRY(c, hipSetDevice(c->device));
-    int rc;
-    if ((rc = ensure(c, &c->d_refit_work, &c->cap_refit_work, work.size())) != CPT_OK) return rc;
-    uint8_t* const d_work = c->d_refit_work;
-    hipStream_t s = c->stream();
-    HIP_TRY(c, hipMemcpyAsync(d_work, work.data(), work.size(), hipMemcpyHostToDevice, s));
-    const size_t image_base = (size_t)c->n_bvh + 8 * (size_t)c->n_walk;
-    uint32_t* image = c->n_wide > 0 ? reinterpret_cast<uint32_t*>(c->d_nodes + image_base) : nullptr;
-    Node* leaves = c->n_wide > 0 ? c->d_nodes + image_base + ((size_t)c->n_wide * 7 + 1) / 2 : nullptr;
-    HIP_TRY(c, cpt::launch_refit(reinterpret_cast<const cpt::RefitLeaf*>(d_work), (int)recs.size(),
-                                 reinterpret_cast<const int32_t*>(d_work + rec_bytes), level_end.data(),
-                                 (int)level_end.size(), nr, c->d_refit_plan, c->d_refit_boxes, c->d_nodes, image, leaves,
-                                 s));
-    if (mats_changed && (rc = upload_materials(c)) != CPT_OK) return rc;
-    // the staging vector must outlive the copy; the render after an update sees the new scene
-    return sync_checked(c);
-}
-
-}  // namespace
+}  // namespace ctx
+}  // namespace cpt
 
 extern "C" {
 
@@ -1027,6 +144,10 @@ int cpt_create(int device, cpt_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&c->ev_start);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_stop);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_main);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev_dn0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev_dn1);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_gathered, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 128 * sizeof(unsigned long long));   // [64..128) execdiag
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_work, 64);   // [0] dequeue counter, [4] error word
     if (e == hipSuccess) e = hipMemset(c->d_work, 0, 64);
@@ -1065,7 +186,11 @@ int cpt_destroy(cpt_ctx* c) {
     (void)hipFree(c->d_work);
     (void)hipFree(c->d_resume);
     (void)hipFree(c->d_gather);
-    (void)hipFree(c->d_gather_map);
+    for (auto& g : c->gather_maps) (void)hipFree(g.d_map);
+    if (c->ev_dn0) (void)hipEventDestroy(c->ev_dn0);
+    if (c->ev_dn1) (void)hipEventDestroy(c->ev_dn1);
+    if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
+    if (c->ev_gathered) (void)hipEventDestroy(c->ev_gathered);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
@@ -1114,177 +239,6 @@ int cpt_camera_get_copy(cpt_camera* cam) {
     return CPT_OK;
 }
 
-int cpt_set_scene(cpt_ctx* c, const cpt_object* objs, int n) {
-    if (!c || n < 0 || (n > 0 && !objs)) return c ? fail(c, CPT_ERR_INVALID_ARG, "cpt_set_scene: bad arguments") : CPT_ERR_INVALID_ARG;
-    c->scene_set = false;   // until the new scene is uploaded
-    try {
-        c->objs.assign(objs, objs + n);
-        build_host_bvh(c->bvh, c->objs);
-        // Objects carry their Material by value (bvh.cu:43); identical materials share one slot.
-        c->mats_h.clear();
-        c->mat_have_tex.clear();
-        c->mat_tex.clear();
-        c->mat_of_obj.assign(n, 0);
-        for (int i = 0; i < n; ++i) c->mat_of_obj[i] = material_slot(c, c->objs[i].material);
-        linearise_all(c);
-    } catch (const std::bad_alloc&) {
-        return fail(c, CPT_ERR_OUT_OF_MEMORY, "cpt_set_scene: host allocation failed");
-    }
-    return upload_scene(c);
-}
-
-// SceneBVH::UpdateObject (bvh.cu:122-157): replace the leaf's object, refit the ancestors
-// (MIN/MAX of the two children per axis), re-upload.
-static int update_objects(cpt_ctx* c, int n, const int* indices, const cpt_object* objs, bool rebuild) {
-    if (!c || n < 0 || (n > 0 && (!indices || !objs))) return CPT_ERR_INVALID_ARG;
-    if (!c->scene_set) return fail(c, CPT_ERR_STATE, "cpt_update_objects: cpt_set_scene first");
-    for (int k = 0; k < n; ++k)
-        if (indices[k] < 0 || indices[k] >= (int)c->objs.size())
-            return fail(c, CPT_ERR_INVALID_ARG, "cpt_update_objects: index %d out of range", indices[k]);
-    if (n == 0) return CPT_OK;
-    const auto t0 = std::chrono::steady_clock::now();
-    // a primitive becoming or ceasing to be a platform changes the walk tree's leaf set: rebuild
-    for (int k = 0; k < n && !rebuild; ++k)
-        if ((c->objs[indices[k]].type == CPT_PRIM_PLATFORM) != (objs[k].type == CPT_PRIM_PLATFORM)) rebuild = true;
-    if (c->refit_plan.empty()) rebuild = true;
-    const size_t n_mats = c->mats_h.size();
-    // SceneBVH::UpdateObject (bvh.cu:144-157) on the host's reference tree (cpt_scene_bvh_export
-    // reads it): the leaf takes the object, its ancestors' boxes become the union of their
-    // children's.  The refit is a function of the leaves only, so the device copies are refit
-    // once per batch below (device_refit), or rebuilt and uploaded once.
-    for (int k = 0; k < n; ++k) {
-        const int index = indices[k];
-        c->objs[index] = objs[k];
-        c->mat_of_obj[index] = material_slot(c, objs[k].material);
-        int ni = c->bvh.leaf_of_object[index];
-        while (ni != -1) {
-            BNode& nd = c->bvh.nodes[ni];
-            if (nd.is_object) {
-                nd.bmax = aabb_max(c->objs[nd.obj]);
-                nd.bmin = aabb_min(c->objs[nd.obj]);
-            } else {
-                const BNode& L = c->bvh.nodes[nd.left];
-                const BNode& R = c->bvh.nodes[nd.right];
-                nd.bmax = F3{MAX_(L.bmax.x, R.bmax.x), MAX_(L.bmax.y, R.bmax.y), MAX_(L.bmax.z, R.bmax.z)};
-                nd.bmin = F3{MIN_(L.bmin.x, R.bmin.x), MIN_(L.bmin.y, R.bmin.y), MIN_(L.bmin.z, R.bmin.z)};
-            }
-            ni = nd.parent;
-        }
-    }
-    int rc;
-    if (rebuild) {
-        // the reference tree keeps its topology (refit above); the walk tree is rebuilt from the
-        // current objects, then all nine orders are re-linearised and uploaded
-        linearise_all(c);
-        rc = upload_scene(c);
-    } else {
-        rc = device_refit(c, n, indices, c->mats_h.size() != n_mats);
-    }
-    c->last_update_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return rc;
-}
-
-int cpt_update_objects(cpt_ctx* c, int n, const int* indices, const cpt_object* objs) {
-    return update_objects(c, n, indices, objs, false);
-}
-
-int cpt_update_objects_rebuild(cpt_ctx* c, int n, const int* indices, const cpt_object* objs) {
-    return update_objects(c, n, indices, objs, true);
-}
-
-int cpt_last_update_ms(cpt_ctx* c, float* ms) {
-    if (!c || !ms) return CPT_ERR_INVALID_ARG;
-    *ms = c->last_update_ms;
-    return CPT_OK;
-}
-
-int cpt_update_object(cpt_ctx* c, int index, const cpt_object* obj) {
-    if (!c || !obj) return CPT_ERR_INVALID_ARG;
-    return cpt_update_objects(c, 1, &index, obj);
-}
-
-int cpt_scene_bvh_export(cpt_ctx* c, float* boxes, int32_t* links, int capacity, int* n_nodes) {
-    if (!c || !n_nodes) return CPT_ERR_INVALID_ARG;
-    int m = (int)c->bvh.nodes.size();
-    *n_nodes = m;
-    for (int i = 0; i < m && i < capacity; ++i) {
-        const BNode& n = c->bvh.nodes[i];
-        if (boxes) {
-            float* b = boxes + 6 * i;
-            b[0] = n.bmin.x; b[1] = n.bmin.y; b[2] = n.bmin.z; b[3] = n.bmax.x; b[4] = n.bmax.y; b[5] = n.bmax.z;
-        }
-        if (links) {
-            int32_t* l = links + 4 * i;
-            l[0] = n.is_object; l[1] = n.left; l[2] = n.right; l[3] = n.obj;
-        }
-    }
-    return CPT_OK;
-}
-
-int cpt_bvh_build_host(const cpt_object* objs, int n, float* boxes, int32_t* links, int capacity, int* n_nodes) {
-    if (n < 0 || (n > 0 && !objs) || !n_nodes) return CPT_ERR_INVALID_ARG;
-    try {
-        std::vector<cpt_object> v(objs, objs + n);
-        HostBvh b;
-        build_host_bvh(b, v);
-        int m = (int)b.nodes.size();
-        *n_nodes = m;
-        for (int i = 0; i < m && i < capacity; ++i) {
-            const BNode& nd = b.nodes[i];
-            if (boxes) {
-                float* x = boxes + 6 * i;
-                x[0] = nd.bmin.x; x[1] = nd.bmin.y; x[2] = nd.bmin.z; x[3] = nd.bmax.x; x[4] = nd.bmax.y; x[5] = nd.bmax.z;
-            }
-            if (links) {
-                int32_t* l = links + 4 * i;
-                l[0] = nd.is_object; l[1] = nd.left; l[2] = nd.right; l[3] = nd.obj;
-            }
-        }
-    } catch (const std::bad_alloc&) {
-        return CPT_ERR_OUT_OF_MEMORY;
-    }
-    return CPT_OK;
-}
-
-int cpt_set_env_texture(cpt_ctx* c, const uint8_t* rgba, int logical_width, int height, int valid_cols) {
-    if (!c) return CPT_ERR_INVALID_ARG;
-    if (logical_width <= 0 || height <= 0 || valid_cols < 0 || valid_cols > logical_width || (valid_cols > 0 && !rgba))
-        return fail(c, CPT_ERR_INVALID_ARG, "cpt_set_env_texture: bad geometry %dx%d cols %d", logical_width, height, valid_cols);
-    HIP_TRY(c, hipSetDevice(c->device));
-    size_t n = (size_t)valid_cols * height;
-    int rc = ensure(c, &c->d_env, &c->cap_env, std::max<size_t>(1, n));
-    if (rc != CPT_OK) return rc;
-    if (n) HIP_TRY(c, hipMemcpy(c->d_env, rgba, n * 4, hipMemcpyHostToDevice));
-    c->env_w = logical_width;
-    c->env_h = height;
-    c->env_cols = valid_cols;
-    return CPT_OK;
-}
-
-int cpt_bind_texture(cpt_ctx* c, uint64_t handle, const uint8_t* rgba, int logical_width, int height, int valid_cols,
-                     int address_mode, int filter_mode) {
-    if (!c) return CPT_ERR_INVALID_ARG;
-    if (logical_width <= 0 || height <= 0 || valid_cols < 0 || valid_cols > logical_width || (valid_cols > 0 && !rgba) ||
-        address_mode < CPT_ADDRESS_WRAP || address_mode > CPT_ADDRESS_BORDER || filter_mode < CPT_FILTER_POINT ||
-        filter_mode > CPT_FILTER_LINEAR)
-        return fail(c, CPT_ERR_INVALID_ARG, "cpt_bind_texture: bad geometry %dx%d cols %d or mode %d/%d", logical_width,
-                    height, valid_cols, address_mode, filter_mode);
-    HIP_TRY(c, hipSetDevice(c->device));
-    const size_t n = (size_t)valid_cols * height;
-    uint32_t* d = nullptr;
-    HIP_TRY(c, hipMalloc((void**)&d, std::max<size_t>(1, n) * 4));
-    if (n) {
-        hipError_t e = hipMemcpy(d, rgba, n * 4, hipMemcpyHostToDevice);
-        if (e != hipSuccess) { (void)hipFree(d); return fail(c, CPT_ERR_HIP, "cpt_bind_texture: %s", hipGetErrorString(e)); }
-    }
-    cpt_ctx::Texture t{handle, d, logical_width, height, valid_cols, address_mode, filter_mode};
-    bool replaced = false;
-    for (auto& x : c->textures)
-        if (x.handle == handle) { (void)hipFree(x.d_texels); x = t; replaced = true; }
-    if (!replaced) c->textures.push_back(t);
-    return c->scene_set ? upload_scene(c) : CPT_OK;   // re-prepare the materials
-}
-
 int cpt_set_frame(cpt_ctx* c, int width, int height, const int32_t* rows, int n_rows) {
     if (!c) return CPT_ERR_INVALID_ARG;
     if (width <= 0 || height <= 0) return fail(c, CPT_ERR_INVALID_ARG, "cpt_set_frame: %dx%d", width, height);
@@ -1304,6 +258,8 @@ int cpt_set_frame(cpt_ctx* c, int width, int height, const int32_t* rows, int n_
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipStreamSynchronize(c->stream()));
     free_frame(c);
+    static std::atomic<uint64_t> frame_gens{0};
+    c->frame_gen = ++frame_gens;
     c->width = width;
     c->height = height;
     c->n_rows = (int)r.size();
@@ -1504,48 +460,120 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
 // same global rows.  One peer copy of src's buffers to dst's device (hipMemcpyPeerAsync: xGMI
 // between two MI355X, a plain device copy when both contexts share a GPU), then one stitch
 // kernel on dst's stream.  Waits for src; asynchronous with respect to dst.
+namespace {
+// Peer access from `dev` to `peer`'s memory, enabled once per ordered pair for the process.
+// Returns false when the pair has no peer path (the gather then stages through a peer copy).
+bool ensure_peer_access(int dev, int peer) {
+    static std::mutex mu;
+    static std::vector<std::pair<std::pair<int, int>, bool>> known;
+    std::lock_guard<std::mutex> lk(mu);
+    for (const auto& k : known)
+        if (k.first == std::make_pair(dev, peer)) return k.second;
+    int can = 0;
+    bool ok = hipDeviceCanAccessPeer(&can, dev, peer) == hipSuccess && can;
+    if (ok) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        ok = hipSetDevice(dev) == hipSuccess;
+        if (ok) {
+            const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+            ok = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+            if (!ok) (void)hipGetLastError();   // clear the sticky error
+        }
+        (void)hipSetDevice(cur);
+    }
+    known.emplace_back(std::make_pair(dev, peer), ok);
+    return ok;
+}
+}  // namespace
+
+// The row map of a (dst, src) frame pair lives in a device buffer of dst, uploaded when either
+// frame changes (cpt_set_frame bumps frame_gen).  src's work is ordered before the stitch by an
+// event (no host wait), and src's later work after it by another, so N gathers queue back to
+// back on dst's stream and one synchronisation of dst covers them all.  On two devices the
+// stitch kernel reads src's buffers directly over xGMI (peer access, enabled once per pair);
+// without a peer path it stages them through hipMemcpyPeerAsync.
 int cpt_gather_rows(cpt_ctx* dst, cpt_ctx* src) {
     if (!dst || !src || dst == src) return dst ? fail(dst, CPT_ERR_INVALID_ARG, "cpt_gather_rows: bad contexts") : CPT_ERR_INVALID_ARG;
     if (!dst->frame_set || !src->frame_set) return fail(dst, CPT_ERR_STATE, "cpt_gather_rows: both contexts need a frame");
     if (dst->width != src->width || dst->height != src->height)
         return fail(dst, CPT_ERR_INVALID_ARG, "cpt_gather_rows: frame %dx%d vs %dx%d", dst->width, dst->height, src->width,
                     src->height);
-    std::vector<int32_t> at(dst->height, -1);   // dst row index of each global row (first occurrence)
-    for (int j = dst->n_rows - 1; j >= 0; --j) at[dst->rows_h[j]] = j;
-    dst->gather_map_h.resize(src->n_rows);
-    for (int i = 0; i < src->n_rows; ++i) {
-        const int32_t j = at[src->rows_h[i]];
-        if (j < 0) return fail(dst, CPT_ERR_INVALID_ARG, "cpt_gather_rows: row %d is not in the destination frame", src->rows_h[i]);
-        dst->gather_map_h[i] = j;
+    cpt_ctx::GatherMap* gm = nullptr;
+    for (auto& g : dst->gather_maps)
+        if (g.src == src) gm = &g;
+    if (!gm) {
+        dst->gather_maps.push_back(cpt_ctx::GatherMap{});
+        gm = &dst->gather_maps.back();
+        gm->src = src;
+    }
+    if (gm->src_gen != src->frame_gen || gm->dst_gen != dst->frame_gen || gm->src_device != src->device) {
+        std::vector<int32_t> at(dst->height, -1);   // dst row index of each global row (first occurrence)
+        for (int j = dst->n_rows - 1; j >= 0; --j) at[dst->rows_h[j]] = j;
+        std::vector<int32_t> map(src->n_rows);
+        for (int i = 0; i < src->n_rows; ++i) {
+            const int32_t j = at[src->rows_h[i]];
+            if (j < 0)
+                return fail(dst, CPT_ERR_INVALID_ARG, "cpt_gather_rows: row %d is not in the destination frame", src->rows_h[i]);
+            map[i] = j;
+        }
+        HIP_TRY(dst, hipSetDevice(dst->device));
+        if (gm->d_map) { (void)hipFree(gm->d_map); gm->d_map = nullptr; }
+        if (!map.empty()) {
+            HIP_TRY(dst, hipMalloc((void**)&gm->d_map, map.size() * sizeof(int32_t)));
+            HIP_TRY(dst, hipMemcpy(gm->d_map, map.data(), map.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        }
+        gm->src_gen = src->frame_gen;
+        gm->dst_gen = dst->frame_gen;
+        gm->src_device = src->device;
+        gm->peer = src->device == dst->device || ensure_peer_access(dst->device, src->device);
     }
     if (src->n_rows == 0) return CPT_OK;
-    if (int rc = sync_checked(src)) return fail(dst, rc, "cpt_gather_rows: source: %s", src->err.c_str());
     const size_t npix = (size_t)src->n_rows * src->width;
     const bool aux = src->d_normal && src->d_depth;
+    // src's queued work (its render) before the stitch
+    HIP_TRY(src, hipSetDevice(src->device));
+    HIP_TRY(src, hipEventRecord(src->ev_ready, src->stream()));
     HIP_TRY(dst, hipSetDevice(dst->device));
     hipStream_t s = dst->stream();
+    HIP_TRY(dst, hipStreamWaitEvent(s, src->ev_ready, 0));
     const size_t dst_npix = (size_t)dst->n_rows * dst->width;
     if (aux) {
-        if (!dst->d_normal) HIP_TRY(dst, hipMalloc((void**)&dst->d_normal, dst_npix * 3 * sizeof(float)));
-        if (!dst->d_depth) HIP_TRY(dst, hipMalloc((void**)&dst->d_depth, dst_npix * sizeof(float)));
+        // rows no source covers read as zero normals and depths
+        if (!dst->d_normal) {
+            HIP_TRY(dst, hipMalloc((void**)&dst->d_normal, dst_npix * 3 * sizeof(float)));
+            HIP_TRY(dst, hipMemsetAsync(dst->d_normal, 0, dst_npix * 3 * sizeof(float), s));
+        }
+        if (!dst->d_depth) {
+            HIP_TRY(dst, hipMalloc((void**)&dst->d_depth, dst_npix * sizeof(float)));
+            HIP_TRY(dst, hipMemsetAsync(dst->d_depth, 0, dst_npix * sizeof(float), s));
+        }
     }
-    int rc;
-    // staging: accumulator (npix float4), then normals (3 npix floats) and depths (npix floats)
-    if ((rc = ensure(dst, &dst->d_gather, &dst->cap_gather, aux ? 2 * npix : npix)) != CPT_OK) return rc;
-    if ((rc = ensure(dst, &dst->d_gather_map, &dst->cap_gather_map, (size_t)src->n_rows)) != CPT_OK) return rc;
-    float* st_nrm = reinterpret_cast<float*>(dst->d_gather + npix);
-    float* st_dep = st_nrm + 3 * npix;
-    HIP_TRY(dst, hipMemcpyAsync(dst->d_gather_map, dst->gather_map_h.data(), src->n_rows * sizeof(int32_t),
-                                hipMemcpyHostToDevice, s));
-    HIP_TRY(dst, hipMemcpyPeerAsync(dst->d_gather, dst->device, src->d_accum, src->device, npix * sizeof(float4), s));
-    if (aux) {
-        HIP_TRY(dst, hipMemcpyPeerAsync(st_nrm, dst->device, src->d_normal, src->device, npix * 3 * sizeof(float), s));
-        HIP_TRY(dst, hipMemcpyPeerAsync(st_dep, dst->device, src->d_depth, src->device, npix * sizeof(float), s));
+    const float4* s_acc = src->d_accum;
+    const float* s_nrm = aux ? src->d_normal : nullptr;
+    const float* s_dep = aux ? src->d_depth : nullptr;
+    if (!gm->peer) {
+        // staging: accumulator (npix float4), then normals (3 npix floats) and depths (npix floats)
+        int rc;
+        if ((rc = ensure(dst, &dst->d_gather, &dst->cap_gather, aux ? 2 * npix : npix)) != CPT_OK) return rc;
+        float* st_nrm = reinterpret_cast<float*>(dst->d_gather + npix);
+        float* st_dep = st_nrm + 3 * npix;
+        HIP_TRY(dst, hipMemcpyPeerAsync(dst->d_gather, dst->device, src->d_accum, src->device, npix * sizeof(float4), s));
+        if (aux) {
+            HIP_TRY(dst, hipMemcpyPeerAsync(st_nrm, dst->device, src->d_normal, src->device, npix * 3 * sizeof(float), s));
+            HIP_TRY(dst, hipMemcpyPeerAsync(st_dep, dst->device, src->d_depth, src->device, npix * sizeof(float), s));
+        }
+        s_acc = dst->d_gather;
+        s_nrm = aux ? st_nrm : nullptr;
+        s_dep = aux ? st_dep : nullptr;
     }
-    HIP_TRY(dst, cpt::launch_stitch_rows(dst->d_gather, aux ? st_nrm : nullptr, aux ? st_dep : nullptr, dst->d_gather_map,
-                                         dst->width, src->n_rows, dst->d_accum, dst->d_normal, dst->d_depth, s));
-    // the host row map is read by the async upload: keep it until the stream passes the copy
-    HIP_TRY(dst, hipStreamSynchronize(s));
+    HIP_TRY(dst, cpt::launch_stitch_rows(s_acc, s_nrm, s_dep, gm->d_map, dst->width, src->n_rows, dst->d_accum,
+                                         dst->d_normal, dst->d_depth, s));
+    // src's later work (a next render into the buffers just read) after the stitch
+    HIP_TRY(dst, hipEventRecord(dst->ev_gathered, s));
+    HIP_TRY(src, hipSetDevice(src->device));
+    HIP_TRY(src, hipStreamWaitEvent(src->stream(), dst->ev_gathered, 0));
+    HIP_TRY(dst, hipSetDevice(dst->device));
     return CPT_OK;
 }
 
@@ -1710,12 +738,24 @@ static int denoise_band(cpt_ctx* c, uint32_t cur_sample_idx, int y0, int y1, uin
         c->band_y0 = y0;
         c->band_y1 = y1;
     }
+    HIP_TRY(c, hipEventRecord(c->ev_dn0, s));
     HIP_TRY(c, cpt::launch_denoise_mix(c->d_accum, c->d_normal, c->d_depth, c->d_mix, c->d_bgra, c->width, c->height,
                                       row0, y0, y1, cur_sample_idx, s));
+    HIP_TRY(c, hipEventRecord(c->ev_dn1, s));
+    c->have_dn_timing = true;
     if (bgra_host) {
         HIP_TRY(c, hipMemcpyAsync(bgra_host, c->d_bgra, cap_rows * c->width * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(c, hipStreamSynchronize(s));
     }
+    return CPT_OK;
+}
+
+int cpt_last_display_ms(cpt_ctx* c, float* ms) {
+    if (!c || !ms) return CPT_ERR_INVALID_ARG;
+    if (!c->have_dn_timing) return fail(c, CPT_ERR_STATE, "cpt_last_display_ms: no display frame yet");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipEventSynchronize(c->ev_dn1));
+    HIP_TRY(c, hipEventElapsedTime(ms, c->ev_dn0, c->ev_dn1));
     return CPT_OK;
 }
 

@@ -701,9 +701,36 @@ __global__ void k_rng_pixels(const uint32_t* __restrict__ rowmats, const uint32_
 // mix = lerp(mix, clamp(denoised, 0, 1), 1/cur_sample_idx); bytes 0..2 = 255.99*(b, g, r)
 // (path_tracer.cu:241-254); the alpha byte is not written.
 // ======================================================================================
+// min(exp(-(dist2) / M_PI), 1.0) in double, stored to float (path_tracer.cu:224,228,231), for a
+// float dist2.  Three exact shortcuts of the same value: dist2 == 0 gives exp(-0) = 1;
+// dist2 >= 2341 gives exp(x) with x < -745.1332 (dm::exp's underflow bound), i.e. 0 -- this also
+// covers +inf, for which div_pi would not return the IEEE quotient; otherwise the quotient is
+// dm::div_pi's (correctly rounded: the sequence depends only on dist2's significand, and
+// tests/test_exact_identities.py checks every significand), NaN included (weight 1 through
+// the `w < 1.0` select, as before).
 __device__ __forceinline__ float dn_weight(float dist2) {
-    double w = dm::exp(-((double)dist2) / REF_PI);
+    if (dist2 == 0.0f) return 1.0f;
+    if (dist2 >= 2341.0f) return 0.0f;
+    const double w = dm::exp(-dm::div_pi(dist2));
     return (float)(w < 1.0 ? w : 1.0);
+}
+
+// The 5x5 stencil's pair weight c_w * n_w * p_w between pixels a and b (path_tracer.cu:
+// 219-233).  Every factor is a function of the difference of the two pixels' values, squared:
+// a - b = -(b - a) exactly, so w(a, b) == w(b, a) bit for bit, and each unordered pair needs
+// evaluating once.  The depth factor is exactly 1 when the depths are equal (a18: depth is the
+// constant 1e30), so its exp only runs where it can differ.
+struct DnPix { float r, g, b, nx, ny, nz, d, pad; };
+
+__device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b) {
+    v3 t = mk(a.r, a.g, a.b) - mk(b.r, b.g, b.b);
+    const float c_w = dn_weight(dot(t, t));
+    t = mk(a.nx, a.ny, a.nz) - mk(b.nx, b.ny, b.nz);
+    const double dn = (double)dot(t, t);
+    const float n_w = dn_weight((float)(dn > 0.0 ? dn : 0.0));
+    const float dd = (a.d - b.d) * (a.d - b.d);
+    const float p_w = dn_weight(dd);
+    return c_w * n_w * p_w;
 }
 
 // One band of output rows [y0, y1) of the W' x H' launch (W' = 16 floor(W/16), H' likewise).
@@ -711,66 +738,163 @@ __device__ __forceinline__ float dn_weight(float dist2) {
 // band plus a 3-row halo, enough for every neighbour the linear-offset stencil reaches (x +- 2
 // wraps into the adjacent row, so rows y - 3 .. y + 3).  mix and out hold the band's rows
 // only.  The full frame is the band [0, H') with row0 = 0.
-__global__ void k_denoise_mix(const float4* __restrict__ accum, const float* __restrict__ normal,
-                              const float* __restrict__ depth, float* __restrict__ mix, uint8_t* __restrict__ out,
-                              int width, int row0, int y0, int y1, int w_eff, int h_eff, float inv_idx) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = y0 + blockIdx.y * blockDim.y + threadIdx.y;
-    if (x >= w_eff || y >= y1) return;
-    const float kernel5[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
-                                 {4.f, 16.f, 26.f, 16.f, 4.f},
-                                 {7.f, 26.f, 41.f, 26.f, 7.f},
-                                 {4.f, 16.f, 26.f, 16.f, 4.f},
-                                 {1.f, 4.f, 7.f, 4.f, 1.f}};
-    auto radiance = [&](int px) {
-        const float4 a = accum[px];
-        return a.w != 0.f ? mk(a.x, a.y, a.z) / a.w : mk(a.x, a.y, a.z);
-    };
-    const int self = (y - row0) * width + x;        // this pixel in the rendered rows
-    const int bself = (y - y0) * width + x;         // ... and in the band's mix / out
-    const v3 cval = radiance(self);
-    const v3 nval = mk(normal[3 * self], normal[3 * self + 1], normal[3 * self + 2]);
-    const float pval = depth[self];
-    v3 sum = mk1(0.f);
-    float cum_w = 0.0f;
+//
+// A block takes a tile of DN_TX x DN_TY output pixels.  The stencil indexes neighbours by the
+// LINEAR offset v*W' + u, so tile row r's neighbours are the linear run r*W' + x0 - 2 ..
+// r*W' + x0 + DN_TX + 1 (which wraps into the adjacent image row exactly as the reference
+// does); the block stages those runs for rows ty0 - 2 .. ty0 + DN_TY + 1 in LDS once, as
+// radiance (accumulator / pass count), normal and depth.  Pair weights are evaluated once per
+// unordered pair: each tile pixel evaluates its 12 forward neighbours (dy > 0, or dy = 0 and
+// dx > 0) and hands each weight to the neighbour when that one is in the tile; the pairs whose
+// first pixel lies outside the tile (the halo band above and beside it) are evaluated by the
+// whole block from a flat list.  Each pixel then sums its 25 taps in the reference's order.
+constexpr int DN_TX = 64, DN_TY = 8, DN_THREADS = 256;
+constexpr int DN_BX = DN_TX + 4, DN_BY = DN_TY + 4;   // staged box (2-pixel halo each side)
+constexpr int DN_PIX_PER_THREAD = DN_TX * DN_TY / DN_THREADS;
+// forward offsets (dx, dy), k = 0..11: dy = 0, dx = 1, 2; dy = 1, dx = -2..2; dy = 2, dx = -2..2
+__device__ __forceinline__ int dn_fdx(int k) { return k < 2 ? k + 1 : ((k - 2) % 5) - 2; }
+__device__ __forceinline__ int dn_fdy(int k) { return k < 2 ? 0 : (k < 7 ? 1 : 2); }
+
+__global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __restrict__ accum,
+                                                           const float* __restrict__ normal,
+                                                           const float* __restrict__ depth, float* __restrict__ mix,
+                                                           uint8_t* __restrict__ out, int width, int row0, int y0,
+                                                           int y1, int w_eff, int h_eff, float inv_idx) {
+    __shared__ DnPix s_pix[DN_BY * DN_BX];
+    __shared__ float s_wb[DN_TY * DN_TX * 12];   // backward weight k of tile pixel (ty, tx)
+    const int x0 = blockIdx.x * DN_TX, ty0 = y0 + blockIdx.y * DN_TY;
+    const int tw = min(DN_TX, w_eff - x0), th = min(DN_TY, y1 - ty0);   // the tile's extent
     const int limit = w_eff * h_eff;
-    for (int i = 0; i < 5; ++i) {
-        for (int j = 0; j < 5; ++j) {
-            const int u = x + (i - 2), v = y + (j - 2);
-            const int cur_off = v * w_eff + u;
-            float weight;
-            v3 ctmp;
-            if (cur_off < 0 || cur_off >= limit) {
-                weight = 0.f * 0.f * 0.f;
-                ctmp = mk1(0.f);
-            } else {
-                const int px = (cur_off / w_eff - row0) * width + (cur_off % w_eff);
-                ctmp = radiance(px);
-                v3 t = cval - ctmp;
-                const float c_w = dn_weight(dot(t, t));
-                const v3 ntmp = mk(normal[3 * px], normal[3 * px + 1], normal[3 * px + 2]);
-                t = nval - ntmp;
-                const double dn = (double)dot(t, t);
-                const float n_w = dn_weight((float)(dn > 0.0 ? dn : 0.0));
-                const float ptmp = depth[px];
-                const float p_w = dn_weight((pval - ptmp) * (pval - ptmp));
-                weight = c_w * n_w * p_w;
-            }
-            sum = sum + (weight * kernel5[i][j]) * ctmp;
-            cum_w += weight * kernel5[i][j];
+    // ---- stage the box: linear pixels (ty0 - 2 + by) * W' + x0 - 2 + bx ----------------
+    for (int i = threadIdx.x; i < DN_BY * DN_BX; i += DN_THREADS) {
+        const int by = i / DN_BX, bx = i - by * DN_BX;
+        const int L = (ty0 - 2 + by) * w_eff + x0 - 2 + bx;
+        DnPix q;
+        if (L >= 0 && L < limit) {
+            const int yy = L / w_eff;
+            const int px = (yy - row0) * width + (L - yy * w_eff);
+            const float4 a = accum[px];
+            const v3 c = a.w != 0.f ? mk(a.x, a.y, a.z) / a.w : mk(a.x, a.y, a.z);
+            q.r = c.x; q.g = c.y; q.b = c.z;
+            q.nx = normal[3 * px]; q.ny = normal[3 * px + 1]; q.nz = normal[3 * px + 2];
+            q.d = depth[px];
+        } else {   // outside [0, W'H'): weight 0 (never read as a value)
+            q.r = q.g = q.b = q.nx = q.ny = q.nz = q.d = 0.f;
+        }
+        q.pad = (L >= 0 && L < limit) ? 1.f : 0.f;   // valid flag
+        s_pix[i] = q;
+    }
+    __syncthreads();
+    auto box = [&](int tx, int ty) -> const DnPix& { return s_pix[(ty + 2) * DN_BX + tx + 2]; };
+    auto in_tile = [&](int tx, int ty) { return tx >= 0 && tx < tw && ty >= 0 && ty < th; };
+    // ---- forward pairs of the tile's pixels ---------------------------------------------
+    float wf[DN_PIX_PER_THREAD][12];
+#pragma unroll
+    for (int j = 0; j < DN_PIX_PER_THREAD; ++j) {
+        const int e = threadIdx.x + j * DN_THREADS;
+        const int ty = e / DN_TX, tx = e - ty * DN_TX;
+        const bool mine = in_tile(tx, ty);
+        const DnPix& p = box(tx, ty);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const int dx = dn_fdx(k), dy = dn_fdy(k);
+            const DnPix& q = box(tx + dx, ty + dy);
+            float w = 0.f;
+            if (mine && p.pad != 0.f && q.pad != 0.f) w = dn_pair_weight(p, q);
+            wf[j][k] = w;
+            if (mine && in_tile(tx + dx, ty + dy)) s_wb[((ty + dy) * DN_TX + tx + dx) * 12 + k] = w;
         }
     }
-    const v3 dn = sum / cum_w;
-    const v3 cl = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),
-                     __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));
-    v3 m = mk(mix[3 * bself], mix[3 * bself + 1], mix[3 * bself + 2]);
-    m = m + inv_idx * (cl - m);      // lerp(a, b, t) = a + t*(b-a) (helper_math.h:1154-1157)
-    mix[3 * bself] = m.x;
-    mix[3 * bself + 1] = m.y;
-    mix[3 * bself + 2] = m.z;
-    out[4 * (size_t)bself + 0] = (uint8_t)(255.99f * m.z);
-    out[4 * (size_t)bself + 1] = (uint8_t)(255.99f * m.y);
-    out[4 * (size_t)bself + 2] = (uint8_t)(255.99f * m.x);
+    // ---- pairs (s, t = s + d) with t in the tile and s outside it ------------------------
+    // For offset k the targets are the first dy rows of the tile (all columns), then in the
+    // other rows the |dx| columns at the side the offset reaches in from.
+    {
+        int count[12], total = 0;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const int dx = dn_fdx(k), dy = dn_fdy(k), adx = dx < 0 ? -dx : dx;
+            const int rows_top = min(dy, th), cols = min(adx, tw);
+            count[k] = rows_top * tw + (th - rows_top) * cols;
+            total += count[k];
+        }
+        for (int e = threadIdx.x; e < total; e += DN_THREADS) {
+            int k = 0, r = e;
+            while (r >= count[k]) { r -= count[k]; ++k; }
+            const int dx = dn_fdx(k), dy = dn_fdy(k), adx = dx < 0 ? -dx : dx;
+            const int rows_top = min(dy, th), cols = min(adx, tw);
+            int tx, ty;
+            if (r < rows_top * tw) {
+                ty = r / tw;
+                tx = r - ty * tw;
+            } else {
+                r -= rows_top * tw;
+                ty = rows_top + r / cols;
+                const int c = r - (ty - rows_top) * cols;
+                tx = dx > 0 ? c : tw - adx + c;
+            }
+            const DnPix& t = box(tx, ty);
+            const DnPix& s = box(tx - dx, ty - dy);
+            const float w = (s.pad != 0.f && t.pad != 0.f) ? dn_pair_weight(s, t) : 0.f;
+            s_wb[(ty * DN_TX + tx) * 12 + k] = w;
+        }
+    }
+    __syncthreads();
+    // ---- the 25 taps in the reference's order (i = dx outer, j = dy inner) -----------------
+    constexpr float kernel5[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
+                                     {4.f, 16.f, 26.f, 16.f, 4.f},
+                                     {7.f, 26.f, 41.f, 26.f, 7.f},
+                                     {4.f, 16.f, 26.f, 16.f, 4.f},
+                                     {1.f, 4.f, 7.f, 4.f, 1.f}};
+#pragma unroll
+    for (int j = 0; j < DN_PIX_PER_THREAD; ++j) {
+        const int e = threadIdx.x + j * DN_THREADS;
+        const int ty = e / DN_TX, tx = e - ty * DN_TX;
+        if (!in_tile(tx, ty)) continue;
+        const DnPix& p = box(tx, ty);
+        v3 sum = mk1(0.f);
+        float cum_w = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+#pragma unroll
+            for (int jj = 0; jj < 5; ++jj) {
+                const int dx = i - 2, dy = jj - 2;
+                const DnPix& q = box(tx + dx, ty + dy);
+                float weight;
+                v3 ctmp;
+                if (q.pad == 0.f) {
+                    weight = 0.f * 0.f * 0.f;
+                    ctmp = mk1(0.f);
+                } else {
+                    ctmp = mk(q.r, q.g, q.b);
+                    if (dx == 0 && dy == 0) {
+                        weight = dn_pair_weight(p, p);
+                    } else if (dy > 0 || (dy == 0 && dx > 0)) {
+                        weight = wf[j][dy == 0 ? dx - 1 : 2 + 5 * (dy - 1) + dx + 2];
+                    } else {
+                        const int k = dy == 0 ? -dx - 1 : 2 + 5 * (-dy - 1) - dx + 2;
+                        weight = s_wb[(ty * DN_TX + tx) * 12 + k];
+                    }
+                }
+                sum = sum + (weight * kernel5[i][jj]) * ctmp;
+                cum_w += weight * kernel5[i][jj];
+            }
+        }
+        const v3 dn = sum / cum_w;
+        const v3 cl = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),
+                         __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));
+        const int y = ty0 + ty, x = x0 + tx;
+        const size_t bself = (size_t)(y - y0) * width + x;   // this pixel in the band's mix / out
+        v3 m = mk(mix[3 * bself], mix[3 * bself + 1], mix[3 * bself + 2]);
+        m = m + inv_idx * (cl - m);      // lerp(a, b, t) = a + t*(b-a) (helper_math.h:1154-1157)
+        mix[3 * bself] = m.x;
+        mix[3 * bself + 1] = m.y;
+        mix[3 * bself + 2] = m.z;
+        // bytes 0..2 = 255.99 * (b, g, r); the alpha byte is never written by the reference and
+        // stays the buffer's zero here (one 32-bit store)
+        const uint32_t bgr = (uint32_t)(uint8_t)(255.99f * m.z) | ((uint32_t)(uint8_t)(255.99f * m.y) << 8) |
+                             ((uint32_t)(uint8_t)(255.99f * m.x) << 16);
+        reinterpret_cast<uint32_t*>(out)[bself] = bgr;
+    }
 }
 
 hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
@@ -779,9 +903,9 @@ hipError_t launch_denoise_mix(const float4* accum, const float* normal, const fl
     const int w_eff = 16 * (width / 16), h_eff = 16 * (height / 16);
     if (w_eff == 0 || h_eff == 0 || y1 <= y0) return hipSuccess;
     const float inv_idx = 1.f / float(cur_sample_idx);
-    dim3 block(16, 16), grid(w_eff / 16, (y1 - y0 + 15) / 16);
-    hipLaunchKernelGGL(k_denoise_mix, grid, block, 0, stream, accum, normal, depth, mix, out, width, row0, y0, y1,
-                       w_eff, h_eff, inv_idx);
+    dim3 grid((w_eff + DN_TX - 1) / DN_TX, (y1 - y0 + DN_TY - 1) / DN_TY);
+    hipLaunchKernelGGL(k_denoise_mix, grid, dim3(DN_THREADS), 0, stream, accum, normal, depth, mix, out, width, row0, y0,
+                       y1, w_eff, h_eff, inv_idx);
     return hipGetLastError();
 }
 

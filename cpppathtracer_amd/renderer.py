@@ -265,11 +265,20 @@ class Renderer:
                  for v in out[1:1 + min(cnt, examples)]]
         return cnt, pairs
 
-    def denoise_mix(self, cur_sample_idx):
-        """Denoising + Mix display pass; returns the BGRA8 frame (height, width, 4)."""
-        out = np.zeros((self.height, self.width, 4), dtype=np.uint8)
+    def denoise_mix(self, cur_sample_idx, out=None):
+        """Denoising + Mix display pass; returns the BGRA8 frame (height, width, 4), into `out`
+        when given (a preallocated, e.g. pinned, host array of that shape)."""
+        if out is None:
+            out = np.zeros((self.height, self.width, 4), dtype=np.uint8)
+        assert out.dtype == np.uint8 and out.size == self.height * self.width * 4 and out.flags["C_CONTIGUOUS"]
         self._check(self._L.cpt_denoise_mix(self._ctx, cur_sample_idx, _p(out)))
         return out
+
+    def last_display_ms(self) -> float:
+        """Device time of the last display kernel (Denoising + Mix), HIP events."""
+        ms = ctypes.c_float()
+        self._check(self._L.cpt_last_display_ms(self._ctx, ctypes.byref(ms)))
+        return ms.value
 
     def denoise_mix_band(self, cur_sample_idx, y0, y1, host=True):
         """Display path for output rows [y0, y1) (cpt_denoise_mix_band): the frame's rows must be

@@ -87,9 +87,16 @@ private:
         bool env_uploaded = false;
         bool rng_ready = false;
     };
+    // One read of SceneBVH's state (SceneBVH::GetState), applied to every tile of a pass, so all
+    // row tiles of a frame render the same scene revision.
+    struct SceneSnap {
+        uint64_t build = 0, rev = 0;
+        std::vector<cpt_object> built, current;
+        std::vector<uint64_t> updates;
+    };
     bool EnsureContext();
     bool SyncScene();
-    bool SyncTile(Tile& t);
+    bool SyncTile(Tile& t, const SceneSnap& snap);
     bool BindTextures(Tile& t, const std::vector<cpt_object>& objs);
     bool EnsureFrame(const MotionalCamera& cam);
     bool RenderPass(MotionalCamera& cam, int spp, bool accumulate);

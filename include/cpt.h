@@ -254,9 +254,12 @@ int cpt_copy_accum_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
  * whole frame from SamplePixel, path_tracer.cu:172-174): places the rows `src` rendered -- its
  * accumulator, and its first-hit normals and depths when it rendered with CPT_RENDER_AUX --
  * into `dst`'s frame at the same global rows (dst must hold every one of them, e.g. a full
- * frame).  src and dst may live on different devices (peer copy over xGMI) or on the same one.
- * Waits for src's work (and reports its device errors); dst then holds a stitched frame for
- * cpt_read_accum, cpt_read_aux and cpt_denoise_mix. */
+ * frame).  src and dst may live on different devices (the stitch reads src over xGMI with peer
+ * access, enabled once per device pair; a staged peer copy where no peer path exists) or on the
+ * same one.  Asynchronous: ordered after src's queued work and before src's later work by
+ * events, with no host wait, so several gathers queue back to back; dst then holds the stitched
+ * frame for its next call (cpt_synchronize, cpt_read_accum, cpt_read_aux, cpt_denoise_mix).
+ * src's device errors are reported by src's own next synchronising call. */
 int cpt_gather_rows(cpt_ctx* dst, cpt_ctx* src);
 int cpt_get_stats(cpt_ctx* ctx, cpt_stats* out);
 int cpt_reset_stats(cpt_ctx* ctx);
@@ -298,6 +301,10 @@ int cpt_denoise_mix(cpt_ctx* ctx, uint32_t cur_sample_idx, uint8_t* bgra_host);
 int cpt_denoise_mix_band(cpt_ctx* ctx, uint32_t cur_sample_idx, int y0, int y1, uint8_t* bgra_host);
 /* Device-to-device copy of the current display band's BGRA8 rows (for an RCCL gather). */
 int cpt_copy_bgra_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
+/* Device time of the last display kernel (Denoising + Mix, the reference's per-pass log of
+ * path_tracer.cu:261,300 split by kernel), from HIP events on the context's stream; waits
+ * for it. */
+int cpt_last_display_ms(cpt_ctx* ctx, float* ms);
 /* Zero the Mix running mean (the reference's buffer starts uninitialised; here it is zeroed
  * when the frame is created and by this call). */
 int cpt_reset_display(cpt_ctx* ctx);

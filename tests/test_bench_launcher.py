@@ -59,5 +59,8 @@ def test_main_spawns_before_touching_the_gpu(monkeypatch):
 def test_defaults_are_the_baseline_workload():
     b = _bench()
     a = b.parse_args([])
-    assert (a.gpus, a.config, a.scaling, a.walk, a.path) == (None, "c4", "weak", "ordered", "megakernel")
+    # N > 1 headline: the C4 1920x1080 frame strong-scaled over the ranks (the metric's resolution,
+    # BASELINE.json north_star "1920x1080 ... at 1, 2, 4 and 8 GPUs"); weak scaling is a side field
+    assert (a.gpus, a.config, a.scaling, a.walk, a.path) == (None, "c4", "strong", "ordered", "megakernel")
     assert b.parse_args(["--config", "c5"]).config == "c5"
+    assert a.dispatch == 0   # the per-pass DispatchRay timing is opt-in, never the default line

@@ -453,6 +453,21 @@ def test_wide_walk_beyond_lds_image(gpu, oracle_mod, sky, path):
     np.testing.assert_array_equal(gr, orng)
     _check_stats(gs, os_, path)
     np.testing.assert_array_equal(ga.view(np.uint32), oa.view(np.uint32))
+    assert_hbm_part_walked(gpu, path, 64, 36, 16)
+
+
+def assert_hbm_part_walked(gpu, path, W, H, depth):
+    """The render above really read wide nodes past the LDS image (raw counter 6, the HYB
+    branch of load_wide_node): a "+timed" path has no counters, so its counting
+    instantiation renders the same frame once more."""
+    if _timed(path):
+        cam = camera_get_copy(scenes.camera_for(W, H))
+        gpu.init_rng(5)
+        gpu.reset_stats()
+        kw = _kw(path.split("+")[0])
+        gpu.render(cam, 1, depth, stats=True, sync=True, **kw)
+    global_nodes = int(gpu.raw_counters()[6])
+    assert global_nodes > 0, "no wide-node visit read the image in global memory"
 
 
 def test_hbm_read_probe(gpu):

@@ -95,6 +95,55 @@ def test_device_refit_beyond_lds_image(gpu, oracle_mod, sky, path):
     gpu.set_scene(objs)
     assert gpu.walk_info()["n_wide"] > 512
     _render_edited(gpu, oracle_mod, sky, objs, _edits(objs, 300, 2), 64, 36, 2, 16, path, rebuild=False)
+    if path.startswith("megakernel:ordered"):   # the plain walk uses the binary orders, not the image
+        from test_gpu_parity import assert_hbm_part_walked
+        assert_hbm_part_walked(gpu, path, 64, 36, 16)
+
+
+def _new_material(base, k):
+    """A material no object of the scene uses: its own colour and emission."""
+    m = base.copy()
+    m["kd"] = np.array([0.11 + 0.07 * k, 0.83 - 0.05 * k, 0.37], np.float32)
+    m["emit_intensity"] = np.float32(0.25 + k)
+    return m
+
+
+@pytest.mark.parametrize("path", ["megakernel:ordered", "megakernel", "megakernel:ordered+timed"])
+def test_device_refit_new_materials(gpu, oracle_mod, sky, path):
+    """An update batch (device refit, no rebuild) that gives objects materials no object had
+    before: the material array grows past its allocation.  Two batches, the second growing it
+    again, each against the oracle bit for bit."""
+    objs = scenes.scene_s1000(n=120)
+    bounded = np.flatnonzero(objs["type"] != 1)
+    edits = []
+    for k, i in enumerate(bounded[:6]):
+        o = objs[int(i)].copy()
+        o["material"] = _new_material(o["material"], k)
+        o["center"][1] += np.float32(2.0)
+        edits.append((int(i), o))
+    _render_edited(gpu, oracle_mod, sky, objs, edits, 48, 32, 2, 8, path, rebuild=False)
+    more = list(edits)
+    for k, i in enumerate(bounded[6:40]):
+        o = objs[int(i)].copy()
+        o["material"] = _new_material(o["material"], 10 + k)
+        more.append((int(i), o))
+    _render_edited(gpu, oracle_mod, sky, objs, more, 48, 32, 2, 8, path, rebuild=False, batch=False)
+
+
+@pytest.mark.parametrize("path", ["megakernel:ordered", "megakernel", "megakernel:plain"])
+def test_device_refit_platform_height(gpu, oracle_mod, sky, path):
+    """A platform that stays a platform with a new y_pos (and a new material): its copies at the
+    head of every octant order and of the wide tree's leaf array are rewritten by the device
+    refit alone (no rebuild), and the image is the oracle's."""
+    objs = scenes.scene_s1000(n=80)
+    floor = int(np.flatnonzero(objs["type"] == 1)[0])
+    o = objs[floor].copy()
+    o["y_pos"] = np.float32(4.5)
+    o["material"] = _new_material(o["material"], 3)
+    sph = int(np.flatnonzero(objs["type"] == 0)[1])
+    o2 = objs[sph].copy()
+    o2["center"][1] += np.float32(3.0)
+    _render_edited(gpu, oracle_mod, sky, objs, [(floor, o), (sph, o2)], 48, 32, 2, 8, path, rebuild=False)
 
 
 @pytest.mark.parametrize("path", ["megakernel:ordered", "megakernel:plain"])
