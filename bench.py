@@ -501,6 +501,13 @@ def run(args):
                             "wave scheduling; lanes_per_valu = active lanes per VALU instruction",
                     **{k: prof["issue"][k] for k in ("lanes_per_valu", "wait_frac", "clock_ghz") if k in prof["issue"]},
                 }
+                # the binding roof: VALU issue x the share of a wave's 64 lanes each VALU
+                # instruction does useful work on
+                iss, lanes = prof["issue"].get("valu_issue_frac"), prof["issue"].get("lanes_per_valu")
+                if iss is not None and lanes is not None:
+                    roof["useful_lane_issue_frac"] = round(iss * lanes / 64.0, 4)
+                    roof["useful_lane_issue_note"] = ("valu_issue_roofline.achieved_frac x lanes_per_valu / 64: the "
+                                                      "fraction of the SIMDs' lane-issue capacity doing useful work")
                 roof["limiter"] = prof["limiter"]
                 roof["profile"] = prof["source"]
             out["roofline"] = roof

@@ -1,5 +1,5 @@
 """Exact replacements the device code uses instead of slower IEEE sequences (cpt_device.hpp
-dm::div_pi, dm::div255; cpt_path.hpp mirror_index's division-free range).  Each must return
+dm::div_pi -- also under the display's pair weights, cpt_kernels.hip dn_weight --, dm::div255; cpt_path.hpp mirror_index's division-free range).  Each must return
 the bit pattern of the expression it replaces, checked here exhaustively on the host: the
 formulas are plain IEEE double operations (fma included), which the GPU executes alike."""
 import os
@@ -42,6 +42,19 @@ int main(void) {
             if (memcmp(&x, &y, 8) != 0) { if (bad < 5) printf("div_pi %a\n", a); bad++; }
             n++;
         }
+    }
+    /* the denoise weights' range (cpt_kernels.hip dn_weight): every float in [2, 2341); from
+       2341 on, exp(-x / pi) is below exp's underflow bound and dn_weight returns 0 directly */
+    {
+        float lim = 2341.0f;
+        uint32_t lb; memcpy(&lb, &lim, 4);
+        for (uint32_t b = 0x40000000u; b < lb; ++b) {
+            float a; memcpy(&a, &b, 4);
+            double x = div_pi(a), y = (double)a / REF_PI;
+            if (memcmp(&x, &y, 8) != 0) { if (bad < 5) printf("div_pi %a\n", a); bad++; }
+            n++;
+        }
+        if (!((double)lim / REF_PI > 745.1332191019412)) { printf("dn_weight bound\n"); bad++; }
     }
     for (uint32_t k = 0; k < 256; ++k) {
         float x = (float)((double)k * (1.0 / 255.0)), y = (float)k / 255.0f;
