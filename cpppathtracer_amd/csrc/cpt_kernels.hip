@@ -722,15 +722,22 @@ __device__ __forceinline__ float dn_weight(float dist2) {
 // constant 1e30), so its exp only runs where it can differ.
 struct DnPix { float r, g, b, nx, ny, nz, d, pad; };
 
+// The three squared differences in the reference's order (colour, normal clamped at 0 in
+// double, depth); the weight is their dn_weights' product, left to right.  One dn_weight per
+// loop step (not unrolled): the kernel carries a single copy of the exp sequence.
 __device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b) {
     v3 t = mk(a.r, a.g, a.b) - mk(b.r, b.g, b.b);
-    const float c_w = dn_weight(dot(t, t));
+    const float dc = dot(t, t);
     t = mk(a.nx, a.ny, a.nz) - mk(b.nx, b.ny, b.nz);
     const double dn = (double)dot(t, t);
-    const float n_w = dn_weight((float)(dn > 0.0 ? dn : 0.0));
     const float dd = (a.d - b.d) * (a.d - b.d);
-    const float p_w = dn_weight(dd);
-    return c_w * n_w * p_w;
+    float w = 1.0f;   // 1 * c_w == c_w exactly
+#pragma unroll 1
+    for (int f = 0; f < 3; ++f) {
+        const float d2 = f == 0 ? dc : (f == 1 ? (float)(dn > 0.0 ? dn : 0.0) : dd);
+        w = w * dn_weight(d2);
+    }
+    return w;
 }
 
 // One band of output rows [y0, y1) of the W' x H' launch (W' = 16 floor(W/16), H' likewise).
@@ -744,13 +751,15 @@ __device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b) 
 // r*W' + x0 + DN_TX + 1 (which wraps into the adjacent image row exactly as the reference
 // does); the block stages those runs for rows ty0 - 2 .. ty0 + DN_TY + 1 in LDS once, as
 // radiance (accumulator / pass count), normal and depth.  Pair weights are evaluated once per
-// unordered pair: each tile pixel evaluates its 12 forward neighbours (dy > 0, or dy = 0 and
-// dx > 0) and hands each weight to the neighbour when that one is in the tile; the pairs whose
-// first pixel lies outside the tile (the halo band above and beside it) are evaluated by the
-// whole block from a flat list.  Each pixel then sums its 25 taps in the reference's order.
+// unordered pair: every (tile pixel, forward offset) pair (dy > 0, or dy = 0 and dx > 0) in one
+// flat loop over the block's threads, each weight stored for the pixel and handed to its
+// neighbour when that one is in the tile; the pairs whose first pixel lies outside the tile
+// (the halo band above and beside it) from a second flat list.  Each pixel then sums its 25
+// taps in the reference's order.  The loops are not unrolled: one copy of the exp sequence
+// keeps the kernel inside the instruction cache.
 constexpr int DN_TX = 64, DN_TY = 8, DN_THREADS = 256;
 constexpr int DN_BX = DN_TX + 4, DN_BY = DN_TY + 4;   // staged box (2-pixel halo each side)
-constexpr int DN_PIX_PER_THREAD = DN_TX * DN_TY / DN_THREADS;
+constexpr int DN_PIX = DN_TX * DN_TY;
 // forward offsets (dx, dy), k = 0..11: dy = 0, dx = 1, 2; dy = 1, dx = -2..2; dy = 2, dx = -2..2
 __device__ __forceinline__ int dn_fdx(int k) { return k < 2 ? k + 1 : ((k - 2) % 5) - 2; }
 __device__ __forceinline__ int dn_fdy(int k) { return k < 2 ? 0 : (k < 7 ? 1 : 2); }
@@ -761,11 +770,13 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
                                                            uint8_t* __restrict__ out, int width, int row0, int y0,
                                                            int y1, int w_eff, int h_eff, float inv_idx) {
     __shared__ DnPix s_pix[DN_BY * DN_BX];
-    __shared__ float s_wb[DN_TY * DN_TX * 12];   // backward weight k of tile pixel (ty, tx)
+    __shared__ float s_wf[DN_PIX * 12];   // forward weight k of tile pixel (ty, tx)
+    __shared__ float s_wb[DN_PIX * 12];   // backward weight k: w(p - d_k, p)
     const int x0 = blockIdx.x * DN_TX, ty0 = y0 + blockIdx.y * DN_TY;
     const int tw = min(DN_TX, w_eff - x0), th = min(DN_TY, y1 - ty0);   // the tile's extent
     const int limit = w_eff * h_eff;
     // ---- stage the box: linear pixels (ty0 - 2 + by) * W' + x0 - 2 + bx ----------------
+#pragma unroll 1
     for (int i = threadIdx.x; i < DN_BY * DN_BX; i += DN_THREADS) {
         const int by = i / DN_BX, bx = i - by * DN_BX;
         const int L = (ty0 - 2 + by) * w_eff + x0 - 2 + bx;
@@ -778,50 +789,53 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
             q.r = c.x; q.g = c.y; q.b = c.z;
             q.nx = normal[3 * px]; q.ny = normal[3 * px + 1]; q.nz = normal[3 * px + 2];
             q.d = depth[px];
+            q.pad = 1.f;   // in [0, W'H')
         } else {   // outside [0, W'H'): weight 0 (never read as a value)
             q.r = q.g = q.b = q.nx = q.ny = q.nz = q.d = 0.f;
+            q.pad = 0.f;
         }
-        q.pad = (L >= 0 && L < limit) ? 1.f : 0.f;   // valid flag
         s_pix[i] = q;
     }
     __syncthreads();
     auto box = [&](int tx, int ty) -> const DnPix& { return s_pix[(ty + 2) * DN_BX + tx + 2]; };
     auto in_tile = [&](int tx, int ty) { return tx >= 0 && tx < tw && ty >= 0 && ty < th; };
     // ---- forward pairs of the tile's pixels ---------------------------------------------
-    float wf[DN_PIX_PER_THREAD][12];
-#pragma unroll
-    for (int j = 0; j < DN_PIX_PER_THREAD; ++j) {
-        const int e = threadIdx.x + j * DN_THREADS;
-        const int ty = e / DN_TX, tx = e - ty * DN_TX;
-        const bool mine = in_tile(tx, ty);
+#pragma unroll 1
+    for (int e = threadIdx.x; e < DN_PIX * 12; e += DN_THREADS) {
+        const int pix = e / 12, k = e - pix * 12;
+        const int ty = pix / DN_TX, tx = pix - ty * DN_TX;
+        if (!in_tile(tx, ty)) continue;
+        const int dx = dn_fdx(k), dy = dn_fdy(k);
         const DnPix& p = box(tx, ty);
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const int dx = dn_fdx(k), dy = dn_fdy(k);
-            const DnPix& q = box(tx + dx, ty + dy);
-            float w = 0.f;
-            if (mine && p.pad != 0.f && q.pad != 0.f) w = dn_pair_weight(p, q);
-            wf[j][k] = w;
-            if (mine && in_tile(tx + dx, ty + dy)) s_wb[((ty + dy) * DN_TX + tx + dx) * 12 + k] = w;
-        }
+        const DnPix& q = box(tx + dx, ty + dy);
+        const float w = q.pad != 0.f ? dn_pair_weight(p, q) : 0.f;
+        s_wf[pix * 12 + k] = w;
+        if (in_tile(tx + dx, ty + dy)) s_wb[((ty + dy) * DN_TX + tx + dx) * 12 + k] = w;
     }
     // ---- pairs (s, t = s + d) with t in the tile and s outside it ------------------------
     // For offset k the targets are the first dy rows of the tile (all columns), then in the
     // other rows the |dx| columns at the side the offset reaches in from.
     {
-        int count[12], total = 0;
+        int total = 0;
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
             const int dx = dn_fdx(k), dy = dn_fdy(k), adx = dx < 0 ? -dx : dx;
             const int rows_top = min(dy, th), cols = min(adx, tw);
-            count[k] = rows_top * tw + (th - rows_top) * cols;
-            total += count[k];
+            total += rows_top * tw + (th - rows_top) * cols;
         }
+#pragma unroll 1
         for (int e = threadIdx.x; e < total; e += DN_THREADS) {
-            int k = 0, r = e;
-            while (r >= count[k]) { r -= count[k]; ++k; }
-            const int dx = dn_fdx(k), dy = dn_fdy(k), adx = dx < 0 ? -dx : dx;
-            const int rows_top = min(dy, th), cols = min(adx, tw);
+            int k = 0, r = e, dx = 0, dy = 0, adx = 0, rows_top = 0, cols = 0;
+            for (;; ++k) {
+                dx = dn_fdx(k);
+                dy = dn_fdy(k);
+                adx = dx < 0 ? -dx : dx;
+                rows_top = min(dy, th);
+                cols = min(adx, tw);
+                const int cnt = rows_top * tw + (th - rows_top) * cols;
+                if (r < cnt) break;
+                r -= cnt;
+            }
             int tx, ty;
             if (r < rows_top * tw) {
                 ty = r / tw;
@@ -833,51 +847,47 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
                 tx = dx > 0 ? c : tw - adx + c;
             }
             const DnPix& t = box(tx, ty);
-            const DnPix& s = box(tx - dx, ty - dy);
-            const float w = (s.pad != 0.f && t.pad != 0.f) ? dn_pair_weight(s, t) : 0.f;
+            const DnPix& sp = box(tx - dx, ty - dy);
+            const float w = sp.pad != 0.f ? dn_pair_weight(sp, t) : 0.f;
             s_wb[(ty * DN_TX + tx) * 12 + k] = w;
         }
     }
     __syncthreads();
     // ---- the 25 taps in the reference's order (i = dx outer, j = dy inner) -----------------
-    constexpr float kernel5[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
-                                     {4.f, 16.f, 26.f, 16.f, 4.f},
-                                     {7.f, 26.f, 41.f, 26.f, 7.f},
-                                     {4.f, 16.f, 26.f, 16.f, 4.f},
-                                     {1.f, 4.f, 7.f, 4.f, 1.f}};
-#pragma unroll
-    for (int j = 0; j < DN_PIX_PER_THREAD; ++j) {
-        const int e = threadIdx.x + j * DN_THREADS;
-        const int ty = e / DN_TX, tx = e - ty * DN_TX;
+    const float kernel5[5] = {1.f, 4.f, 7.f, 4.f, 1.f};   // the rows of kernel[5][5] (path_tracer.cu:191-197)
+    const float kmid[5] = {4.f, 16.f, 26.f, 16.f, 4.f};
+    const float kctr[5] = {7.f, 26.f, 41.f, 26.f, 7.f};
+#pragma unroll 1
+    for (int pix = threadIdx.x; pix < DN_PIX; pix += DN_THREADS) {
+        const int ty = pix / DN_TX, tx = pix - ty * DN_TX;
         if (!in_tile(tx, ty)) continue;
         const DnPix& p = box(tx, ty);
         v3 sum = mk1(0.f);
         float cum_w = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-#pragma unroll
-            for (int jj = 0; jj < 5; ++jj) {
-                const int dx = i - 2, dy = jj - 2;
-                const DnPix& q = box(tx + dx, ty + dy);
-                float weight;
-                v3 ctmp;
-                if (q.pad == 0.f) {
-                    weight = 0.f * 0.f * 0.f;
-                    ctmp = mk1(0.f);
+#pragma unroll 1
+        for (int tap = 0; tap < 25; ++tap) {
+            const int i = tap / 5, jj = tap - i * 5;
+            const int dx = i - 2, dy = jj - 2;
+            // kernel[i][j] of path_tracer.cu:191-197 (rows 0/4, 1/3 and 2)
+            const float kw = (i == 0 || i == 4) ? kernel5[jj] : ((i == 1 || i == 3) ? kmid[jj] : kctr[jj]);
+            const DnPix& q = box(tx + dx, ty + dy);
+            float weight;
+            v3 ctmp;
+            if (q.pad == 0.f) {
+                weight = 0.f * 0.f * 0.f;
+                ctmp = mk1(0.f);
+            } else {
+                ctmp = mk(q.r, q.g, q.b);
+                if (dx == 0 && dy == 0) {
+                    weight = dn_pair_weight(p, p);
+                } else if (dy > 0 || (dy == 0 && dx > 0)) {
+                    weight = s_wf[pix * 12 + (dy == 0 ? dx - 1 : 2 + 5 * (dy - 1) + dx + 2)];
                 } else {
-                    ctmp = mk(q.r, q.g, q.b);
-                    if (dx == 0 && dy == 0) {
-                        weight = dn_pair_weight(p, p);
-                    } else if (dy > 0 || (dy == 0 && dx > 0)) {
-                        weight = wf[j][dy == 0 ? dx - 1 : 2 + 5 * (dy - 1) + dx + 2];
-                    } else {
-                        const int k = dy == 0 ? -dx - 1 : 2 + 5 * (-dy - 1) - dx + 2;
-                        weight = s_wb[(ty * DN_TX + tx) * 12 + k];
-                    }
+                    weight = s_wb[pix * 12 + (dy == 0 ? -dx - 1 : 2 + 5 * (-dy - 1) - dx + 2)];
                 }
-                sum = sum + (weight * kernel5[i][jj]) * ctmp;
-                cum_w += weight * kernel5[i][jj];
             }
+            sum = sum + (weight * kw) * ctmp;
+            cum_w += weight * kw;
         }
         const v3 dn = sum / cum_w;
         const v3 cl = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),

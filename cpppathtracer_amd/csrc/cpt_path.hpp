@@ -723,7 +723,6 @@ __device__ __forceinline__ uint32_t wide_pair(const f2v e[3], const f2v x[3], co
 struct WalkState {
     lds_i16* top;
     int cur, parked, best, kind, best_rank;
-    int parked2;   // PARK2: a second parked leaf (parked2 >= 0 implies parked >= 0)
     float tmax, limit;
     bool active;   // a walk is in progress (suspended in an earlier round)
 };
@@ -779,7 +778,6 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         ws.top = stk;
         ws.cur = 0;        // the root
         ws.parked = -1;    // leaf-array index of the parked leaf
-        ws.parked2 = -1;
     }
     stamps::lap(7);
     // the walk runs on the lane's WalkState itself (one copy of it lives across the round)
@@ -791,7 +789,6 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     lds_i16*& top = ws.top;   // the next free stack entry (entries are BLK apart)
     int& cur = ws.cur;
     int& parked = ws.parked;
-    int& parked2 = ws.parked2;
     const int sx = oct & 1, sy = (oct >> 1) & 1, sz = oct >> 2;
     auto pop = [&]() -> int {
         if (top == stk) return NONE;
@@ -848,10 +845,6 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
                     parked = leaf_of(cur);
                     cur = pop();
                 }
-                if (PARK2 && cur <= -2 && parked2 < 0) {   // and a second one (PARK2)
-                    parked2 = leaf_of(cur);
-                    cur = pop();
-                }
             }
             // (one ballot per compare, combined as masks: a ballot of anything but a single
             // compare -- __ballot's int argument, a named bool, an || -- is materialised in a
@@ -888,15 +881,7 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
                 limit = walk_limit(tmax);
             }
             parked = -1;
-            if (PARK2) {   // the second parked leaf moves up; a leaf the lane stopped at takes the free slot
-                parked = parked2;
-                parked2 = -1;
-                if (cur <= -2) {
-                    if (parked < 0) parked = leaf_of(cur);
-                    else parked2 = leaf_of(cur);
-                    cur = pop();
-                }
-            } else if (cur <= -2) {   // the lane stopped at a second leaf: park it
+            if (cur <= -2) {   // the lane stopped at a second leaf: park it
                 parked = leaf_of(cur);
                 cur = pop();
             }

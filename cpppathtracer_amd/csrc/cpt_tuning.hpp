@@ -42,13 +42,7 @@ namespace cpt {
 #define CPT_STATIC_FIRST 1
 #endif
 
-// A lane of the wide walk parks up to two leaves before it stops for a leaf round (1: one).
-#ifndef CPT_PARK2
-#define CPT_PARK2 0
-#endif
-
 constexpr int SUSPEND_AT = CPT_SUSPEND_AT;
-constexpr bool PARK2 = CPT_PARK2 != 0;
 constexpr int SUSPEND_MIN_DONE = CPT_SUSPEND_MIN_DONE;
 constexpr int SPEC_LEAF_ROUND = CPT_SPEC_LEAF_ROUND;
 constexpr int DEFER_MISS_ROUND = CPT_DEFER_MISS_ROUND;
