@@ -702,17 +702,40 @@ __global__ void k_rng_pixels(const uint32_t* __restrict__ rowmats, const uint32_
 // (path_tracer.cu:241-254); the alpha byte is not written.
 // ======================================================================================
 // min(exp(-(dist2) / M_PI), 1.0) in double, stored to float (path_tracer.cu:224,228,231), for a
-// float dist2.  Three exact shortcuts of the same value: dist2 == 0 gives exp(-0) = 1;
-// dist2 >= 2341 gives exp(x) with x < -745.1332 (dm::exp's underflow bound), i.e. 0 -- this also
-// covers +inf, for which div_pi would not return the IEEE quotient; otherwise the quotient is
-// dm::div_pi's (correctly rounded: the sequence depends only on dist2's significand, and
-// tests/test_exact_identities.py checks every significand), NaN included (weight 1 through
-// the `w < 1.0` select, as before).
+// float dist2 -- the oracle's dm_exp(-(double)dist2 / REF_PI), branch-free:
+//  * dist2 in (0, 330): x = -dist2/pi in (-105.05, 0), the quotient from dm::div_pi's sequence
+//    (correctly rounded: it depends only on dist2's significand, and every significand is
+//    checked); then dm::exp's own steps -- k, the two-part reduction, the Horner polynomial --
+//    and its ldexp, which for k in [-152, 0] is one exact multiplication by 2^k (v_ldexp_f64);
+//  * dist2 == 0: exp(-0) = 1;  dist2 >= 330 (inf included): exp(x) < 2^-150, which rounds to
+//    float 0;  NaN: exp(NaN) = NaN, and `w < 1.0 ? w : 1.0` gives 1.
+// tests/test_exact_identities.py checks the whole function against the oracle's expression
+// for every float in [0, 2341] and the special values.
 __device__ __forceinline__ float dn_weight(float dist2) {
-    if (dist2 == 0.0f) return 1.0f;
-    if (dist2 >= 2341.0f) return 0.0f;
-    const double w = dm::exp(-dm::div_pi(dist2));
-    return (float)(w < 1.0 ? w : 1.0);
+    constexpr double INV_PI = 1.0 / REF_PI;
+    const double a = (double)dist2;
+    const double q = a * INV_PI;
+    const double x = -__builtin_fma(__builtin_fma(-q, REF_PI, a), INV_PI, q);
+    const double k = __builtin_floor(__builtin_fma(x, dm::kc(dm::INV_LN2), 0.5));
+    const double r = __builtin_fma(-k, dm::kc(dm::LN2_LO), __builtin_fma(-k, dm::kc(dm::LN2_HI), x));
+    double p = 1.0 / 6227020800.0;
+    p = __builtin_fma(r, p, dm::kc(1.0 / 479001600.0));
+    p = __builtin_fma(r, p, dm::kc(1.0 / 39916800.0));
+    p = __builtin_fma(r, p, dm::kc(1.0 / 3628800.0));
+    p = __builtin_fma(r, p, dm::kc(1.0 / 362880.0));
+    p = __builtin_fma(r, p, dm::kc(1.0 / 40320.0));
+    p = __builtin_fma(r, p, dm::kc(1.0 / 5040.0));
+    p = __builtin_fma(r, p, dm::kc(1.0 / 720.0));
+    p = __builtin_fma(r, p, dm::kc(1.0 / 120.0));
+    p = __builtin_fma(r, p, dm::kc(1.0 / 24.0));
+    p = __builtin_fma(r, p, dm::kc(1.0 / 6.0));
+    p = __builtin_fma(r, p, dm::kc(0.5));
+    p = __builtin_fma(r, p, dm::kc(1.0));
+    p = __builtin_fma(r, p, dm::kc(1.0));
+    const double w = __builtin_ldexp(p, (int)k);
+    float f = (float)(w < 1.0 ? w : 1.0);
+    f = dist2 >= 330.0f ? 0.0f : f;
+    return dist2 == 0.0f ? 1.0f : f;
 }
 
 // The 5x5 stencil's pair weight c_w * n_w * p_w between pixels a and b (path_tracer.cu:
@@ -722,22 +745,22 @@ __device__ __forceinline__ float dn_weight(float dist2) {
 // constant 1e30), so its exp only runs where it can differ.
 struct DnPix { float r, g, b, nx, ny, nz, d, pad; };
 
-// The three squared differences in the reference's order (colour, normal clamped at 0 in
-// double, depth); the weight is their dn_weights' product, left to right.  One dn_weight per
-// loop step (not unrolled): the kernel carries a single copy of the exp sequence.
+// The pair weight c_w * n_w * p_w (left to right) from the two pixels' values: colour
+// difference squared, normal difference squared clamped at 0 in double, depth difference
+// squared (path_tracer.cu:219-233).  Inlined where the pairs are independent (the forward
+// pairs of a pixel, unrolled), so several exp sequences are in flight per lane.
 __device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b) {
     v3 t = mk(a.r, a.g, a.b) - mk(b.r, b.g, b.b);
-    const float dc = dot(t, t);
+    const float c_w = dn_weight(dot(t, t));
     t = mk(a.nx, a.ny, a.nz) - mk(b.nx, b.ny, b.nz);
     const double dn = (double)dot(t, t);
+    const float n_w = dn_weight((float)(dn > 0.0 ? dn : 0.0));
     const float dd = (a.d - b.d) * (a.d - b.d);
-    float w = 1.0f;   // 1 * c_w == c_w exactly
-#pragma unroll 1
-    for (int f = 0; f < 3; ++f) {
-        const float d2 = f == 0 ? dc : (f == 1 ? (float)(dn > 0.0 ? dn : 0.0) : dd);
-        w = w * dn_weight(d2);
-    }
-    return w;
+    // a18: the depths are the constant 1e30, so dd == 0 and p_w == 1 (dn_weight(0)) almost
+    // always; the branch skips the sequence when no lane of the wave needs it
+    float p_w = 1.0f;
+    if (dd != 0.0f) p_w = dn_weight(dd);
+    return c_w * n_w * p_w;
 }
 
 // One band of output rows [y0, y1) of the W' x H' launch (W' = 16 floor(W/16), H' likewise).
@@ -746,23 +769,21 @@ __device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b) 
 // wraps into the adjacent row, so rows y - 3 .. y + 3).  mix and out hold the band's rows
 // only.  The full frame is the band [0, H') with row0 = 0.
 //
-// A block takes a tile of DN_TX x DN_TY output pixels.  The stencil indexes neighbours by the
-// LINEAR offset v*W' + u, so tile row r's neighbours are the linear run r*W' + x0 - 2 ..
-// r*W' + x0 + DN_TX + 1 (which wraps into the adjacent image row exactly as the reference
-// does); the block stages those runs for rows ty0 - 2 .. ty0 + DN_TY + 1 in LDS once, as
-// radiance (accumulator / pass count), normal and depth.  Pair weights are evaluated once per
-// unordered pair: every (tile pixel, forward offset) pair (dy > 0, or dy = 0 and dx > 0) in one
-// flat loop over the block's threads, each weight stored for the pixel and handed to its
-// neighbour when that one is in the tile; the pairs whose first pixel lies outside the tile
-// (the halo band above and beside it) from a second flat list.  Each pixel then sums its 25
-// taps in the reference's order.  The loops are not unrolled: one copy of the exp sequence
-// keeps the kernel inside the instruction cache.
-constexpr int DN_TX = 64, DN_TY = 8, DN_THREADS = 256;
+// A block of DN_TX x DN_TY threads takes a tile of as many output pixels, one per thread.  The
+// stencil indexes neighbours by the LINEAR offset v*W' + u, so tile row r's neighbours are the
+// linear run r*W' + x0 - 2 .. r*W' + x0 + DN_TX + 1 (which wraps into the adjacent image row
+// exactly as the reference does); the block stages those runs for rows ty0 - 2 .. ty0 + DN_TY
+// + 1 in LDS once, as radiance (accumulator / pass count), normal and depth.  Pair weights are
+// evaluated once per unordered pair: each pixel evaluates its 12 forward neighbours (dy > 0, or
+// dy = 0 and dx > 0; unrolled, kept in registers) and hands each weight to the neighbour when
+// that one is in the tile; the pairs whose first pixel lies outside the tile (the halo band
+// above and beside it) are evaluated by the whole block from a flat list.  Each pixel then
+// sums its 25 taps in the reference's order.  30 KB of LDS per block: five blocks per CU.
+constexpr int DN_TX = 64, DN_TY = 4, DN_THREADS = DN_TX * DN_TY;
 constexpr int DN_BX = DN_TX + 4, DN_BY = DN_TY + 4;   // staged box (2-pixel halo each side)
-constexpr int DN_PIX = DN_TX * DN_TY;
 // forward offsets (dx, dy), k = 0..11: dy = 0, dx = 1, 2; dy = 1, dx = -2..2; dy = 2, dx = -2..2
-__device__ __forceinline__ int dn_fdx(int k) { return k < 2 ? k + 1 : ((k - 2) % 5) - 2; }
-__device__ __forceinline__ int dn_fdy(int k) { return k < 2 ? 0 : (k < 7 ? 1 : 2); }
+__host__ __device__ constexpr int dn_fdx(int k) { return k < 2 ? k + 1 : ((k - 2) % 5) - 2; }
+__host__ __device__ constexpr int dn_fdy(int k) { return k < 2 ? 0 : (k < 7 ? 1 : 2); }
 
 __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __restrict__ accum,
                                                            const float* __restrict__ normal,
@@ -770,8 +791,7 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
                                                            uint8_t* __restrict__ out, int width, int row0, int y0,
                                                            int y1, int w_eff, int h_eff, float inv_idx) {
     __shared__ DnPix s_pix[DN_BY * DN_BX];
-    __shared__ float s_wf[DN_PIX * 12];   // forward weight k of tile pixel (ty, tx)
-    __shared__ float s_wb[DN_PIX * 12];   // backward weight k: w(p - d_k, p)
+    __shared__ float s_wb[DN_THREADS * 12];   // backward weight k of tile pixel (ty, tx): w(p - d_k, p)
     const int x0 = blockIdx.x * DN_TX, ty0 = y0 + blockIdx.y * DN_TY;
     const int tw = min(DN_TX, w_eff - x0), th = min(DN_TY, y1 - ty0);   // the tile's extent
     const int limit = w_eff * h_eff;
@@ -799,18 +819,17 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
     __syncthreads();
     auto box = [&](int tx, int ty) -> const DnPix& { return s_pix[(ty + 2) * DN_BX + tx + 2]; };
     auto in_tile = [&](int tx, int ty) { return tx >= 0 && tx < tw && ty >= 0 && ty < th; };
-    // ---- forward pairs of the tile's pixels ---------------------------------------------
-#pragma unroll 1
-    for (int e = threadIdx.x; e < DN_PIX * 12; e += DN_THREADS) {
-        const int pix = e / 12, k = e - pix * 12;
-        const int ty = pix / DN_TX, tx = pix - ty * DN_TX;
-        if (!in_tile(tx, ty)) continue;
+    const int ty = threadIdx.x / DN_TX, tx = threadIdx.x - ty * DN_TX;
+    const bool mine = in_tile(tx, ty);
+    const DnPix p = box(tx, ty);
+    // ---- this pixel's forward pairs (independent: unrolled) ------------------------------
+    float wf[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
         const int dx = dn_fdx(k), dy = dn_fdy(k);
-        const DnPix& p = box(tx, ty);
         const DnPix& q = box(tx + dx, ty + dy);
-        const float w = q.pad != 0.f ? dn_pair_weight(p, q) : 0.f;
-        s_wf[pix * 12 + k] = w;
-        if (in_tile(tx + dx, ty + dy)) s_wb[((ty + dy) * DN_TX + tx + dx) * 12 + k] = w;
+        wf[k] = (mine && q.pad != 0.f) ? dn_pair_weight(p, q) : 0.f;
+        if (mine && in_tile(tx + dx, ty + dy)) s_wb[((ty + dy) * DN_TX + tx + dx) * 12 + k] = wf[k];
     }
     // ---- pairs (s, t = s + d) with t in the tile and s outside it ------------------------
     // For offset k the targets are the first dy rows of the tile (all columns), then in the
@@ -819,9 +838,8 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
         int total = 0;
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
-            const int dx = dn_fdx(k), dy = dn_fdy(k), adx = dx < 0 ? -dx : dx;
-            const int rows_top = min(dy, th), cols = min(adx, tw);
-            total += rows_top * tw + (th - rows_top) * cols;
+            const int adx = dn_fdx(k) < 0 ? -dn_fdx(k) : dn_fdx(k), rows_top = min(dn_fdy(k), th);
+            total += rows_top * tw + (th - rows_top) * min(adx, tw);
         }
 #pragma unroll 1
         for (int e = threadIdx.x; e < total; e += DN_THREADS) {
@@ -836,40 +854,44 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
                 if (r < cnt) break;
                 r -= cnt;
             }
-            int tx, ty;
+            int sx, sy;
             if (r < rows_top * tw) {
-                ty = r / tw;
-                tx = r - ty * tw;
+                sy = r / tw;
+                sx = r - sy * tw;
             } else {
                 r -= rows_top * tw;
-                ty = rows_top + r / cols;
-                const int c = r - (ty - rows_top) * cols;
-                tx = dx > 0 ? c : tw - adx + c;
+                sy = rows_top + r / cols;
+                const int c = r - (sy - rows_top) * cols;
+                sx = dx > 0 ? c : tw - adx + c;
             }
-            const DnPix& t = box(tx, ty);
-            const DnPix& sp = box(tx - dx, ty - dy);
-            const float w = sp.pad != 0.f ? dn_pair_weight(sp, t) : 0.f;
-            s_wb[(ty * DN_TX + tx) * 12 + k] = w;
+            const DnPix& t = box(sx, sy);
+            const DnPix& sp = box(sx - dx, sy - dy);
+            s_wb[(sy * DN_TX + sx) * 12 + k] = sp.pad != 0.f ? dn_pair_weight(sp, t) : 0.f;
         }
     }
     __syncthreads();
+    if (!mine) return;
     // ---- the 25 taps in the reference's order (i = dx outer, j = dy inner) -----------------
-    const float kernel5[5] = {1.f, 4.f, 7.f, 4.f, 1.f};   // the rows of kernel[5][5] (path_tracer.cu:191-197)
-    const float kmid[5] = {4.f, 16.f, 26.f, 16.f, 4.f};
-    const float kctr[5] = {7.f, 26.f, 41.f, 26.f, 7.f};
-#pragma unroll 1
-    for (int pix = threadIdx.x; pix < DN_PIX; pix += DN_THREADS) {
-        const int ty = pix / DN_TX, tx = pix - ty * DN_TX;
-        if (!in_tile(tx, ty)) continue;
-        const DnPix& p = box(tx, ty);
-        v3 sum = mk1(0.f);
-        float cum_w = 0.0f;
-#pragma unroll 1
-        for (int tap = 0; tap < 25; ++tap) {
-            const int i = tap / 5, jj = tap - i * 5;
+    constexpr float kernel5[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
+                                     {4.f, 16.f, 26.f, 16.f, 4.f},
+                                     {7.f, 26.f, 41.f, 26.f, 7.f},
+                                     {4.f, 16.f, 26.f, 16.f, 4.f},
+                                     {1.f, 4.f, 7.f, 4.f, 1.f}};
+    // the centre tap: w(p, p) = 1 for finite values (every squared difference is 0); the
+    // general expression otherwise (inf - inf, NaN)
+    const bool finite = __builtin_isfinite(p.r) && __builtin_isfinite(p.g) && __builtin_isfinite(p.b) &&
+                        __builtin_isfinite(p.nx) && __builtin_isfinite(p.ny) && __builtin_isfinite(p.nz) &&
+                        __builtin_isfinite(p.d);
+    float w_self = 1.0f;
+    if (!finite) w_self = dn_pair_weight(p, p);
+    const float* wb = s_wb + threadIdx.x * 12;
+    v3 sum = mk1(0.f);
+    float cum_w = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+#pragma unroll
+        for (int jj = 0; jj < 5; ++jj) {
             const int dx = i - 2, dy = jj - 2;
-            // kernel[i][j] of path_tracer.cu:191-197 (rows 0/4, 1/3 and 2)
-            const float kw = (i == 0 || i == 4) ? kernel5[jj] : ((i == 1 || i == 3) ? kmid[jj] : kctr[jj]);
             const DnPix& q = box(tx + dx, ty + dy);
             float weight;
             v3 ctmp;
@@ -878,33 +900,29 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
                 ctmp = mk1(0.f);
             } else {
                 ctmp = mk(q.r, q.g, q.b);
-                if (dx == 0 && dy == 0) {
-                    weight = dn_pair_weight(p, p);
-                } else if (dy > 0 || (dy == 0 && dx > 0)) {
-                    weight = s_wf[pix * 12 + (dy == 0 ? dx - 1 : 2 + 5 * (dy - 1) + dx + 2)];
-                } else {
-                    weight = s_wb[pix * 12 + (dy == 0 ? -dx - 1 : 2 + 5 * (-dy - 1) - dx + 2)];
-                }
+                if (dx == 0 && dy == 0) weight = w_self;
+                else if (dy > 0 || (dy == 0 && dx > 0)) weight = wf[dy == 0 ? dx - 1 : 2 + 5 * (dy - 1) + dx + 2];
+                else weight = wb[dy == 0 ? -dx - 1 : 2 + 5 * (-dy - 1) - dx + 2];
             }
-            sum = sum + (weight * kw) * ctmp;
-            cum_w += weight * kw;
+            sum = sum + (weight * kernel5[i][jj]) * ctmp;
+            cum_w += weight * kernel5[i][jj];
         }
-        const v3 dn = sum / cum_w;
-        const v3 cl = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),
-                         __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));
-        const int y = ty0 + ty, x = x0 + tx;
-        const size_t bself = (size_t)(y - y0) * width + x;   // this pixel in the band's mix / out
-        v3 m = mk(mix[3 * bself], mix[3 * bself + 1], mix[3 * bself + 2]);
-        m = m + inv_idx * (cl - m);      // lerp(a, b, t) = a + t*(b-a) (helper_math.h:1154-1157)
-        mix[3 * bself] = m.x;
-        mix[3 * bself + 1] = m.y;
-        mix[3 * bself + 2] = m.z;
-        // bytes 0..2 = 255.99 * (b, g, r); the alpha byte is never written by the reference and
-        // stays the buffer's zero here (one 32-bit store)
-        const uint32_t bgr = (uint32_t)(uint8_t)(255.99f * m.z) | ((uint32_t)(uint8_t)(255.99f * m.y) << 8) |
-                             ((uint32_t)(uint8_t)(255.99f * m.x) << 16);
-        reinterpret_cast<uint32_t*>(out)[bself] = bgr;
     }
+    const v3 dn = sum / cum_w;
+    const v3 cl = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),
+                     __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));
+    const int y = ty0 + ty, x = x0 + tx;
+    const size_t bself = (size_t)(y - y0) * width + x;   // this pixel in the band's mix / out
+    v3 m = mk(mix[3 * bself], mix[3 * bself + 1], mix[3 * bself + 2]);
+    m = m + inv_idx * (cl - m);      // lerp(a, b, t) = a + t*(b-a) (helper_math.h:1154-1157)
+    mix[3 * bself] = m.x;
+    mix[3 * bself + 1] = m.y;
+    mix[3 * bself + 2] = m.z;
+    // bytes 0..2 = 255.99 * (b, g, r); the alpha byte is never written by the reference and stays
+    // the buffer's zero here (one 32-bit store)
+    const uint32_t bgr = (uint32_t)(uint8_t)(255.99f * m.z) | ((uint32_t)(uint8_t)(255.99f * m.y) << 8) |
+                         ((uint32_t)(uint8_t)(255.99f * m.x) << 16);
+    reinterpret_cast<uint32_t*>(out)[bself] = bgr;
 }
 
 hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,

@@ -81,3 +81,83 @@ def test_exact_identities(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout
     assert "bad 0" in r.stdout
+
+
+# The display's branch-free pair weight (cpt_kernels.hip dn_weight) against the oracle's own
+# expression min(exp(-(double)d2 / M_PI), 1.0) stored to float (oracle or_exp = dm_exp,
+# path_tracer.cu:224,228,231), for every float d2 in [0, 2341] -- the quotient, dm_exp's steps
+# with a plain ldexp below x = -105.05, and the shortcuts (0 -> 1, >= 330 -> 0) -- and the
+# special values.  The harness calls the oracle library (test infrastructure).
+DN_SRC = r"""
+#include <dlfcn.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+static const double REF_PI = 3.14159265358979323846;
+static const double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+static const double INV_LN2 = 1.44269504088896338700e+00;
+static double (*or_exp)(double);
+static float ref_w(float d2) {
+    double w = or_exp(-((double)d2) / REF_PI);
+    return (float)(w < 1.0 ? w : 1.0);
+}
+static float fast_w(float d2) {   /* cpt_kernels.hip dn_weight, operation for operation */
+    const double INV_PI = 1.0 / REF_PI;
+    const double a = (double)d2, q = a * INV_PI;
+    const double x = -fma(fma(-q, REF_PI, a), INV_PI, q);
+    const double k = floor(fma(x, INV_LN2, 0.5));
+    const double r = fma(-k, LN2_LO, fma(-k, LN2_HI, x));
+    double p = 1.0 / 6227020800.0;
+    const double c[13] = {1.0 / 479001600.0, 1.0 / 39916800.0, 1.0 / 3628800.0, 1.0 / 362880.0, 1.0 / 40320.0,
+                          1.0 / 5040.0, 1.0 / 720.0, 1.0 / 120.0, 1.0 / 24.0, 1.0 / 6.0, 0.5, 1.0, 1.0};
+    for (int i = 0; i < 13; ++i) p = fma(r, p, c[i]);
+    int ki = (k == k) ? (int)k : 0;    /* (the device's cvt of a NaN: any k, ldexp(NaN) stays NaN) */
+    const double w = ldexp(p, ki);
+    float f = (float)(w < 1.0 ? w : 1.0);
+    f = d2 >= 330.0f ? 0.0f : f;
+    return d2 == 0.0f ? 1.0f : f;
+}
+static uint32_t g_lim;
+static unsigned long long g_bad[8];
+static void* run(void* arg) {
+    int t = (int)(intptr_t)arg;
+    for (uint32_t b = (uint32_t)t; b <= g_lim; b += 8) {
+        float d; memcpy(&d, &b, 4);
+        float x = ref_w(d), y = fast_w(d);
+        if (memcmp(&x, &y, 4) != 0) { if (g_bad[t] < 3) printf("dn_weight %a: %a vs %a\n", d, x, y); g_bad[t]++; }
+    }
+    return 0;
+}
+int main(int argc, char** argv) {
+    void* h = dlopen(argv[1], RTLD_NOW);
+    if (!h) { printf("dlopen failed\n"); return 2; }
+    or_exp = (double (*)(double))dlsym(h, "or_exp");
+    float lim = 2341.0f; memcpy(&g_lim, &lim, 4);
+    pthread_t th[8];
+    for (int t = 0; t < 8; ++t) pthread_create(&th[t], 0, run, (void*)(intptr_t)t);
+    unsigned long long bad = 0;
+    for (int t = 0; t < 8; ++t) { pthread_join(th[t], 0); bad += g_bad[t]; }
+    const float sp[] = {INFINITY, NAN, -0.0f, 3.4e38f, 1e-45f, 329.99998f, 330.0f, 2340.9f};
+    for (int i = 0; i < 8; ++i) {
+        float x = ref_w(sp[i]), y = fast_w(sp[i]);
+        if (memcmp(&x, &y, 4) != 0) { printf("special %a: %a vs %a\n", sp[i], x, y); bad++; }
+    }
+    printf("bad %llu\n", bad);
+    return bad != 0;
+}
+"""
+
+
+def test_denoise_weight_exhaustive(tmp_path):
+    import oracle
+    lib = oracle.build()
+    src = tmp_path / "dnw.c"
+    exe = tmp_path / "dnw"
+    src.write_text(DN_SRC)
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-fno-fast-math", "-o", str(exe), str(src), "-lm", "-ldl",
+                    "-lpthread"], check=True)
+    r = subprocess.run([str(exe), lib], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout
+    assert "bad 0" in r.stdout
