@@ -83,6 +83,9 @@ def parse_args(argv=None):
                          "Denoising + Mix + BGRA8 copy; one JSON line, not the headline)")
     ap.add_argument("--dispatch-contexts", type=int, default=8,
                     help="--dispatch: also time the loop with this many row-tile contexts + gather (1: skip)")
+    ap.add_argument("--dispatch-schedule", default="previous", choices=["previous", "tiles"],
+                    help="--dispatch: the per-pass render's tile order (previous: heaviest first by the last pass's "
+                         "draws, as PathTracer::DispatchRay does; tiles: row-major)")
     ap.add_argument("--profile-json", default=None,
                     help="rocprof summary of this workload (profiles/rocprof_*.json, tools/rocprof_summary.py)")
     return ap.parse_args(argv)
@@ -574,7 +577,7 @@ def dispatch_bench(args):
     for k in range(warm + K):
         idx = k + 1
         t0 = time.perf_counter()
-        r.render(cam_at(idx), 1, depth, aux=True, ordered=args.walk == "ordered")
+        r.render(cam_at(idx), 1, depth, aux=True, ordered=args.walk == "ordered", schedule=args.dispatch_schedule)
         r.denoise_mix(idx, out=host)   # waits for the frame on the host
         t1 = time.perf_counter()
         if k >= warm:
@@ -609,7 +612,8 @@ def dispatch_bench(args):
             idx = k + 1
             t0 = time.perf_counter()
             for t in tiles:
-                t.render(cam_at(idx), 1, depth, aux=True, ordered=args.walk == "ordered")
+                t.render(cam_at(idx), 1, depth, aux=True, ordered=args.walk == "ordered",
+                         schedule=args.dispatch_schedule)
             for t in tiles:
                 frame.gather_rows(t)
             frame.denoise_mix(idx, out=host)
@@ -634,7 +638,8 @@ def dispatch_bench(args):
     out = {
         "metric": "ms per DispatchRay pass (1 spp SamplePixel + Denoising + Mix + BGRA8 to the host)",
         "config": {"workload": f"{args.config}: {cfg['scene']} {W}x{H} 1spp depth {depth} per pass",
-                   "width": W, "height": H, "walk": args.walk, "passes": K, "warmup": warm,
+                   "width": W, "height": H, "walk": args.walk, "schedule": args.dispatch_schedule, "passes": K,
+                   "warmup": warm,
                    "host_buffer": "pinned"},
         "higher_is_better": False,
         "single": one,

@@ -76,6 +76,7 @@ CPT_TRAVERSAL_PLAIN_LEAVES = 0x400
 CPT_SCHEDULE_COST = 0x800
 CPT_SCHEDULE_CONSOLIDATE = 0x1000
 CPT_SCHEDULE_NO_CONSOLIDATE = 0x2000
+CPT_SCHEDULE_PREVIOUS = 0x4000
 CPT_ERR_STATE = 5
 CPT_ERR_DEVICE = 7   # a kernel abandoned work (reported at the next synchronising call)
 

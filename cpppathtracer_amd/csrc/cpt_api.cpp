@@ -514,8 +514,10 @@ bool PathTracer::EnsureFrame(const MotionalCamera& cam) {
 bool PathTracer::RenderPass(MotionalCamera& cam, int spp, bool accumulate) {
     if (!SyncScene() || !EnsureFrame(cam)) return false;
     // many passes per pixel: heaviest tiles first (same image, shorter tail)
+    // few passes (the DispatchRay loop): heaviest tiles first by the previous pass's work, no pilot
     const uint32_t flags = CPT_RENDER_AUX | (accumulate ? CPT_RENDER_ACCUMULATE : 0u) |
-                           (ordered_walk_ ? CPT_TRAVERSAL_ORDERED : 0u) | (spp >= 64 ? CPT_SCHEDULE_COST : 0u);
+                           (ordered_walk_ ? CPT_TRAVERSAL_ORDERED : 0u) |
+                           (spp >= 64 ? CPT_SCHEDULE_COST : CPT_SCHEDULE_PREVIOUS);
     if (!frame_) {
         if (cpt_render(tiles_[0].ctx, reinterpret_cast<const cpt_camera*>(&cam), spp, (int)max_recursion_depth_,
                        flags | CPT_RENDER_SYNC) != CPT_OK)

@@ -73,6 +73,9 @@ void free_frame(cpt_ctx* c) {
     (void)hipFree(c->d_scratch_m); c->d_scratch_m = nullptr;
     (void)hipFree(c->d_sched); c->d_sched = nullptr; c->cap_sched = 0;
     (void)hipFree(c->d_tile_order); c->d_tile_order = nullptr; c->cap_tile_order = 0;
+    (void)hipFree(c->d_prev_d); c->d_prev_d = nullptr;
+    (void)hipFree(c->d_prev_order); c->d_prev_order = nullptr;
+    c->prev_d_valid = c->prev_order_valid = false;
     c->frame_set = c->rng_set = false;
 }
 
@@ -285,6 +288,7 @@ int cpt_init_rng(cpt_ctx* c, uint64_t seed) {
     if (c->n_rows == 0) { c->rng_set = true; return CPT_OK; }
     if (!c->d_scratch_w) HIP_TRY(c, hipMalloc((void**)&c->d_scratch_w, 5 * (size_t)c->width * sizeof(uint32_t)));
     if (!c->d_scratch_m) HIP_TRY(c, hipMalloc((void**)&c->d_scratch_m, (size_t)c->n_rows * 800 * sizeof(uint32_t)));
+    c->prev_d_valid = false;   // CPT_SCHEDULE_PREVIOUS counts draws from the next render on
     uint32_t st[6];
     curand_seed_state(seed, st);
     HIP_TRY(c, cpt::launch_init_rng(c->d_jumps, st, c->width, c->d_rows, c->n_rows, c->d_scratch_w, c->d_scratch_m,
@@ -314,6 +318,7 @@ int cpt_write_rng(cpt_ctx* c, const uint32_t* planar6) {
     size_t n = 6 * (size_t)c->n_rows * c->width;
     if (n) HIP_TRY(c, hipMemcpy(c->d_rng, planar6, n * sizeof(uint32_t), hipMemcpyHostToDevice));
     c->rng_set = true;
+    c->prev_d_valid = false;
     return CPT_OK;
 }
 
@@ -411,6 +416,17 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
         c->last_launches = launches;
     } else {
         c->last_launches = 1;
+        bool prev_schedule = false;
+        if (!(flags & CPT_SCHEDULE_COST) && (flags & CPT_SCHEDULE_PREVIOUS) && spp > 0 && c->n_rows > 0) {
+            // the order the previous render's draws gave; the draws of this one from here
+            const size_t npix = (size_t)c->n_rows * c->width;
+            if (c->prev_order_valid) p.tile_order = c->d_prev_order;
+            if (!c->d_prev_d) HIP_TRY(c, hipMalloc((void**)&c->d_prev_d, npix * sizeof(uint32_t)));
+            if (!c->prev_d_valid)
+                HIP_TRY(c, hipMemcpyAsync(c->d_prev_d, c->d_rng + 5 * npix, npix * sizeof(uint32_t),
+                                          hipMemcpyDeviceToDevice, s));
+            prev_schedule = true;
+        }
         if ((flags & CPT_SCHEDULE_COST) && spp > 0 && c->n_rows > 0) {
             // pilot: 1 pass per 512 (1..4), then the tiles sorted heaviest first
             const int passes = std::min(4, std::max(1, spp / 512));
@@ -449,8 +465,26 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
         }
         HIP_TRY(c, hipEventRecord(c->ev_main, s));
         HIP_TRY(c, cpt::launch_megakernel(p, (flags & CPT_RENDER_STATS) != 0, aux, s));
+        HIP_TRY(c, hipEventRecord(c->ev_stop, s));
+        if (prev_schedule) {
+            // the next render's order from this one's draws (after the timed events: the render's
+            // own time is the kernel's; the stream runs this before the caller's next work)
+            const size_t n_tiles = (size_t)((c->width + 7) / 8) * ((c->n_rows + 7) / 8);
+            const size_t bytes = cpt::tile_schedule_scratch_bytes(c->width, c->n_rows);
+            if (c->cap_sched < bytes) {
+                (void)hipFree(c->d_sched);
+                c->d_sched = nullptr;
+                c->cap_sched = 0;
+                HIP_TRY(c, hipMalloc(&c->d_sched, bytes));
+                c->cap_sched = bytes;
+            }
+            if (!c->d_prev_order) HIP_TRY(c, hipMalloc((void**)&c->d_prev_order, n_tiles * sizeof(uint32_t)));
+            HIP_TRY(c, cpt::launch_tile_order_from_draws(p, c->d_prev_d, c->d_sched, c->cap_sched, c->d_prev_order, s));
+            c->prev_d_valid = true;
+            c->prev_order_valid = true;
+        }
     }
-    HIP_TRY(c, hipEventRecord(c->ev_stop, s));
+    if (flags & CPT_PATH_WAVEFRONT) HIP_TRY(c, hipEventRecord(c->ev_stop, s));
     c->have_timing = true;
     if (flags & CPT_RENDER_SYNC) return sync_checked(c);
     return CPT_OK;

@@ -96,6 +96,11 @@ struct cpt_ctx {
     size_t cap_sched = 0;
     uint32_t* d_tile_order = nullptr;
     size_t cap_tile_order = 0;
+    // CPT_SCHEDULE_PREVIOUS: the Weyl plane after the last such render, and the tile order
+    // its draws gave (the next render's dequeue order)
+    uint32_t* d_prev_d = nullptr;
+    uint32_t* d_prev_order = nullptr;
+    bool prev_d_valid = false, prev_order_valid = false;
     uint4* d_resume = nullptr;          // tail consolidation: handed-over chains (5 x uint4 each)
     size_t cap_resume = 0;
     cpt::WfState wf{};           // wavefront path state (allocated on first use)

@@ -83,6 +83,10 @@ enum : uint32_t {
 // megakernel sums each 8x8 tile's work, then `order` (one u32 per tile) gets the tiles
 // heaviest first.  `scratch` holds tile_schedule_scratch_bytes() bytes.
 size_t tile_schedule_scratch_bytes(int width, int n_rows);
+// CPT_SCHEDULE_PREVIOUS: each 8x8 tile's RNG draws since `d_prev` (the Weyl plane d of the
+// states, planar [5] of p.rng), then d_prev := d; the tiles sorted heaviest first into `order`.
+hipError_t launch_tile_order_from_draws(const KParams& p, uint32_t* d_prev, void* scratch, size_t scratch_bytes,
+                                        uint32_t* order, hipStream_t stream);
 hipError_t launch_tile_schedule(const KParams& p, int passes, void* scratch, size_t scratch_bytes, uint32_t* order,
                                 hipStream_t stream);
 

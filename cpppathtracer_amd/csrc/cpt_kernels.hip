@@ -754,7 +754,11 @@ __device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b) 
     const float c_w = dn_weight(dot(t, t));
     t = mk(a.nx, a.ny, a.nz) - mk(b.nx, b.ny, b.nz);
     const double dn = (double)dot(t, t);
-    const float n_w = dn_weight((float)(dn > 0.0 ? dn : 0.0));
+    const float dnf = (float)(dn > 0.0 ? dn : 0.0);
+    // equal normals (a flat surface: the floor's are exactly (0, +-1, 0)) give n_w = 1; the
+    // branch skips the sequence when no lane of the wave needs it
+    float n_w = 1.0f;
+    if (dnf != 0.0f) n_w = dn_weight(dnf);
     const float dd = (a.d - b.d) * (a.d - b.d);
     // a18: the depths are the constant 1e30, so dd == 0 and p_w == 1 (dn_weight(0)) almost
     // always; the branch skips the sequence when no lane of the wave needs it
@@ -778,8 +782,11 @@ __device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b) 
 // dy = 0 and dx > 0; unrolled, kept in registers) and hands each weight to the neighbour when
 // that one is in the tile; the pairs whose first pixel lies outside the tile (the halo band
 // above and beside it) are evaluated by the whole block from a flat list.  Each pixel then
-// sums its 25 taps in the reference's order.  30 KB of LDS per block: five blocks per CU.
-constexpr int DN_TX = 64, DN_TY = 4, DN_THREADS = DN_TX * DN_TY;
+// sums its 25 taps in the reference's order.
+#ifndef CPT_DN_TY
+#define CPT_DN_TY 8
+#endif
+constexpr int DN_TX = 64, DN_TY = CPT_DN_TY, DN_THREADS = DN_TX * DN_TY;
 constexpr int DN_BX = DN_TX + 4, DN_BY = DN_TY + 4;   // staged box (2-pixel halo each side)
 // forward offsets (dx, dy), k = 0..11: dy = 0, dx = 1, 2; dy = 1, dx = -2..2; dy = 2, dx = -2..2
 __host__ __device__ constexpr int dn_fdx(int k) { return k < 2 ? k + 1 : ((k - 2) % 5) - 2; }
@@ -1063,6 +1070,54 @@ size_t tile_schedule_scratch_bytes(int width, int n_rows) {
     (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                                        (const uint32_t*)nullptr, (uint32_t*)nullptr, n);
     return 3 * (size_t)n * sizeof(uint32_t) + temp + 256;
+}
+
+// CPT_SCHEDULE_PREVIOUS: one wave per 8x8 tile; lane k = pixel k of the tile (decode_pixel's
+// layout).  A pixel's draws since the last call are (d - d_prev) / 362437 mod 2^32 (every
+// curand() adds 362437 to d, an odd number: a multiplication by its inverse mod 2^32).
+__global__ void __launch_bounds__(64) k_tile_draws(const uint32_t* __restrict__ d_now, uint32_t* __restrict__ d_prev,
+                                                   int width, int n_rows, uint32_t* __restrict__ cost) {
+    constexpr uint32_t WEYL = 362437u;
+    constexpr uint32_t INV = [] {   // WEYL^-1 mod 2^32 (Newton: x <- x (2 - WEYL x))
+        uint32_t x = WEYL;
+        for (int i = 0; i < 5; ++i) x *= 2u - WEYL * x;
+        return x;
+    }();
+    static_assert(WEYL * INV == 1u, "inverse of the Weyl step");
+    const int tiles_x = (width + 7) >> 3;
+    const uint32_t tile = blockIdx.x;
+    const int k = threadIdx.x;
+    const int x = (int)(tile % tiles_x) * 8 + (k & 7), ri = (int)(tile / tiles_x) * 8 + (k >> 3);
+    uint32_t draws = 0;
+    if (x < width && ri < n_rows) {
+        const size_t pix = (size_t)ri * width + x;
+        const uint32_t d = d_now[pix];
+        draws = (d - d_prev[pix]) * INV;
+        d_prev[pix] = d;
+    }
+    const uint64_t sum = wave_sum(draws);
+    if (k == 0) cost[tile] = (uint32_t)(sum < 0xffffffffull ? sum : 0xffffffffull);
+}
+
+hipError_t launch_tile_order_from_draws(const KParams& p, uint32_t* d_prev, void* scratch, size_t scratch_bytes,
+                                        uint32_t* order, hipStream_t stream) {
+    const int n = ((p.width + 7) / 8) * ((p.n_rows + 7) / 8);
+    if (n <= 0) return hipSuccess;
+    uint32_t* cost = (uint32_t*)scratch;
+    uint32_t* cost_sorted = cost + n;
+    uint32_t* ids = cost_sorted + n;
+    void* temp = (void*)(((uintptr_t)(ids + n) + 255) & ~(uintptr_t)255);
+    size_t temp_bytes = scratch_bytes - ((char*)temp - (char*)scratch);
+    const size_t npix = (size_t)p.n_rows * p.width;
+    hipLaunchKernelGGL(k_tile_draws, dim3((unsigned)n), dim3(64), 0, stream, p.rng + 5 * npix, d_prev, p.width,
+                       p.n_rows, cost);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_iota, dim3((n + 255) / 256), dim3(256), 0, stream, ids, (uint32_t)n);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, cost, cost_sorted, ids, order, n, 0, 32,
+                                                        stream);
 }
 
 hipError_t launch_tile_schedule(const KParams& p0, int passes, void* scratch, size_t scratch_bytes, uint32_t* order,

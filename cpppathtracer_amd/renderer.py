@@ -10,7 +10,8 @@ import numpy as np
 
 from . import _lib
 from ._lib import (CPT_PATH_WAVEFRONT, CPT_RENDER_ACCUMULATE, CPT_RENDER_AUX, CPT_RENDER_STATS, CPT_RENDER_SYNC,
-                   CPT_SCHEDULE_CONSOLIDATE, CPT_SCHEDULE_COST, CPT_SCHEDULE_NO_CONSOLIDATE, CPT_TRAVERSAL_ORDERED,
+                   CPT_SCHEDULE_CONSOLIDATE, CPT_SCHEDULE_COST, CPT_SCHEDULE_NO_CONSOLIDATE, CPT_SCHEDULE_PREVIOUS,
+                   CPT_TRAVERSAL_ORDERED,
                    CPT_TRAVERSAL_PLAIN_LEAVES, CptError, check)
 
 PATHS = ("megakernel", "wavefront")
@@ -143,14 +144,16 @@ class Renderer:
         counts, CPT_TRAVERSAL_PLAIN_LEAVES) instead of parking leaves for wave-wide rounds.
         schedule: "tiles" (8x8 tiles dequeued in row-major order) or "cost" (CPT_SCHEDULE_COST: a
         short pilot render measures each tile's work and the megakernel dequeues the tiles
-        heaviest first; same results, DESIGN.md §Cost schedule).
+        heaviest first; same results, DESIGN.md §Cost schedule) or "previous"
+        (CPT_SCHEDULE_PREVIOUS: heaviest first by the previous such render's per-tile RNG draws,
+        no pilot; for repeated renders of few passes, the DispatchRay loop).
         consolidate: None (the library's default: on for frames of <= 4 pixels per lane and
         spp >= 512), True or
         False (CPT_SCHEDULE_[NO_]CONSOLIDATE): the megakernel's tail consolidation, same results."""
         if path not in PATHS:
             raise ValueError(f"path must be one of {PATHS}")
-        if schedule not in ("tiles", "cost"):
-            raise ValueError("schedule must be 'tiles' or 'cost'")
+        if schedule not in ("tiles", "cost", "previous"):
+            raise ValueError("schedule must be 'tiles', 'cost' or 'previous'")
         c = np.ascontiguousarray(np.array(cam, dtype=CAMERA_DTYPE))
         f = flags | (CPT_PATH_WAVEFRONT if path == "wavefront" else 0)
         f |= CPT_TRAVERSAL_ORDERED if ordered else 0
@@ -160,6 +163,7 @@ class Renderer:
         f |= CPT_RENDER_STATS if stats else 0
         f |= CPT_RENDER_SYNC if sync else 0
         f |= CPT_SCHEDULE_COST if schedule == "cost" else 0
+        f |= CPT_SCHEDULE_PREVIOUS if schedule == "previous" else 0
         if consolidate is not None:
             f |= CPT_SCHEDULE_CONSOLIDATE if consolidate else CPT_SCHEDULE_NO_CONSOLIDATE
         self._check(self._L.cpt_render(self._ctx, _p(c), spp, max_depth, f))

@@ -165,6 +165,13 @@ typedef struct cpt_ctx cpt_ctx;
  * cannot complete ends the render with CPT_ERR_DEVICE, never with silently missing pixels. */
 #define CPT_SCHEDULE_CONSOLIDATE    0x1000u
 #define CPT_SCHEDULE_NO_CONSOLIDATE 0x2000u
+/* Megakernel pixel schedule without a pilot, for renders of few passes that repeat over the
+ * same frame (the DispatchRay loop, path_tracer.cu:256-306): the tiles are dequeued heaviest
+ * first by the work of the context's PREVIOUS render with this flag -- each tile's RNG draws,
+ * read off the XORWOW Weyl counters (d advances by 362437 per draw), which follow the path
+ * lengths -- and the first render in a frame uses the row-major order.  Identical results;
+ * ignored with CPT_SCHEDULE_COST and by CPT_PATH_WAVEFRONT. */
+#define CPT_SCHEDULE_PREVIOUS       0x4000u
 
 int cpt_abi_version(void);
 const char* cpt_status_string(int status);

@@ -475,3 +475,26 @@ def test_hbm_read_probe(gpu):
     for a 1 GiB buffer: above 1 TB/s, below the 8 TB/s spec (with 5% slack for timer noise)."""
     gbps = gpu.measure_read_bandwidth(1 << 30, 5)
     assert 1000.0 < gbps < 8400.0, gbps
+
+
+@pytest.mark.parametrize("ordered", [True, False])
+def test_previous_pass_schedule(gpu, oracle_mod, sky, ordered):
+    """CPT_SCHEDULE_PREVIOUS (the DispatchRay loop's order: tiles heaviest first by the last
+    pass's RNG draws, no pilot): five accumulated 1-spp renders, the first in row-major order and
+    the others in the order the draws gave, equal the oracle's 5-pass render bit for bit; a
+    re-seeded context (its draw baseline reset) stays exact."""
+    objs = scenes.scene_s1000(n=300)
+    W, H = 72, 40
+    cam = camera_get_copy(scenes.camera_for(W, H))
+    rows = np.arange(H, dtype=np.int32)
+    gpu.set_scene(objs)
+    gpu.set_env(sky)
+    gpu.set_frame(W, H)
+    for seed in (1234, 77):
+        gpu.init_rng(seed)
+        for k in range(5):
+            gpu.render(cam, 1, 8, accumulate=k > 0, ordered=ordered, schedule="previous", sync=True)
+        rng = oracle_mod.init_rng(seed, W, rows, threads=8)
+        oa, _, _, _ = oracle_mod.render(objs, cam, sky, rows, 5, 8, rng, threads=8)
+        np.testing.assert_array_equal(gpu.read_rng(), rng)
+        np.testing.assert_array_equal(gpu.read_accum().view(np.uint32), oa.view(np.uint32))
