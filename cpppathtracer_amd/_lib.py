@@ -43,6 +43,8 @@ PROTOTYPES = {
     "cpt_read_accum": (_I, [_P, _P]),
     "cpt_clear_accum": (_I, [_P]),
     "cpt_read_aux": (_I, [_P, _P, _P]),
+    "cpt_write_accum": (_I, [_P, _P]),
+    "cpt_write_aux": (_I, [_P, _P, _P]),
     "cpt_copy_accum_device": (_I, [_P, _P, _SZ]),
     "cpt_gather_rows": (_I, [_P, _P]),
     "cpt_get_stats": (_I, [_P, _P]),

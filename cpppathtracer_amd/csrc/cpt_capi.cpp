@@ -655,6 +655,33 @@ int cpt_read_aux(cpt_ctx* c, float* normal3, float* depth) {
     return CPT_OK;
 }
 
+// Checkpoint / resume: the accumulator and the first-hit aux buffers restored
+// from host copies (with cpt_write_rng, a render resumes bit for bit where it stopped).
+int cpt_write_accum(cpt_ctx* c, const float* rgba) {
+    if (!c || !rgba) return CPT_ERR_INVALID_ARG;
+    if (!c->frame_set) return fail(c, CPT_ERR_STATE, "cpt_write_accum: no frame");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    const size_t n = (size_t)c->n_rows * c->width;
+    if (n) HIP_TRY(c, hipMemcpy(c->d_accum, rgba, n * sizeof(float4), hipMemcpyHostToDevice));
+    return CPT_OK;
+}
+
+int cpt_write_aux(cpt_ctx* c, const float* normal3, const float* depth) {
+    if (!c || !normal3 || !depth) return CPT_ERR_INVALID_ARG;
+    if (!c->frame_set) return fail(c, CPT_ERR_STATE, "cpt_write_aux: no frame");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream()));
+    const size_t n = (size_t)c->n_rows * c->width;
+    if (!c->d_normal && n) HIP_TRY(c, hipMalloc((void**)&c->d_normal, n * 3 * sizeof(float)));
+    if (!c->d_depth && n) HIP_TRY(c, hipMalloc((void**)&c->d_depth, n * sizeof(float)));
+    if (n) {
+        HIP_TRY(c, hipMemcpy(c->d_normal, normal3, n * 3 * sizeof(float), hipMemcpyHostToDevice));
+        HIP_TRY(c, hipMemcpy(c->d_depth, depth, n * sizeof(float), hipMemcpyHostToDevice));
+    }
+    return CPT_OK;
+}
+
 int cpt_copy_accum_device(cpt_ctx* c, void* dst, size_t bytes) {
     if (!c || (!dst && bytes)) return CPT_ERR_INVALID_ARG;
     size_t have = (size_t)c->n_rows * c->width * sizeof(float4);

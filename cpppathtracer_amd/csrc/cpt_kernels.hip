@@ -799,7 +799,17 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
                                                            int y1, int w_eff, int h_eff, float inv_idx) {
     __shared__ DnPix s_pix[DN_BY * DN_BX];
     __shared__ float s_wb[DN_THREADS * 12];   // backward weight k of tile pixel (ty, tx): w(p - d_k, p)
-    const int x0 = blockIdx.x * DN_TX, ty0 = y0 + blockIdx.y * DN_TY;
+    // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs (each with its own
+    // L2; MI355X_MICROARCH.md §Workgroup dispatch), so block b runs on the XCD of b mod 8.  Each
+    // XCD takes one contiguous run of tiles in column-major order, so consecutive tiles on an
+    // XCD are vertical neighbours whose 2-row halos overlap in that XCD's L2.
+    const int tiles_x = (w_eff + DN_TX - 1) / DN_TX, tiles_y = (y1 - y0 + DN_TY - 1) / DN_TY;
+    const int n_tiles = tiles_x * tiles_y;
+    const int xcd = (int)(blockIdx.x & 7u), k_on = (int)(blockIdx.x >> 3);
+    const int per = n_tiles >> 3, extra = n_tiles & 7;
+    const int t = xcd * per + min(xcd, extra) + k_on;   // bijective over [0, n_tiles)
+    const int tile_x = t / tiles_y, tile_y = t - tile_x * tiles_y;
+    const int x0 = tile_x * DN_TX, ty0 = y0 + tile_y * DN_TY;
     const int tw = min(DN_TX, w_eff - x0), th = min(DN_TY, y1 - ty0);   // the tile's extent
     const int limit = w_eff * h_eff;
     // ---- stage the box: linear pixels (ty0 - 2 + by) * W' + x0 - 2 + bx ----------------
@@ -938,8 +948,8 @@ hipError_t launch_denoise_mix(const float4* accum, const float* normal, const fl
     const int w_eff = 16 * (width / 16), h_eff = 16 * (height / 16);
     if (w_eff == 0 || h_eff == 0 || y1 <= y0) return hipSuccess;
     const float inv_idx = 1.f / float(cur_sample_idx);
-    dim3 grid((w_eff + DN_TX - 1) / DN_TX, (y1 - y0 + DN_TY - 1) / DN_TY);
-    hipLaunchKernelGGL(k_denoise_mix, grid, dim3(DN_THREADS), 0, stream, accum, normal, depth, mix, out, width, row0, y0,
+    const int n_tiles = ((w_eff + DN_TX - 1) / DN_TX) * ((y1 - y0 + DN_TY - 1) / DN_TY);
+    hipLaunchKernelGGL(k_denoise_mix, dim3((unsigned)n_tiles), dim3(DN_THREADS), 0, stream, accum, normal, depth, mix, out, width, row0, y0,
                        y1, w_eff, h_eff, inv_idx);
     return hipGetLastError();
 }

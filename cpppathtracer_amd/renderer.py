@@ -212,6 +212,17 @@ class Renderer:
         self._check(self._L.cpt_read_aux(self._ctx, _p(n), _p(d)))
         return n, d
 
+    def write_accum(self, rgba):
+        """Restore the accumulator ([npix, 4] float32) from a host copy (checkpoint / resume)."""
+        a = np.ascontiguousarray(rgba, dtype=np.float32).reshape(self.npix, 4)
+        self._check(self._L.cpt_write_accum(self._ctx, _p(a)))
+
+    def write_aux(self, normal3, depth):
+        """Restore the first-hit normal ([npix, 3]) and depth ([npix]) buffers from host copies."""
+        n = np.ascontiguousarray(normal3, dtype=np.float32).reshape(self.npix, 3)
+        d = np.ascontiguousarray(depth, dtype=np.float32).reshape(self.npix)
+        self._check(self._L.cpt_write_aux(self._ctx, _p(n), _p(d)))
+
     def copy_accum_device(self, device_ptr, nbytes):
         self._check(self._L.cpt_copy_accum_device(self._ctx, ctypes.c_void_p(device_ptr), nbytes))
 

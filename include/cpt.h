@@ -255,6 +255,12 @@ int cpt_synchronize(cpt_ctx* ctx);
 int cpt_read_accum(cpt_ctx* ctx, float* rgba);               /* [n_rows*width][4] */
 int cpt_clear_accum(cpt_ctx* ctx);
 int cpt_read_aux(cpt_ctx* ctx, float* normal3, float* depth); /* either may be NULL */
+/* Checkpoint / resume (the reference keeps its running state only in device memory,
+ * path_tracer.cu:91-99): restore the accumulator ([rows*W][4]: rgb sums + pass count) and the
+ * first-hit normal / depth buffers from host copies made with cpt_read_accum / cpt_read_aux.
+ * With cpt_write_rng, a render (and the display path) resumes bit for bit. */
+int cpt_write_accum(cpt_ctx* ctx, const float* rgba);
+int cpt_write_aux(cpt_ctx* ctx, const float* normal3, const float* depth);
 /* Device-to-device copy of the accumulator (e.g. into an RCCL send buffer). */
 int cpt_copy_accum_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
 /* Row-tile gather (multi-GPU row tiling; the single-GPU reference writes the

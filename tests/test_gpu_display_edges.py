@@ -1,0 +1,75 @@
+"""k_denoise_mix (Denoising + Mix, path_tracer.cu:177-254) on synthetic buffers written through
+the checkpoint entry points (cpt_write_accum / cpt_write_aux), against the oracle's restatement
+on the same arrays, byte for byte.  The inputs reach every branch of the kernel's weight code:
+equal neighbours (exact zero differences: the skipped factors), colour differences up to 1e3
+(weights that round to 0, the >= 330 shortcut), depth differences (the depth factor the
+rendered frames never exercise: a18 makes depth the constant 1e30), infinite depths (inf - inf
+in the pair and the centre weight), accumulators with pass count 0, and frame sizes whose 16-aligned
+launch is narrower than the frame and than one 64-pixel tile.  Also: a render resumed from a
+checkpoint equals the uninterrupted render."""
+import numpy as np
+import pytest
+
+from cpppathtracer_amd import camera_get_copy, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def _buffers(W, H, seed):
+    rng = np.random.default_rng(seed)
+    n = W * H
+    acc = np.empty((n, 4), np.float32)
+    acc[:, 3] = rng.integers(0, 4, n).astype(np.float32)          # pass counts, some 0
+    base = rng.random((n, 3)).astype(np.float32)
+    scale = np.where(rng.random(n) < 0.05, 1e3, 1.0).astype(np.float32)[:, None]
+    acc[:, :3] = base * scale * np.maximum(acc[:, 3:4], 1)
+    flat = rng.random(n) < 0.3                                     # runs of equal colours
+    acc[flat, :3] = np.float32(0.5) * np.maximum(acc[flat, 3:4], 1)
+    nrm = rng.standard_normal((n, 3)).astype(np.float32)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True).astype(np.float32)
+    floor = rng.random(n) < 0.5                                    # equal normals: n_w's zero skip
+    nrm[floor] = np.array([0, 1, 0], np.float32)
+    dep = np.full(n, 1e30, np.float32)                             # the rendered constant
+    varied = rng.random(n) < 0.2
+    dep[varied] = (rng.random(varied.sum()) * 40).astype(np.float32)
+    dep[rng.random(n) < 0.01] = np.inf
+    return acc, nrm, dep
+
+
+@pytest.mark.parametrize("W,H", [(200, 70), (1920 // 4, 36), (50, 40), (128, 16)])
+def test_denoise_edges_match_oracle(gpu, oracle_mod, W, H):
+    gpu.set_frame(W, H)
+    for frame, seed in enumerate((1, 2, 3)):
+        acc, nrm, dep = _buffers(W, H, seed)
+        gpu.write_accum(acc)
+        gpu.write_aux(nrm, dep)
+        out = gpu.denoise_mix(frame + 1)
+        if frame == 0:
+            mix = np.zeros((W * H, 3), np.float32)
+            ref = np.zeros((H, W, 4), np.uint8)
+        oracle_mod.denoise_mix(acc, nrm, dep, mix, ref, W, H, frame + 1)
+        np.testing.assert_array_equal(out, ref)
+
+
+def test_resume_from_checkpoint(gpu, oracle_mod, sky):
+    """Render 3 passes, save (accumulator, RNG, aux), render 2 more; a fresh context restored from
+    the save and rendering the same 2 passes ends with the same accumulator and RNG states."""
+    objs = scenes.scene_s1000(n=150)
+    W, H = 48, 32
+    cam = camera_get_copy(scenes.camera_for(W, H))
+    gpu.set_scene(objs)
+    gpu.set_env(sky)
+    gpu.set_frame(W, H)
+    gpu.init_rng(9)
+    gpu.render(cam, 3, 8, aux=True, ordered=True, sync=True)
+    acc, rng = gpu.read_accum(), gpu.read_rng()
+    nrm, dep = gpu.read_aux()
+    gpu.render(cam, 2, 8, aux=True, accumulate=True, ordered=True, sync=True)
+    want_acc, want_rng = gpu.read_accum(), gpu.read_rng()
+    gpu.set_frame(W, H)          # a new frame: everything on the device is gone
+    gpu.write_rng(rng)
+    gpu.write_accum(acc)
+    gpu.write_aux(nrm, dep)
+    gpu.render(cam, 2, 8, aux=True, accumulate=True, ordered=True, sync=True)
+    np.testing.assert_array_equal(gpu.read_rng(), want_rng)
+    np.testing.assert_array_equal(gpu.read_accum().view(np.uint32), want_acc.view(np.uint32))
