@@ -171,6 +171,11 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     const bool stat = STATIC_FIRST && LDST && !PROBE && p.lanes == 64 && p.tile_order != nullptr;
     const uint32_t n_static = gridDim.x * (uint32_t)BLK;
     bool first_take = true;
+    // CPT_TAKE_BATCH: the wave's reserved ids [res_id, res_end), the counter position it last
+    // saw, and whether the counter has run past the image (all wave-uniform)
+    uint32_t res_id = 0, res_end = 0, res_seen = 0;
+    bool counter_done = false;
+    (void)res_id; (void)res_end; (void)res_seen; (void)counter_done;
     stamps::init();
     for (;;) {
         stamps::lap(5);
@@ -242,6 +247,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             if (need) {
                 const int leader = __ffsll((unsigned long long)need) - 1;
                 uint32_t base = 0;
+                uint32_t lane_id = 0;   // the id this lane takes (if it needs one)
                 const bool first_take_was = first_take;
                 first_take = false;
                 if (stat && first_take_was) {
@@ -250,7 +256,46 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                     // one heavy wave that runs alone once its lighter neighbours finish
                     base = (level * (gridDim.x * 4u) + blockIdx.x * 4u + ((threadIdx.x >> 6) & 3u)) * 64u;
                     if (n_static >= n_work) exhausted = true;
-                } else {
+                    lane_id = base + lane_rank(need);
+                }
+#if CPT_TAKE_BATCH
+                else if (p.replicate == 1) {
+                    // Batched take: the wave draws a tile's worth of ids (CPT_TAKE_BATCH = 64) from
+                    // the counter and serves its idle lanes from that range over the next rounds,
+                    // so the device atomic on the one counter every wave of the grid contends for
+                    // is issued once per 64 takes instead of once per round (at 1 spp a wave
+                    // takes ~11 pixels every round: 2.43 -> 1.43 ms per 1-spp C4 render,
+                    // DESIGN.md §The reference's per-pass loop).  Near the end of the image (less
+                    // than one id per lane of the grid left) it draws only what it needs, so no
+                    // wave sits on unstarted pixels while others run dry.  Pixels are independent
+                    // chains, so the order they are taken in does not change the image.
+                    const uint32_t n_need = wave_count(need);
+                    const uint32_t avail = res_end - res_id;
+                    const uint32_t off = stat ? n_static : 0u;
+                    uint32_t nb = 0, ncnt = 0;
+                    if (n_need > avail && !counter_done) {
+                        const uint32_t want = n_need - avail;
+                        const uint32_t grab = n_work - res_seen > (uint32_t)CPT_TAKE_BATCH / 64u * n_static ? (uint32_t)CPT_TAKE_BATCH : want;
+                        if (lane == leader) nb = atomicAdd(p.work, grab);
+                        nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader)) + off;
+                        ncnt = grab;
+                    }
+                    if (ncnt) {
+                        res_seen = nb + ncnt;
+                        if (nb + ncnt >= n_work) counter_done = true;
+                    }
+                    const uint32_t rank = lane_rank(need);
+                    lane_id = rank < avail ? res_id + rank : (rank - avail < ncnt ? nb + (rank - avail) : n_work);
+                    if (ncnt) {
+                        res_id = nb + min(n_need - avail, ncnt);
+                        res_end = nb + ncnt;
+                    } else {
+                        res_id += n_need < avail ? n_need : avail;
+                    }
+                    if (counter_done && res_id >= res_end) exhausted = true;
+                }
+#endif
+                else {
                     // DIAGNOSTIC p.replicate > 1: every taken pixel runs on that many lanes, as
                     // identical copies (tools/lane_latency.py); 1 in normal use
                     const uint32_t rep = (uint32_t)p.replicate;
@@ -258,11 +303,11 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                     if (lane == leader) base = atomicAdd(p.work, n_take);
                     base = __shfl(base, leader) + (stat ? n_static : 0u);
                     if (base + n_take >= n_work) exhausted = true;
+                    lane_id = base + lane_rank(need) / rep;
                 }
                 bool took = false;
                 if ((need >> lane) & 1ull) {
-                    const uint32_t rank = stat && first_take_was ? lane_rank(need) : lane_rank(need) / (uint32_t)p.replicate;
-                    const uint32_t id = base + rank;
+                    const uint32_t id = lane_id;
                     int x, ri;
                     if (id < n_work && decode_pixel(p, id, x, ri, L.tile)) {
                         execdiag::lanes(p.stats + 64, 0);
@@ -310,7 +355,12 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         }
         stamps::lap(0);
         if (!__any(busy)) {
-            if (!cons || retiring) break;
+            // (a wave whose takes all fell outside the frame takes again while ids remain: with
+            // CPT_TAKE_BATCH it may still hold reserved ids, which no other wave would render)
+            if (!cons || retiring) {
+                if (CPT_TAKE_BATCH && !exhausted) continue;
+                break;
+            }
             if (exhausted) {
                 // a keeper with nothing to do: wait for hand-overs while any chain is live (a
                 // chain in flight is never more than a pass away from its hand-over or its end)

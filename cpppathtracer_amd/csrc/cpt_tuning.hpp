@@ -42,6 +42,14 @@ namespace cpt {
 #define CPT_STATIC_FIRST 1
 #endif
 
+// The refill draws a tile's worth of pixel ids (64) per counter atomic and serves the wave's
+// idle lanes from them over the following rounds (cpt_kernels.hip k_megakernel; 0 = one atomic
+// per refill).  1-spp C4 render 1.43 vs 2.43 ms; 128 ids 1.50 ms; requesting the next range
+// ahead of need 1.49-1.56 ms and up to 10% slower at 1024 spp (profiles/r04/ab_take_batch_*.log).
+#ifndef CPT_TAKE_BATCH
+#define CPT_TAKE_BATCH 64
+#endif
+
 constexpr int SUSPEND_AT = CPT_SUSPEND_AT;
 constexpr int SUSPEND_MIN_DONE = CPT_SUSPEND_MIN_DONE;
 constexpr int SPEC_LEAF_ROUND = CPT_SPEC_LEAF_ROUND;
