@@ -275,7 +275,11 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                     uint32_t nb = 0, ncnt = 0;
                     if (n_need > avail && !counter_done) {
                         const uint32_t want = n_need - avail;
-                        const uint32_t grab = n_work - res_seen > (uint32_t)CPT_TAKE_BATCH / 64u * n_static ? (uint32_t)CPT_TAKE_BATCH : want;
+                        // long chains (spp >= 64): smaller ranges, since a wave's unstarted ids then hold
+                        // back long chains other waves' idle lanes could run
+                        const uint32_t bsz = p.spp >= 64 ? (uint32_t)CPT_TAKE_BATCH_LONG : (uint32_t)CPT_TAKE_BATCH;
+                        // the consolidating kernel (frames of <= 4 pixels per lane) takes exactly what it needs
+                        const uint32_t grab = (!CONS || CPT_TAKE_BATCH_CONS) && n_work - res_seen > n_static && bsz > want ? bsz : want;
                         if (lane == leader) nb = atomicAdd(p.work, grab);
                         nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader)) + off;
                         ncnt = grab;

@@ -49,6 +49,17 @@ namespace cpt {
 #ifndef CPT_TAKE_BATCH
 #define CPT_TAKE_BATCH 64
 #endif
+// Long chains (spp >= 64) take ranges of CPT_TAKE_BATCH_LONG ids.  The consolidating kernel
+// (frames of <= 4 pixels per lane, the strong-scaling ranks) takes exactly what it needs unless
+// CPT_TAKE_BATCH_CONS: there a wave's unstarted ids are a large share of the frame's work and
+// hold back long chains other waves' idle lanes could run (C4 rehearsal N = 2 / 4: 677 / 469 ms
+// batched vs 622 / 416 exact; C5 N = 8 2787 vs 2528; profiles/r04/ab_take_hold_rehearsal.log).
+#ifndef CPT_TAKE_BATCH_LONG
+#define CPT_TAKE_BATCH_LONG 64
+#endif
+#ifndef CPT_TAKE_BATCH_CONS
+#define CPT_TAKE_BATCH_CONS 0
+#endif
 
 constexpr int SUSPEND_AT = CPT_SUSPEND_AT;
 constexpr int SUSPEND_MIN_DONE = CPT_SUSPEND_MIN_DONE;
