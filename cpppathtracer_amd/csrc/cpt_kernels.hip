@@ -156,14 +156,6 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         for (int i = threadIdx.x; i < QS; i += BLK) s_qflag[i] = 0;
         __syncthreads();
     }
-    // CPT_TAKE_WG: the workgroup's shared id range [s_tk[0], s_tk[1]), its lock (s_tk[2]) and
-    // whether the counter has run past the image (s_tk[3])
-    constexpr bool TKWG = CPT_TAKE_WG == 2 || (CPT_TAKE_WG == 1 && CONS);
-    __shared__ uint32_t s_tk[TKWG ? 4 : 1];
-    if (TKWG) {
-        if (threadIdx.x < 4) s_tk[threadIdx.x] = 0u;
-        __syncthreads();
-    }
     // a chain's next pass (RayGen, path_tracer.cu:134)
     auto start_pass = [&]() {
         ray = ray_gen(kernarg_field<CamK>(offsetof(KParams, cam)), (int)(L.xy & 0xffffu), (int)(L.xy >> 16), L.s);
@@ -266,62 +258,6 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                     if (n_static >= n_work) exhausted = true;
                     lane_id = base + lane_rank(need);
                 }
-#if CPT_TAKE_WG
-                else if (TKWG && p.replicate == 1) {
-                    // Workgroup-shared take: the 16 waves of the workgroup draw from one range of
-                    // 64 ids (one counter atomic per 64 takes of the workgroup), under an LDS lock
-                    // held by one lane for a few LDS operations (and the atomic when the range runs
-                    // out).  At most 63 ids of a workgroup wait unstarted.
-                    const uint32_t n_need = wave_count(need);
-                    const uint32_t off = stat ? n_static : 0u;
-                    uint32_t r0 = 0, r1 = 0, nb = 0, ncnt = 0, dn = 0;
-                    if (lane == leader) {
-                        uint32_t spins = 0;
-                        uint32_t expect = 0u;
-                        while (!__hip_atomic_compare_exchange_strong(&s_tk[2], &expect, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
-                                                                      __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                            expect = 0u;
-                            __builtin_amdgcn_s_sleep(1);
-                            if (++spins > publish_wait) break;   // never hang: take from the counter alone
-                        }
-                        const bool locked = spins <= publish_wait;
-                        if (!locked) atomicOr(p.error, CPT_DEVERR_PUBLISH_TIMEOUT);
-                        r0 = locked ? s_tk[0] : 0u;
-                        r1 = locked ? s_tk[1] : 0u;
-                        dn = locked ? s_tk[3] : 0u;
-                        const uint32_t avail = r1 - r0;
-                        if (n_need > avail && !dn) {
-                            const uint32_t want = n_need - avail;
-                            const uint32_t grab = locked && 64u > want ? 64u : want;
-                            nb = atomicAdd(p.work, grab) + off;
-                            ncnt = grab;
-                            if (nb + grab >= n_work) dn = 1u;
-                        }
-                        uint32_t left = 0;   // ids left in the workgroup's range after this take
-                        if (locked) {
-                            const uint32_t n0 = ncnt ? nb + min(n_need - avail, ncnt) : r0 + min(n_need, avail);
-                            const uint32_t n1 = ncnt ? nb + ncnt : r1;
-                            s_tk[0] = n0;
-                            s_tk[1] = n1;
-                            s_tk[3] = dn;
-                            __hip_atomic_store(&s_tk[2], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            left = n1 - n0;
-                        }
-                        // this wave stops taking once the counter is past the image and the
-                        // workgroup's range is empty (no wave can refill it any more)
-                        dn = dn && left == 0 ? 1u : 0u;
-                    }
-                    r0 = __builtin_amdgcn_readfirstlane(__shfl(r0, leader));
-                    r1 = __builtin_amdgcn_readfirstlane(__shfl(r1, leader));
-                    nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader));
-                    ncnt = __builtin_amdgcn_readfirstlane(__shfl(ncnt, leader));
-                    dn = __builtin_amdgcn_readfirstlane(__shfl(dn, leader));
-                    const uint32_t avail = r1 - r0;
-                    const uint32_t rank = lane_rank(need);
-                    lane_id = rank < avail ? r0 + rank : (rank - avail < ncnt ? nb + (rank - avail) : n_work);
-                    if (dn) exhausted = true;
-                }
-#endif
 #if CPT_TAKE_BATCH
                 else if (p.replicate == 1) {
                     // Batched take: the wave draws a tile's worth of ids (CPT_TAKE_BATCH = 64) from

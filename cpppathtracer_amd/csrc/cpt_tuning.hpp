@@ -57,11 +57,6 @@ namespace cpt {
 #ifndef CPT_TAKE_BATCH_LONG
 #define CPT_TAKE_BATCH_LONG 64
 #endif
-// Workgroup-shared take range instead of the per-wave one: 0 off, 1 in the consolidating kernel,
-// 2 in every LDS-walk kernel.
-#ifndef CPT_TAKE_WG
-#define CPT_TAKE_WG 0
-#endif
 #ifndef CPT_TAKE_BATCH_CONS
 #define CPT_TAKE_BATCH_CONS 0
 #endif
