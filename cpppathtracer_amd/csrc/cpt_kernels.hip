@@ -1128,6 +1128,14 @@ __global__ void k_iota(uint32_t* v, uint32_t n) {
     if (i < n) v[i] = i;
 }
 
+// CPT_ORDER_BANDS > 0: the sort key keeps only the cost's binary exponent and that many leading
+// mantissa bits (relative bands of 2^-bands), so tiles of one band keep their row-major order
+// (the radix sort is stable): a wave's consecutive takes then come from neighbouring tiles.
+__global__ void k_band_costs(uint32_t* cost, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && CPT_ORDER_BANDS > 0) cost[i] = __float_as_uint((float)cost[i]) >> (23 - CPT_ORDER_BANDS);
+}
+
 size_t tile_schedule_scratch_bytes(int width, int n_rows) {
     const int n = ((width + 7) / 8) * ((n_rows + 7) / 8);
     size_t temp = 0;
@@ -1180,6 +1188,11 @@ hipError_t launch_tile_order_from_draws(const KParams& p, uint32_t* d_prev, void
     hipLaunchKernelGGL(k_iota, dim3((n + 255) / 256), dim3(256), 0, stream, ids, (uint32_t)n);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (CPT_ORDER_BANDS > 0) {
+        hipLaunchKernelGGL(k_band_costs, dim3((n + 255) / 256), dim3(256), 0, stream, cost, (uint32_t)n);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     return hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, cost, cost_sorted, ids, order, n, 0, 32,
                                                         stream);
 }
@@ -1206,6 +1219,11 @@ hipError_t launch_tile_schedule(const KParams& p0, int passes, void* scratch, si
     hipLaunchKernelGGL(k_iota, dim3((n + 255) / 256), dim3(256), 0, stream, ids, (uint32_t)n);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (CPT_ORDER_BANDS > 0) {
+        hipLaunchKernelGGL(k_band_costs, dim3((n + 255) / 256), dim3(256), 0, stream, cost, (uint32_t)n);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     return hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, cost, cost_sorted, ids, order, n, 0, 32,
                                                         stream);
 }
