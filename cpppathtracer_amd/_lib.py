@@ -58,6 +58,8 @@ PROTOTYPES = {
     "cpt_get_execdiag_counters": (_I, [_P, _P]),
     "cpt_last_kernel_stats": (_I, [_P, _P, _P]),
     "cpt_denoise_mix": (_I, [_P, _U32, _P]),
+    "cpt_host_register": (_I, [_P, _SZ]),
+    "cpt_host_unregister": (_I, [_P]),
     "cpt_denoise_mix_band": (_I, [_P, _U32, _I, _I, _P]),
     "cpt_copy_bgra_device": (_I, [_P, _P, _SZ]),
     "cpt_last_display_ms": (_I, [_P, _P]),

@@ -298,6 +298,7 @@ PathTracer::PathTracer() {}
 
 PathTracer::~PathTracer() {
     Stop();
+    if (output_pinned_) (void)cpt_host_unregister(output_buffer_.data());
     for (Tile& t : tiles_)
         if (t.ctx) cpt_destroy(t.ctx);
     if (frame_) cpt_destroy(frame_);
@@ -499,7 +500,12 @@ bool PathTracer::EnsureFrame(const MotionalCamera& cam) {
         if (frame_ && cpt_set_frame(frame_, cam.width_, cam.height_, nullptr, 0) != CPT_OK) return Fail("cpt_set_frame", frame_);
         width_ = cam.width_;
         height_ = cam.height_;
+        if (output_pinned_) (void)cpt_host_unregister(output_buffer_.data());
         output_buffer_.assign((size_t)width_ * height_ * 4, 0);
+        // pinned, so each pass's frame reaches it without a staging copy (cpt_denoise_mix); a
+        // buffer that cannot be pinned still works through the copy
+        output_pinned_ = !output_buffer_.empty() &&
+                         cpt_host_register(output_buffer_.data(), output_buffer_.size()) == CPT_OK;
     }
     for (Tile& t : tiles_)
         if (!t.rng_ready) {

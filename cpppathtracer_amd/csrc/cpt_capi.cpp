@@ -799,12 +799,29 @@ static int denoise_band(cpt_ctx* c, uint32_t cur_sample_idx, int y0, int y1, uin
         c->band_y0 = y0;
         c->band_y1 = y1;
     }
+    // A pinned host frame (hipHostMalloc / hipHostRegister, e.g. torch's pin_memory) is written by
+    // the kernel itself through its device alias, so the PCIe transfer overlaps the stencil
+    // instead of following it; pageable memory takes the copy after the kernel.
+    uint8_t* host_alias = nullptr;
+    if (bgra_host && c->width % 16 == 0) {   // (columns past 16*(W/16) are never written by the kernel)
+        hipPointerAttribute_t attr;
+        if (hipPointerGetAttributes(&attr, bgra_host) == hipSuccess && attr.type == hipMemoryTypeHost &&
+            attr.devicePointer != nullptr)
+            host_alias = static_cast<uint8_t*>(attr.devicePointer);
+        else
+            (void)hipGetLastError();   // pageable: not an error
+    }
     HIP_TRY(c, hipEventRecord(c->ev_dn0, s));
-    HIP_TRY(c, cpt::launch_denoise_mix(c->d_accum, c->d_normal, c->d_depth, c->d_mix, c->d_bgra, c->width, c->height,
-                                      row0, y0, y1, cur_sample_idx, s));
+    HIP_TRY(c, cpt::launch_denoise_mix(c->d_accum, c->d_normal, c->d_depth, c->d_mix, c->d_bgra, host_alias, c->width,
+                                      c->height, row0, y0, y1, cur_sample_idx, s));
     HIP_TRY(c, hipEventRecord(c->ev_dn1, s));
     c->have_dn_timing = true;
-    if (bgra_host) {
+    if (bgra_host && host_alias) {
+        // the kernel writes the band's rows; the rest of the frame is zero, as the copy gives
+        const size_t band = (size_t)(y1 - y0) * c->width * 4;
+        std::memset(bgra_host + band, 0, cap_rows * c->width * 4 - band);
+        HIP_TRY(c, hipStreamSynchronize(s));
+    } else if (bgra_host) {
         HIP_TRY(c, hipMemcpyAsync(bgra_host, c->d_bgra, cap_rows * c->width * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(c, hipStreamSynchronize(s));
     }
@@ -832,6 +849,20 @@ int cpt_denoise_mix(cpt_ctx* c, uint32_t cur_sample_idx, uint8_t* bgra_host) {
     }
     // the whole frame's rows (those past H' are never written and stay 0)
     return denoise_band(c, cur_sample_idx, 0, h_eff, bgra_host, (size_t)c->height);
+}
+
+int cpt_host_register(void* ptr, size_t bytes) {
+    if (!ptr || bytes == 0) return fail(nullptr, CPT_ERR_INVALID_ARG, "cpt_host_register: empty buffer");
+    const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterMapped);
+    if (e != hipSuccess) return fail(nullptr, CPT_ERR_HIP, "cpt_host_register: %s", hipGetErrorString(e));
+    return CPT_OK;
+}
+
+int cpt_host_unregister(void* ptr) {
+    if (!ptr) return fail(nullptr, CPT_ERR_INVALID_ARG, "cpt_host_unregister: null buffer");
+    const hipError_t e = hipHostUnregister(ptr);
+    if (e != hipSuccess) return fail(nullptr, CPT_ERR_HIP, "cpt_host_unregister: %s", hipGetErrorString(e));
+    return CPT_OK;
 }
 
 int cpt_denoise_mix_band(cpt_ctx* c, uint32_t cur_sample_idx, int y0, int y1, uint8_t* bgra_host) {

@@ -849,8 +849,9 @@ __host__ __device__ constexpr int dn_fdy(int k) { return k < 2 ? 0 : (k < 7 ? 1 
 __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __restrict__ accum,
                                                            const float* __restrict__ normal,
                                                            const float* __restrict__ depth, float* __restrict__ mix,
-                                                           uint8_t* __restrict__ out, int width, int row0, int y0,
-                                                           int y1, int w_eff, int h_eff, float inv_idx) {
+                                                           uint8_t* __restrict__ out, uint8_t* __restrict__ out_host,
+                                                           int width, int row0, int y0, int y1, int w_eff, int h_eff,
+                                                           float inv_idx) {
     __shared__ DnPix s_pix[DN_BY * DN_BX];
     __shared__ float s_wb[DN_THREADS * 12];   // backward weight k of tile pixel (ty, tx): w(p - d_k, p)
     // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs (each with its own
@@ -994,17 +995,20 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
     const uint32_t bgr = (uint32_t)(uint8_t)(255.99f * m.z) | ((uint32_t)(uint8_t)(255.99f * m.y) << 8) |
                          ((uint32_t)(uint8_t)(255.99f * m.x) << 16);
     reinterpret_cast<uint32_t*>(out)[bself] = bgr;
+    // the caller's pinned host frame (the callback's buffer), written over PCIe by the kernel
+    // itself instead of a copy after it
+    if (out_host) reinterpret_cast<uint32_t*>(out_host)[bself] = bgr;
 }
 
 hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
-                              int width, int height, int row0, int y0, int y1, uint32_t cur_sample_idx,
+                              uint8_t* out_host, int width, int height, int row0, int y0, int y1, uint32_t cur_sample_idx,
                               hipStream_t stream) {
     const int w_eff = 16 * (width / 16), h_eff = 16 * (height / 16);
     if (w_eff == 0 || h_eff == 0 || y1 <= y0) return hipSuccess;
     const float inv_idx = 1.f / float(cur_sample_idx);
     const int n_tiles = ((w_eff + DN_TX - 1) / DN_TX) * ((y1 - y0 + DN_TY - 1) / DN_TY);
-    hipLaunchKernelGGL(k_denoise_mix, dim3((unsigned)n_tiles), dim3(DN_THREADS), 0, stream, accum, normal, depth, mix, out, width, row0, y0,
-                       y1, w_eff, h_eff, inv_idx);
+    hipLaunchKernelGGL(k_denoise_mix, dim3((unsigned)n_tiles), dim3(DN_THREADS), 0, stream, accum, normal, depth, mix, out, out_host, width,
+                       row0, y0, y1, w_eff, h_eff, inv_idx);
     return hipGetLastError();
 }
 
@@ -1128,14 +1132,6 @@ __global__ void k_iota(uint32_t* v, uint32_t n) {
     if (i < n) v[i] = i;
 }
 
-// CPT_ORDER_BANDS > 0: the sort key keeps only the cost's binary exponent and that many leading
-// mantissa bits (relative bands of 2^-bands), so tiles of one band keep their row-major order
-// (the radix sort is stable): a wave's consecutive takes then come from neighbouring tiles.
-__global__ void k_band_costs(uint32_t* cost, uint32_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && CPT_ORDER_BANDS > 0) cost[i] = __float_as_uint((float)cost[i]) >> (23 - CPT_ORDER_BANDS);
-}
-
 size_t tile_schedule_scratch_bytes(int width, int n_rows) {
     const int n = ((width + 7) / 8) * ((n_rows + 7) / 8);
     size_t temp = 0;
@@ -1188,11 +1184,6 @@ hipError_t launch_tile_order_from_draws(const KParams& p, uint32_t* d_prev, void
     hipLaunchKernelGGL(k_iota, dim3((n + 255) / 256), dim3(256), 0, stream, ids, (uint32_t)n);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (CPT_ORDER_BANDS > 0) {
-        hipLaunchKernelGGL(k_band_costs, dim3((n + 255) / 256), dim3(256), 0, stream, cost, (uint32_t)n);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
     return hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, cost, cost_sorted, ids, order, n, 0, 32,
                                                         stream);
 }
@@ -1219,11 +1210,6 @@ hipError_t launch_tile_schedule(const KParams& p0, int passes, void* scratch, si
     hipLaunchKernelGGL(k_iota, dim3((n + 255) / 256), dim3(256), 0, stream, ids, (uint32_t)n);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (CPT_ORDER_BANDS > 0) {
-        hipLaunchKernelGGL(k_band_costs, dim3((n + 255) / 256), dim3(256), 0, stream, cost, (uint32_t)n);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-    }
     return hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, cost, cost_sorted, ids, order, n, 0, 32,
                                                         stream);
 }

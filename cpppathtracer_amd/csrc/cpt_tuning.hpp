@@ -57,11 +57,6 @@ namespace cpt {
 #ifndef CPT_TAKE_BATCH_LONG
 #define CPT_TAKE_BATCH_LONG 64
 #endif
-// Tile order: sort keys banded to this many leading mantissa bits of the cost (0: exact cost
-// order; see cpt_kernels.hip k_band_costs).
-#ifndef CPT_ORDER_BANDS
-#define CPT_ORDER_BANDS 0
-#endif
 #ifndef CPT_TAKE_BATCH_CONS
 #define CPT_TAKE_BATCH_CONS 0
 #endif

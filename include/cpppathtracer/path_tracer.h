@@ -115,6 +115,7 @@ private:
     PocaTexture env_ = 0;
     std::shared_ptr<MotionalCamera> camera_;
     std::vector<uint8_t> output_buffer_;   // BGRA8 handed to the callback
+    bool output_pinned_ = false;           // output_buffer_ registered with cpt_host_register
     std::string err_;
 
     std::mutex mu_;                        // guards the queue and the context

@@ -303,8 +303,16 @@ int cpt_last_kernel_stats(cpt_ctx* ctx, float* avg_ms, int* launches);
 
 /* Display path (path_tracer.cu:177-254): 5x5 edge-aware denoise of the current 1-spp
  * radiance (accumulator / pass count), running-mean Mix with weight 1/cur_sample_idx,
- * BGRA8 out (alpha byte untouched).  Needs a full frame (rows == NULL). */
+ * BGRA8 out (alpha byte untouched).  Needs a full frame (rows == NULL).  A pinned bgra_host
+ * (cpt_host_register, hipHostMalloc, torch pin_memory) of a 16-aligned width is written by the
+ * display kernel itself over PCIe; other memory gets a copy after it (the reference's
+ * cudaMemcpy, path_tracer.cu:303). */
 int cpt_denoise_mix(cpt_ctx* ctx, uint32_t cur_sample_idx, uint8_t* bgra_host);
+/* Pin / unpin a host buffer (hipHostRegister, mapped) so display frames reach it without a
+ * staging copy -- e.g. the BGRA8 buffer the reference hands to its per-pass callback
+ * (path_tracer.cu:303-304).  Unregister before freeing it. */
+int cpt_host_register(void* ptr, size_t bytes);
+int cpt_host_unregister(void* ptr);
 /* Display path for output rows [y0, y1) of the 16-aligned launch (0 <= y0 < y1 <= 16*(H/16)),
  * for row-banded multi-GPU display: the context's frame rows (cpt_set_frame) must be one
  * ascending run covering [max(0, y0-3), min(16*(H/16), y1+3)) -- the band and the rows its

@@ -73,3 +73,27 @@ def test_resume_from_checkpoint(gpu, oracle_mod, sky):
     gpu.render(cam, 2, 8, aux=True, accumulate=True, ordered=True, sync=True)
     np.testing.assert_array_equal(gpu.read_rng(), want_rng)
     np.testing.assert_array_equal(gpu.read_accum().view(np.uint32), want_acc.view(np.uint32))
+
+
+@pytest.mark.parametrize("W,H", [(256, 40), (200, 70)])
+def test_pinned_host_frame(gpu, oracle_mod, W, H):
+    """A pinned host frame is written by the display kernel itself (cpt_denoise_mix's zero-copy
+    path, 16-aligned widths); a pageable one gets the copy.  Both equal the oracle byte for byte,
+    including the rows below the 16-aligned launch (zero) and a frame that held garbage before."""
+    import torch
+    gpu.set_frame(W, H)
+    pinned = torch.full((H, W, 4), 0xAB, dtype=torch.uint8).pin_memory().numpy()
+    pageable = np.full((H, W, 4), 0xCD, np.uint8)
+    mix = np.zeros((W * H, 3), np.float32)
+    ref = np.zeros((H, W, 4), np.uint8)
+    for frame, seed in enumerate((4, 5)):
+        acc, nrm, dep = _buffers(W, H, seed)
+        gpu.write_accum(acc)
+        gpu.write_aux(nrm, dep)
+        oracle_mod.denoise_mix(acc, nrm, dep, mix, ref, W, H, frame + 1)
+        if frame == 0:
+            gpu.denoise_mix(frame + 1, out=pinned)
+            np.testing.assert_array_equal(pinned, ref)
+        else:
+            gpu.denoise_mix(frame + 1, out=pageable)
+            np.testing.assert_array_equal(pageable, ref)
