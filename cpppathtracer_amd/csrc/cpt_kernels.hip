@@ -28,7 +28,7 @@ namespace cpt {
 // accumulator stay in VGPRs; HBM is touched once when the lane takes the pixel (24 B rng +
 // 16 B accumulator) and once when it has run all `spp` passes.  A lane whose path ends
 // starts the pixel's next pass at once; a lane whose pixel is finished takes the next pixel
-// from a device-wide counter (one aggregated atomic per wave and refill), so every lane of
+// from a device-wide counter (a wave draws 64 ids per atomic, see the refill), so every lane of
 // every wave does useful work until the image runs out — no per-pass kernel boundaries and
 // no idle lanes behind a wave's slowest path.  Pixels are handed out in 8x8 tiles so a fresh
 // wave starts coherent; with the cost schedule the tiles come heaviest first (p.tile_order).
