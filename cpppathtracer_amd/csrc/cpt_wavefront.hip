@@ -174,6 +174,7 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
     // miss / hit / past-the-queue), so a wave runs the sky path or the material path, rarely both.
     __shared__ uint32_t s_cnt[3][4];
     __shared__ uint32_t s_slot[256];
+    __shared__ uint32_t s_app[5];   // the block's survivors per wave, then the block's first slot
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (uint32_t t = 0, i0 = blockIdx.x * blockDim.x + threadIdx.x; t < trips; ++t, i0 += stride) {
         const int key = i0 < n ? (__float_as_int(w.hit_p[i0].w) >= 0 ? 1 : 0) : 2;
@@ -256,7 +257,21 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
                 nx4 = aux4;
             }
         }
-        const uint32_t slot = wave_append(alive, nout);
+        // the survivors' queue slots: one counter atomic per block and trip (the block's four
+        // waves' counts summed in LDS) rather than one per wave -- every wave of the grid appends
+        // to this one counter, and one atomic per wave contended for it; the order of the queue
+        // does not change any pixel's result
+        const uint64_t am = __ballot(alive);
+        if (lane == 0) s_app[wv] = (uint32_t)__popcll(am);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t tot = s_app[0] + s_app[1] + s_app[2] + s_app[3];
+            s_app[4] = tot ? atomicAdd(nout, tot) : 0u;
+        }
+        __syncthreads();
+        uint32_t slot = s_app[4];
+        for (int v = 0; v < wv; ++v) slot += s_app[v];
+        slot += __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
         if (alive) {
             const int ob = sb ^ 1;
             qout[slot] = pix;
@@ -277,8 +292,8 @@ __global__ void __launch_bounds__(256) k_wf_shade(const KParams p, WfState w, co
     }
 }
 
-// Tile-ordered identity queue: entry k = the k-th pixel when the frame is walked in 8x8
-// tiles, so each wave's first-bounce rays are coherent.
+// Tile-ordered identity queue: the frame's pixels walked in 8x8 tiles (a wave's 64 consecutive
+// ids are one tile), so each wave's first-bounce rays are coherent.
 __global__ void k_wf_ident(int width, int n_rows, int32_t* q, uint32_t* count) {
     const int tiles_x = (width + 7) / 8;
     const uint32_t n_work = (uint32_t)tiles_x * ((n_rows + 7) / 8) * 64u;
@@ -286,11 +301,11 @@ __global__ void k_wf_ident(int width, int n_rows, int32_t* q, uint32_t* count) {
         const uint32_t tile = id >> 6, k = id & 63;
         const int x = (int)(tile % tiles_x) * 8 + (int)(k & 7);
         const int ri = (int)(tile / tiles_x) * 8 + (int)(k >> 3);
-        if (x < width && ri < n_rows) {
-            // rank of this pixel among valid pixels in tile order = its slot
-            const uint32_t slot = atomicAdd(count, 1u);
-            q[slot] = ri * width + x;
-        }
+        // the valid pixels of a wave's 64 consecutive ids (one tile) get consecutive slots, one
+        // counter atomic per wave (the queue's order only steers coherence, not any result)
+        const bool valid = x < width && ri < n_rows;
+        const uint32_t slot = wave_append(valid, count);
+        if (valid) q[slot] = ri * width + x;
     }
 }
 
