@@ -47,6 +47,8 @@ PROTOTYPES = {
     "cpt_write_aux": (_I, [_P, _P, _P]),
     "cpt_copy_accum_device": (_I, [_P, _P, _SZ]),
     "cpt_gather_rows": (_I, [_P, _P]),
+    "cpt_last_gather_mode": (_I, [_P, _P, _P]),
+    "cpt_set_debug_gather": (_I, [_P, _I]),
     "cpt_get_stats": (_I, [_P, _P]),
     "cpt_reset_stats": (_I, [_P]),
     "cpt_get_raw_counters": (_I, [_P, _P]),
@@ -64,6 +66,7 @@ PROTOTYPES = {
     "cpt_copy_bgra_device": (_I, [_P, _P, _SZ]),
     "cpt_last_display_ms": (_I, [_P, _P]),
     "cpt_reset_display": (_I, [_P]),
+    "cpt_read_mix": (_I, [_P, _P]),
     "cpt_math_batch": (_I, [_P, _I, _P, _P, _P, _SZ]),
     "cpt_selftest_qdiv": (_I, [_P, _I, _U64, _U64, _P, _I]),
     "cpt_set_debug_consolidation": (_I, [_P, _U32, _I, _I]),

@@ -29,6 +29,7 @@ HEADERS = [
     os.path.join(CSRC, "cpt_path.hpp"),
     os.path.join(CSRC, "cpt_stamps.hpp"),
     os.path.join(CSRC, "cpt_tuning.hpp"),
+    os.path.join(CSRC, "cpt_dn_exp.hpp"),
     os.path.join(REPO_DIR, "include", "cpt.h"),
 ]
 

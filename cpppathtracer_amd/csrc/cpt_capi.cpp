@@ -491,9 +491,8 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
 }
 
 // Row-tile gather: the rows `src` rendered, placed into `dst`'s frame at the
-// same global rows.  One peer copy of src's buffers to dst's device (hipMemcpyPeerAsync: xGMI
-// between two MI355X, a plain device copy when both contexts share a GPU), then one stitch
-// kernel on dst's stream.  Waits for src; asynchronous with respect to dst.
+// same global rows by one stitch kernel on dst's stream, ordered by events (no host wait; see
+// cpt_gather_rows below for the three ways the stitch reaches src's buffers).
 namespace {
 // Peer access from `dev` to `peer`'s memory, enabled once per ordered pair for the process.
 // Returns false when the pair has no peer path (the gather then stages through a peer copy).
@@ -562,6 +561,8 @@ int cpt_gather_rows(cpt_ctx* dst, cpt_ctx* src) {
         gm->src_device = src->device;
         gm->peer = src->device == dst->device || ensure_peer_access(dst->device, src->device);
     }
+    const bool staged = !gm->peer || dst->force_staged_gather;
+    gm->mode = staged ? CPT_GATHER_STAGED : src->device == dst->device ? CPT_GATHER_SAME_DEVICE : CPT_GATHER_PEER;
     if (src->n_rows == 0) return CPT_OK;
     const size_t npix = (size_t)src->n_rows * src->width;
     const bool aux = src->d_normal && src->d_depth;
@@ -586,7 +587,7 @@ int cpt_gather_rows(cpt_ctx* dst, cpt_ctx* src) {
     const float4* s_acc = src->d_accum;
     const float* s_nrm = aux ? src->d_normal : nullptr;
     const float* s_dep = aux ? src->d_depth : nullptr;
-    if (!gm->peer) {
+    if (staged) {
         // staging: accumulator (npix float4), then normals (3 npix floats) and depths (npix floats)
         int rc;
         if ((rc = ensure(dst, &dst->d_gather, &dst->cap_gather, aux ? 2 * npix : npix)) != CPT_OK) return rc;
@@ -608,6 +609,20 @@ int cpt_gather_rows(cpt_ctx* dst, cpt_ctx* src) {
     HIP_TRY(src, hipSetDevice(src->device));
     HIP_TRY(src, hipStreamWaitEvent(src->stream(), dst->ev_gathered, 0));
     HIP_TRY(dst, hipSetDevice(dst->device));
+    return CPT_OK;
+}
+
+int cpt_last_gather_mode(cpt_ctx* dst, cpt_ctx* src, int* mode) {
+    if (!dst || !src || !mode) return dst ? fail(dst, CPT_ERR_INVALID_ARG, "cpt_last_gather_mode: null argument") : CPT_ERR_INVALID_ARG;
+    *mode = -1;
+    for (const auto& g : dst->gather_maps)
+        if (g.src == src) *mode = g.mode;
+    return CPT_OK;
+}
+
+int cpt_set_debug_gather(cpt_ctx* c, int force_staged) {
+    if (!c) return CPT_ERR_INVALID_ARG;
+    c->force_staged_gather = force_staged != 0;
     return CPT_OK;
 }
 
@@ -880,6 +895,15 @@ int cpt_copy_bgra_device(cpt_ctx* c, void* device_dst, size_t bytes) {
     return CPT_OK;
 }
 
+int cpt_read_mix(cpt_ctx* c, float* rgb) {
+    if (!c || !rgb) return CPT_ERR_INVALID_ARG;
+    if (!c->d_mix) return fail(c, CPT_ERR_STATE, "cpt_read_mix: no display frame yet");
+    const size_t rows = (size_t)(c->band_y1 - c->band_y0);
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipMemcpyAsync(rgb, c->d_mix, rows * c->width * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream()));
+    return sync_checked(c);
+}
+
 int cpt_reset_display(cpt_ctx* c) {
     if (!c) return CPT_ERR_INVALID_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
@@ -950,7 +974,7 @@ int cpt_measure_read_bandwidth(cpt_ctx* c, size_t bytes, int iters, float* gbps)
 }
 
 int cpt_selftest_qdiv(cpt_ctx* c, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len) {
-    if (!c || !out || out_len < 1 || which < 0 || which > 5) return CPT_ERR_INVALID_ARG;
+    if (!c || !out || out_len < 1 || which < 0 || which > 7) return CPT_ERR_INVALID_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     unsigned long long* d = nullptr;
     HIP_TRY(c, hipMalloc((void**)&d, out_len * sizeof(unsigned long long)));

@@ -118,6 +118,7 @@ struct cpt_ctx {
         uint64_t src_gen = 0, dst_gen = 0;
         int src_device = -1;
         bool peer = false;
+        int mode = -1;   // last gather: CPT_GATHER_SAME_DEVICE / _PEER / _STAGED
         int32_t* d_map = nullptr;
     };
     std::vector<GatherMap> gather_maps;
@@ -128,6 +129,7 @@ struct cpt_ctx {
     hipEvent_t ev_gathered = nullptr; // a gather's destination: the stitch done
     // consolidation test hooks (cpt_set_debug_consolidation)
     uint32_t dbg = 0;
+    bool force_staged_gather = false;   // gather test hook (cpt_set_debug_gather)
     int keeper_spin_log2 = 0, publish_wait_log2 = 0;
 
     hipStream_t stream() const { return user_stream ? user_stream : own_stream; }

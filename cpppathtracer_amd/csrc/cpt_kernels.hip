@@ -17,6 +17,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "cpt_path.hpp"
+#include "cpt_dn_exp.hpp"
 
 namespace cpt {
 
@@ -756,7 +757,8 @@ __global__ void k_rng_pixels(const uint32_t* __restrict__ rowmats, const uint32_
 // (path_tracer.cu:241-254); the alpha byte is not written.
 // ======================================================================================
 // min(exp(-(dist2) / M_PI), 1.0) in double, stored to float (path_tracer.cu:224,228,231), for a
-// float dist2 -- the oracle's dm_exp(-(double)dist2 / REF_PI), branch-free:
+// float dist2 -- the oracle's dm_exp(-(double)dist2 / REF_PI), branch-free.  The SLOW form (round 4),
+// now only the fallback of dn_weight below near a float rounding boundary:
 //  * dist2 in (0, 330): x = -dist2/pi in (-105.05, 0), the quotient from dm::div_pi's sequence
 //    (correctly rounded: it depends only on dist2's significand, and every significand is
 //    checked); then dm::exp's own steps -- k, the two-part reduction, the Horner polynomial --
@@ -765,7 +767,7 @@ __global__ void k_rng_pixels(const uint32_t* __restrict__ rowmats, const uint32_
 //    float 0;  NaN: exp(NaN) = NaN, and `w < 1.0 ? w : 1.0` gives 1.
 // tests/test_exact_identities.py checks the whole function against the oracle's expression
 // for every float in [0, 2341] and the special values.
-__device__ __forceinline__ float dn_weight(float dist2) {
+__device__ __noinline__ float dn_weight_slow(float dist2) {
     constexpr double INV_PI = 1.0 / REF_PI;
     const double a = (double)dist2;
     const double q = a * INV_PI;
@@ -792,6 +794,76 @@ __device__ __forceinline__ float dn_weight(float dist2) {
     return dist2 == 0.0f ? 1.0f : f;
 }
 
+
+// The weight's short form (round 5): the same float, from a double approximation E' of
+// exp(-dist2/pi) that is within 2^-46.8 (relative) of the oracle's double E, rounded to float
+// only where that cannot matter:
+//  * E' = 2^-(n>>8) * T[n & 255] * P(r):  z = dist2 * 256/(pi ln2) (KN_HI + KN_LO), n = round(z)
+//    by the 1.5*2^52 shifter (n is t's low word), r = z - n in [-1/2, 1/2] (one fma against the
+//    exact product dist2 * KN_HI, then the low part), T[j] = 2^(-j/256) correctly rounded from the
+//    LDS table, P = the degree-4 Taylor polynomial of 2^(-r/256) (truncation 2^-54.6), and the
+//    2^-(n>>8) applied to T's exponent field (T >= 1/2 and n>>8 <= 151: stays normal).  E' is
+//    within ~2^-51 of exp(-dist2/pi); the oracle's E = dm_exp(RN(-dist2/pi)) is within 2^-47 (the
+//    quotient's rounding, |x| < 105.05) + 2^-52 of it.
+//  * Guard: if E'(1 - 2^-44) and E'(1 + 2^-44) round to the same float, every double in between
+//    does, E included (rounding is monotone), so that float is the oracle's.  Otherwise (about 2
+//    in 10^6 weights, and NaN) the slow form decides.  dist2 = 0 and dist2 >= 330 keep their
+//    shortcuts.
+// tests/test_exact_identities.py restates it on the host against the oracle for every float in
+// [0, 2341]; test_gpu_parity.py::test_dn_weight_exhaustive runs this device code against
+// dn_weight_slow for all 2^31 non-negative float patterns.
+__device__ const double g_dn_exp_table[256] = CPT_DN_EXP_TABLE_INIT;
+
+__device__ __forceinline__ double dn_exp_short(float dist2, const double* __restrict__ tab) {
+    constexpr double SHIFT = 0x1.8p52;
+    const double a = (double)dist2;
+    const double t = __builtin_fma(a, DN_KN_HI, SHIFT);
+    const double nd = t - SHIFT;
+    const uint32_t n = (uint32_t)__double2loint(t);
+    double r = __builtin_fma(a, DN_KN_HI, -nd);
+    r = __builtin_fma(a, DN_KN_LO, r);
+    double p = __builtin_fma(r, DN_C4, DN_C3);
+    p = __builtin_fma(r, p, DN_C2);
+    p = __builtin_fma(r, p, DN_C1);
+    p = __builtin_fma(r, p, 1.0);
+    const double T = tab[n & 255u];
+    const double Ts = __hiloint2double(__double2hiint(T) - (int)((n >> 8) << 20), __double2loint(T));
+    return Ts * p;
+}
+
+__device__ __forceinline__ float dn_weight(float dist2, const double* __restrict__ tab) {
+#ifdef CPT_DN_SLOW_ONLY   // A/B: the round-4 weight
+    return dn_weight_slow(dist2);
+#endif
+    const double e = dn_exp_short(dist2, tab);
+    const float f_lo = (float)(e * (1.0 - 0x1p-44)), f_hi = (float)(e * (1.0 + 0x1p-44));
+    float f = f_hi;
+    if (f_lo != f_hi && !(dist2 >= 330.0f)) f = dn_weight_slow(dist2);   // near a midpoint, or NaN
+    f = dist2 >= 330.0f ? 0.0f : f;
+    return dist2 == 0.0f ? 1.0f : f;
+}
+
+// Exhaustive check of dn_weight against dn_weight_slow (cpt_selftest_qdiv which = 6: mismatches
+// over the float patterns [0, n); which = 7: how many of them take the fallback).
+__global__ void k_selftest_dn_weight(int which, uint64_t n, unsigned long long* out, int out_len) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float d = __uint_as_float((uint32_t)i);
+        bool flag;
+        if (which == 6) {
+            const float w = dn_weight(d, g_dn_exp_table), w_ref = dn_weight_slow(d);
+            flag = __float_as_uint(w) != __float_as_uint(w_ref);
+        } else {
+            const double e = dn_exp_short(d, g_dn_exp_table);
+            flag = (float)(e * (1.0 - 0x1p-44)) != (float)(e * (1.0 + 0x1p-44)) && !(d >= 330.0f);
+        }
+        if (flag) {
+            unsigned long long k = atomicAdd(&out[0], 1ull);
+            if ((long long)k + 1 < out_len) out[k + 1] = ((unsigned long long)__float_as_uint(d) << 32);
+        }
+    }
+}
+
 // The 5x5 stencil's pair weight c_w * n_w * p_w between pixels a and b (path_tracer.cu:
 // 219-233).  Every factor is a function of the difference of the two pixels' values, squared:
 // a - b = -(b - a) exactly, so w(a, b) == w(b, a) bit for bit, and each unordered pair needs
@@ -803,21 +875,21 @@ struct DnPix { float r, g, b, nx, ny, nz, d, pad; };
 // difference squared, normal difference squared clamped at 0 in double, depth difference
 // squared (path_tracer.cu:219-233).  Inlined where the pairs are independent (the forward
 // pairs of a pixel, unrolled), so several exp sequences are in flight per lane.
-__device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b) {
+__device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b, const double* __restrict__ tab) {
     v3 t = mk(a.r, a.g, a.b) - mk(b.r, b.g, b.b);
-    const float c_w = dn_weight(dot(t, t));
+    const float c_w = dn_weight(dot(t, t), tab);
     t = mk(a.nx, a.ny, a.nz) - mk(b.nx, b.ny, b.nz);
     const double dn = (double)dot(t, t);
     const float dnf = (float)(dn > 0.0 ? dn : 0.0);
     // equal normals (a flat surface: the floor's are exactly (0, +-1, 0)) give n_w = 1; the
     // branch skips the sequence when no lane of the wave needs it
     float n_w = 1.0f;
-    if (dnf != 0.0f) n_w = dn_weight(dnf);
+    if (dnf != 0.0f) n_w = dn_weight(dnf, tab);
     const float dd = (a.d - b.d) * (a.d - b.d);
     // a18: the depths are the constant 1e30, so dd == 0 and p_w == 1 (dn_weight(0)) almost
     // always; the branch skips the sequence when no lane of the wave needs it
     float p_w = 1.0f;
-    if (dd != 0.0f) p_w = dn_weight(dd);
+    if (dd != 0.0f) p_w = dn_weight(dd, tab);
     return c_w * n_w * p_w;
 }
 
@@ -846,7 +918,10 @@ constexpr int DN_BX = DN_TX + 4, DN_BY = DN_TY + 4;   // staged box (2-pixel hal
 __host__ __device__ constexpr int dn_fdx(int k) { return k < 2 ? k + 1 : ((k - 2) % 5) - 2; }
 __host__ __device__ constexpr int dn_fdy(int k) { return k < 2 ? 0 : (k < 7 ? 1 : 2); }
 
-__global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __restrict__ accum,
+#ifndef CPT_DN_MINWAVES
+#define CPT_DN_MINWAVES 1
+#endif
+__global__ void __launch_bounds__(DN_THREADS, CPT_DN_MINWAVES) k_denoise_mix(const float4* __restrict__ accum,
                                                            const float* __restrict__ normal,
                                                            const float* __restrict__ depth, float* __restrict__ mix,
                                                            uint8_t* __restrict__ out, uint8_t* __restrict__ out_host,
@@ -854,6 +929,7 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
                                                            float inv_idx) {
     __shared__ DnPix s_pix[DN_BY * DN_BX];
     __shared__ float s_wb[DN_THREADS * 12];   // backward weight k of tile pixel (ty, tx): w(p - d_k, p)
+    __shared__ double s_tab[256];             // dn_weight's 2^(-j/256) table
     // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs (each with its own
     // L2; MI355X_MICROARCH.md §Workgroup dispatch), so block b runs on the XCD of b mod 8.  Each
     // XCD takes one contiguous run of tiles in column-major order, so consecutive tiles on an
@@ -868,6 +944,7 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
     const int tw = min(DN_TX, w_eff - x0), th = min(DN_TY, y1 - ty0);   // the tile's extent
     const int limit = w_eff * h_eff;
     // ---- stage the box: linear pixels (ty0 - 2 + by) * W' + x0 - 2 + bx ----------------
+    for (int i = threadIdx.x; i < 256; i += DN_THREADS) s_tab[i] = g_dn_exp_table[i];
 #pragma unroll 1
     for (int i = threadIdx.x; i < DN_BY * DN_BX; i += DN_THREADS) {
         const int by = i / DN_BX, bx = i - by * DN_BX;
@@ -900,7 +977,7 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
     for (int k = 0; k < 12; ++k) {
         const int dx = dn_fdx(k), dy = dn_fdy(k);
         const DnPix& q = box(tx + dx, ty + dy);
-        wf[k] = (mine && q.pad != 0.f) ? dn_pair_weight(p, q) : 0.f;
+        wf[k] = (mine && q.pad != 0.f) ? dn_pair_weight(p, q, s_tab) : 0.f;
         if (mine && in_tile(tx + dx, ty + dy)) s_wb[((ty + dy) * DN_TX + tx + dx) * 12 + k] = wf[k];
     }
     // ---- pairs (s, t = s + d) with t in the tile and s outside it ------------------------
@@ -938,7 +1015,7 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
             }
             const DnPix& t = box(sx, sy);
             const DnPix& sp = box(sx - dx, sy - dy);
-            s_wb[(sy * DN_TX + sx) * 12 + k] = sp.pad != 0.f ? dn_pair_weight(sp, t) : 0.f;
+            s_wb[(sy * DN_TX + sx) * 12 + k] = sp.pad != 0.f ? dn_pair_weight(sp, t, s_tab) : 0.f;
         }
     }
     __syncthreads();
@@ -955,7 +1032,7 @@ __global__ void __launch_bounds__(DN_THREADS) k_denoise_mix(const float4* __rest
                         __builtin_isfinite(p.nx) && __builtin_isfinite(p.ny) && __builtin_isfinite(p.nz) &&
                         __builtin_isfinite(p.d);
     float w_self = 1.0f;
-    if (!finite) w_self = dn_pair_weight(p, p);
+    if (!finite) w_self = dn_pair_weight(p, p, s_tab);
     const float* wb = s_wb + threadIdx.x * 12;
     v3 sum = mk1(0.f);
     float cum_w = 0.0f;
@@ -1358,7 +1435,10 @@ hipError_t launch_stream_read(const float4* p, size_t n, float* out, int grid, h
 
 hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len,
                                 hipStream_t stream) {
-    hipLaunchKernelGGL(k_selftest_qdiv, dim3(4096), dim3(256), 0, stream, which, n, seed, out, out_len);
+    if (which >= 6)
+        hipLaunchKernelGGL(k_selftest_dn_weight, dim3(8192), dim3(256), 0, stream, which, n, out, out_len);
+    else
+        hipLaunchKernelGGL(k_selftest_qdiv, dim3(4096), dim3(256), 0, stream, which, n, seed, out, out_len);
     return hipGetLastError();
 }
 

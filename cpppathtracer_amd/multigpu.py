@@ -33,8 +33,11 @@ class TileGather:
         # (a no-op wait when the context launches on torch's stream, as bench.py sets up), and
         # surface any device error of the render
         renderer.synchronize()
-        if self.world == 1:
+        if self.world == 1 and not dist.is_initialized():
             return self.send.view(self.max_rows, self.width, 4)[: self.height]
+        # with a process group the collective runs at any world size, 1 included (bench.py under
+        # torch.distributed.run with one rank, tests/test_gpu_rccl.py): the RCCL branch below is
+        # then exercised on a one-GPU box
         if self.backend == "nccl":
             dist.all_gather_into_tensor(self.gathered, self.send)
         else:   # gloo: host copies (rehearsal with ranks sharing a GPU)

@@ -87,7 +87,8 @@ class Renderer:
         the ordered walk's tree rebuilt on the host (rebuild=True, cpt_update_objects_rebuild)."""
         idx = np.ascontiguousarray(indices, dtype=np.int32)
         o = np.ascontiguousarray(objs, dtype=OBJECT_DTYPE)
-        assert o.shape == idx.shape
+        if o.shape != idx.shape:
+            raise ValueError(f"update_objects: {o.shape[0] if o.ndim else 1} objects for {idx.size} indices")
         fn = self._L.cpt_update_objects_rebuild if rebuild else self._L.cpt_update_objects
         self._check(fn(self._ctx, int(idx.size), _p(idx), _p(o)))
 
@@ -203,7 +204,8 @@ class Renderer:
 
     def write_rng(self, planar6):
         a = np.ascontiguousarray(planar6, dtype=np.uint32)
-        assert a.shape == (6, self.npix)
+        if a.shape != (6, self.npix):
+            raise ValueError(f"write_rng: expected shape (6, {self.npix}), got {a.shape}")
         self._check(self._L.cpt_write_rng(self._ctx, _p(a)))
 
     def read_aux(self):
@@ -229,6 +231,19 @@ class Renderer:
     def gather_rows(self, src):
         """cpt_gather_rows: place the rows Renderer `src` rendered into this frame (row tiling)."""
         self._check(self._L.cpt_gather_rows(self._ctx, src._ctx))
+
+    GATHER_MODES = {-1: None, 0: "same_device", 1: "peer", 2: "staged"}
+
+    def last_gather_mode(self, src):
+        """How the last gather_rows(src) reached src's buffers: "same_device", "peer" (xGMI
+        reads with peer access), "staged" (a peer copy first), or None (no gather yet)."""
+        m = ctypes.c_int(-1)
+        self._check(self._L.cpt_last_gather_mode(self._ctx, src._ctx, ctypes.byref(m)))
+        return self.GATHER_MODES[m.value]
+
+    def set_debug_gather(self, force_staged):
+        """Test hook: route this context's gathers through the staged peer copy."""
+        self._check(self._L.cpt_set_debug_gather(self._ctx, int(bool(force_staged))))
 
     def stats(self):
         s = (ctypes.c_uint64 * 5)()
@@ -280,13 +295,35 @@ class Renderer:
                  for v in out[1:1 + min(cnt, examples)]]
         return cnt, pairs
 
-    def denoise_mix(self, cur_sample_idx, out=None):
+    def denoise_mix(self, cur_sample_idx, out=None, host=True):
         """Denoising + Mix display pass; returns the BGRA8 frame (height, width, 4), into `out`
-        when given (a preallocated, e.g. pinned, host array of that shape)."""
+        when given (a preallocated, e.g. pinned, host array of that shape).  host=False keeps the
+        frame on the device (no host write; returns None): the display kernel's device-only time."""
+        if not host:
+            self._check(self._L.cpt_denoise_mix(self._ctx, cur_sample_idx, None))
+            self._band_rows = None
+            return None
         if out is None:
             out = np.zeros((self.height, self.width, 4), dtype=np.uint8)
-        assert out.dtype == np.uint8 and out.size == self.height * self.width * 4 and out.flags["C_CONTIGUOUS"]
+        # explicit checks, not asserts: the C-ABI writes a full H*W*4 frame into `out` (a kernel
+        # store through a pinned alias or a hipMemcpyAsync), so a bad buffer must raise, also
+        # under `python -O`
+        if not isinstance(out, np.ndarray) or out.dtype != np.uint8:
+            raise ValueError("denoise_mix: `out` must be a numpy uint8 array")
+        if out.size != self.height * self.width * 4:
+            raise ValueError(f"denoise_mix: `out` holds {out.size} bytes, the frame needs "
+                             f"{self.height * self.width * 4}")
+        if not out.flags["C_CONTIGUOUS"] or not out.flags["WRITEABLE"]:
+            raise ValueError("denoise_mix: `out` must be C-contiguous and writeable")
         self._check(self._L.cpt_denoise_mix(self._ctx, cur_sample_idx, _p(out)))
+        self._band_rows = None
+        return out
+
+    def read_mix(self):
+        """The Mix running mean of the display band: [(y1 - y0) * width, 3] float32."""
+        rows = self._band_rows if getattr(self, "_band_rows", None) else 16 * (self.height // 16)
+        out = np.zeros((rows * self.width, 3), dtype=np.float32)
+        self._check(self._L.cpt_read_mix(self._ctx, _p(out)))
         return out
 
     def last_display_ms(self) -> float:
@@ -302,6 +339,7 @@ class Renderer:
         out = np.zeros((y1 - y0, self.width, 4), dtype=np.uint8) if host else None
         self._check(self._L.cpt_denoise_mix_band(self._ctx, cur_sample_idx, int(y0), int(y1),
                                                  _p(out) if host else None))
+        self._band_rows = int(y1 - y0)
         return out
 
     def copy_bgra_device(self, device_ptr, nbytes):

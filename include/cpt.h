@@ -274,6 +274,17 @@ int cpt_copy_accum_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
  * frame for its next call (cpt_synchronize, cpt_read_accum, cpt_read_aux, cpt_denoise_mix).
  * src's device errors are reported by src's own next synchronising call. */
 int cpt_gather_rows(cpt_ctx* dst, cpt_ctx* src);
+/* How the last cpt_gather_rows(dst, src) reached src's buffers (-1: no gather of the pair yet):
+ * the stitch read them in place on the same device, read them over xGMI with peer access
+ * (contexts on two devices), or read a staged hipMemcpyPeerAsync copy (no peer path, or
+ * forced by cpt_set_debug_gather).  No reference counterpart: a test hook for §8(e). */
+#define CPT_GATHER_SAME_DEVICE 0
+#define CPT_GATHER_PEER 1
+#define CPT_GATHER_STAGED 2
+int cpt_last_gather_mode(cpt_ctx* dst, cpt_ctx* src, int* mode);
+/* TEST HOOK: force dst's gathers through the staged peer copy (the fallback for device pairs
+ * without peer access), so that branch runs on a one-GPU box too. */
+int cpt_set_debug_gather(cpt_ctx* dst, int force_staged);
 int cpt_get_stats(cpt_ctx* ctx, cpt_stats* out);
 int cpt_reset_stats(cpt_ctx* ctx);
 /* All 8 raw device counters (0-4 = cpt_stats; 5 = ordered-walk segments that failed the
@@ -322,6 +333,9 @@ int cpt_host_unregister(void* ptr);
 int cpt_denoise_mix_band(cpt_ctx* ctx, uint32_t cur_sample_idx, int y0, int y1, uint8_t* bgra_host);
 /* Device-to-device copy of the current display band's BGRA8 rows (for an RCCL gather). */
 int cpt_copy_bgra_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
+/* The Mix running mean of the current display band ([(y1-y0)*W][3] floats: rows y0..y1-1; the
+ * whole 16-aligned launch's rows for cpt_denoise_mix), read back for checking and checkpoints. */
+int cpt_read_mix(cpt_ctx* ctx, float* rgb);
 /* Device time of the last display kernel (Denoising + Mix, the reference's per-pass log of
  * path_tracer.cu:261,300 split by kernel), from HIP events on the context's stream; waits
  * for it. */
@@ -350,6 +364,9 @@ int cpt_math_batch(cpt_ctx* ctx, int op, const float* a, const float* b, float* 
  * its domain (2^-126 <= |d| < 2^126, 0, inf, NaN) and rcp_f(sqrtf(d)) for every pattern.
  * which = 5: the f32 square-root helper sqrt_nn against sqrtf on its domain (+-0,
  * |x| >= 2^-96, inf, NaN).
+ * which = 6: the display weight dn_weight (short exp + rounding guard) against its slow form
+ * dn_weight_slow for the float bit patterns [0, n) (n = 2^31: every non-negative float, inf and
+ * NaN); which = 7: counts the patterns whose guard sends them to the slow form (not an error).
  * out[0] receives the mismatch count (0 expected), out[1..out_len) up to out_len-1 failing
  * pairs as (a bits << 32 | d bits). */
 int cpt_selftest_qdiv(cpt_ctx* ctx, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len);

@@ -81,14 +81,18 @@ def test_exact_identities(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout
     assert "bad 0" in r.stdout
+    print(r.stdout)
 
 
-# The display's branch-free pair weight (cpt_kernels.hip dn_weight) against the oracle's own
-# expression min(exp(-(double)d2 / M_PI), 1.0) stored to float (oracle or_exp = dm_exp,
-# path_tracer.cu:224,228,231), for every float d2 in [0, 2341] -- the quotient, dm_exp's steps
-# with a plain ldexp below x = -105.05, and the shortcuts (0 -> 1, >= 330 -> 0) -- and the
-# special values.  The harness calls the oracle library (test infrastructure).
+# The display's pair weight against the oracle's own expression min(exp(-(double)d2 / M_PI), 1.0)
+# stored to float (oracle or_exp = dm_exp, path_tracer.cu:224,228,231), for every float d2 in
+# [0, 2341] and the special values: the round-4 branch-free form (cpt_kernels.hip dn_weight_slow:
+# the quotient, dm_exp's steps with a plain ldexp below x = -105.05, the shortcuts 0 -> 1,
+# >= 330 -> 0), and the round-5 short form (dn_weight: the 2^(-j/256) table exp of
+# cpt_dn_exp.hpp and the rounding guard that falls back to the slow form).  The harness calls the
+# oracle library (test infrastructure).
 DN_SRC = r"""
+#include "cpt_dn_exp.hpp"
 #include <dlfcn.h>
 #include <math.h>
 #include <pthread.h>
@@ -119,14 +123,40 @@ static float fast_w(float d2) {   /* cpt_kernels.hip dn_weight, operation for op
     f = d2 >= 330.0f ? 0.0f : f;
     return d2 == 0.0f ? 1.0f : f;
 }
+static const double DN_TAB[256] = CPT_DN_EXP_TABLE_INIT;
+static int g_guard_fallbacks[8];
+static float short_w(float d2, int t) {   /* cpt_kernels.hip dn_exp_short + dn_weight */
+    const double SHIFT = 0x1.8p52, a = (double)d2;
+    const double tt = fma(a, cpt::DN_KN_HI, SHIFT), nd = tt - SHIFT;
+    uint64_t tb; memcpy(&tb, &tt, 8);
+    const uint32_t n = (uint32_t)tb;
+    double r = fma(a, cpt::DN_KN_HI, -nd);
+    r = fma(a, cpt::DN_KN_LO, r);
+    double p = fma(r, cpt::DN_C4, cpt::DN_C3);
+    p = fma(r, p, cpt::DN_C2);
+    p = fma(r, p, cpt::DN_C1);
+    p = fma(r, p, 1.0);
+    double T = DN_TAB[n & 255u];
+    uint64_t Tb; memcpy(&Tb, &T, 8);
+    const uint32_t hi = (uint32_t)(Tb >> 32) - ((n >> 8) << 20);
+    Tb = ((uint64_t)hi << 32) | (Tb & 0xffffffffull);
+    memcpy(&T, &Tb, 8);
+    const double e = T * p;
+    const float f_lo = (float)(e * (1.0 - 0x1p-44)), f_hi = (float)(e * (1.0 + 0x1p-44));
+    float f = f_hi;
+    if (f_lo != f_hi && !(d2 >= 330.0f)) { f = fast_w(d2); if (t >= 0) g_guard_fallbacks[t]++; }
+    f = d2 >= 330.0f ? 0.0f : f;
+    return d2 == 0.0f ? 1.0f : f;
+}
 static uint32_t g_lim;
 static unsigned long long g_bad[8];
 static void* run(void* arg) {
     int t = (int)(intptr_t)arg;
     for (uint32_t b = (uint32_t)t; b <= g_lim; b += 8) {
         float d; memcpy(&d, &b, 4);
-        float x = ref_w(d), y = fast_w(d);
-        if (memcmp(&x, &y, 4) != 0) { if (g_bad[t] < 3) printf("dn_weight %a: %a vs %a\n", d, x, y); g_bad[t]++; }
+        float x = ref_w(d), y = fast_w(d), z = short_w(d, t);
+        if (memcmp(&x, &y, 4) != 0) { if (g_bad[t] < 3) printf("dn_weight_slow %a: %a vs %a\n", d, x, y); g_bad[t]++; }
+        if (memcmp(&x, &z, 4) != 0) { if (g_bad[t] < 3) printf("dn_weight %a: %a vs %a\n", d, x, z); g_bad[t]++; }
     }
     return 0;
 }
@@ -141,9 +171,13 @@ int main(int argc, char** argv) {
     for (int t = 0; t < 8; ++t) { pthread_join(th[t], 0); bad += g_bad[t]; }
     const float sp[] = {INFINITY, NAN, -0.0f, 3.4e38f, 1e-45f, 329.99998f, 330.0f, 2340.9f};
     for (int i = 0; i < 8; ++i) {
-        float x = ref_w(sp[i]), y = fast_w(sp[i]);
+        float x = ref_w(sp[i]), y = fast_w(sp[i]), z = short_w(sp[i], -1);
         if (memcmp(&x, &y, 4) != 0) { printf("special %a: %a vs %a\n", sp[i], x, y); bad++; }
+        if (memcmp(&x, &z, 4) != 0) { printf("special short %a: %a vs %a\n", sp[i], x, z); bad++; }
     }
+    long fb = 0;
+    for (int t = 0; t < 8; ++t) fb += g_guard_fallbacks[t];
+    printf("guard fallbacks %ld of %u\n", fb, g_lim + 1);
     printf("bad %llu\n", bad);
     return bad != 0;
 }
@@ -153,11 +187,13 @@ int main(int argc, char** argv) {
 def test_denoise_weight_exhaustive(tmp_path):
     import oracle
     lib = oracle.build()
-    src = tmp_path / "dnw.c"
+    src = tmp_path / "dnw.cpp"
     exe = tmp_path / "dnw"
     src.write_text(DN_SRC)
-    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-fno-fast-math", "-o", str(exe), str(src), "-lm", "-ldl",
-                    "-lpthread"], check=True)
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "cpppathtracer_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-ffp-contract=off", "-fno-fast-math", "-I", csrc, "-o", str(exe), str(src), "-lm",
+                    "-ldl", "-lpthread"], check=True)
     r = subprocess.run([str(exe), lib], capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout
     assert "bad 0" in r.stdout
+    print(r.stdout)

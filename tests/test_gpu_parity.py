@@ -97,6 +97,20 @@ def test_sqrt_nn_exhaustive(gpu):
     assert cnt == 0, [float(d) for _, d in pairs]
 
 
+def test_dn_weight_exhaustive(gpu):
+    """The display weight (cpt_kernels.hip dn_weight: the short table exp + rounding guard) ==
+    its slow form dn_weight_slow (the round-4 sequence, itself equal to the oracle's
+    min(dm_exp(-(double)d2 / M_PI), 1.0) on every float in [0, 2341]:
+    test_exact_identities.py::test_denoise_weight_exhaustive) for all 2^31 non-negative float
+    patterns: 0, subnormals, (0, 330) where the short exp decides, the >= 330 shortcut, inf and
+    every NaN.  Also records how rarely the guard falls back (path_tracer.cu:219-233)."""
+    cnt, pairs = gpu.selftest_qdiv(6, 1 << 31)
+    assert cnt == 0, [float(a) for a, _ in pairs]
+    fallbacks, _ = gpu.selftest_qdiv(7, 0x43A50000)   # [0, 330): the guard's fallbacks
+    nan_free = 0x43A50000
+    assert fallbacks < 1e-5 * nan_free, fallbacks
+
+
 # ------------------------------------------------------------------------------- rng
 @pytest.mark.parametrize("w,rows", [(64, list(range(64))), (3840, [0, 1, 7, 1079, 2159]),
                                     (333, [5, 3, 200, 3])])

@@ -139,3 +139,21 @@ def test_cpp_driver_scenes_equal_python_scenes(tmp_path, scene):
     got = np.fromfile(out, dtype=np.uint8)
     want = np.ascontiguousarray(scenes.SCENES[scene]()).view(np.uint8).ravel()
     np.testing.assert_array_equal(got, want)
+
+
+def test_denoise_mix_rejects_bad_host_buffers():
+    """Advisor r04: the display call checks the caller's frame with exceptions (not asserts, which
+    `python -O` strips): the C-ABI would write H*W*4 bytes into it."""
+    import numpy as np
+    import pytest
+    from cpppathtracer_amd import Renderer
+    r = object.__new__(Renderer)   # no context: the checks run before any C-ABI call
+    r.height, r.width = 4, 8
+    for bad in (np.zeros((4, 8, 4), dtype=np.float32), np.zeros((4, 8, 3), dtype=np.uint8),
+                np.zeros((8, 8, 4), dtype=np.uint8)[::2], bytearray(128)):
+        with pytest.raises(ValueError):
+            r.denoise_mix(1, out=bad)
+    ro = np.zeros((4, 8, 4), dtype=np.uint8)
+    ro.flags.writeable = False
+    with pytest.raises(ValueError):
+        r.denoise_mix(1, out=ro)

@@ -23,10 +23,13 @@ REF_PNG = "/root/reference/textures/sky.png"
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets", "sky.cptex")
 
 
-def main() -> int:
+def fixture_bytes(png_path: str = REF_PNG) -> bytes:
+    """The .cptex file's bytes for the PNG at `png_path` (header + the W/4 valid columns as
+    RGBA8).  tests/test_sky_fixture.py re-runs this on the reference's PNG and compares it with
+    the committed assets/sky.cptex byte for byte."""
     from PIL import Image
 
-    img = Image.open(REF_PNG)
+    img = Image.open(png_path)
     assert img.mode == "RGB", img.mode
     rgb = np.asarray(img, dtype=np.uint8)  # (H, W, 3)
     h, w, _ = rgb.shape
@@ -36,10 +39,14 @@ def main() -> int:
     rgba[..., 3] = 255
     # header: magic, logical width, height, stored (valid) columns, reserved
     hdr = b"CPTTEX01" + struct.pack("<IIII", w, h, valid_cols, 0)
+    return hdr + np.ascontiguousarray(rgba).tobytes()
+
+
+def main() -> int:
+    data = fixture_bytes(REF_PNG)
     with open(OUT, "wb") as f:
-        f.write(hdr)
-        f.write(np.ascontiguousarray(rgba).tobytes())
-    print(f"wrote {OUT}: logical {w}x{h}, stored cols {valid_cols}, {rgba.nbytes} texel bytes")
+        f.write(data)
+    print(f"wrote {OUT}: {len(data)} bytes")
     return 0
 
 
