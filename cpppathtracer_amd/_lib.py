@@ -30,6 +30,7 @@ PROTOTYPES = {
     "cpt_update_objects": (_I, [_P, _I, _P, _P]),
     "cpt_update_objects_rebuild": (_I, [_P, _I, _P, _P]),
     "cpt_last_update_ms": (_I, [_P, _P]),
+    "cpt_get_material_count": (_I, [_P, _P]),
     "cpt_scene_bvh_export": (_I, [_P, _P, _P, _I, _P]),
     "cpt_bvh_build_host": (_I, [_P, _I, _P, _P, _I, _P]),
     "cpt_set_env_texture": (_I, [_P, _P, _I, _I, _I]),

@@ -279,8 +279,21 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                         // long chains (spp >= 64): smaller ranges, since a wave's unstarted ids then hold
                         // back long chains other waves' idle lanes could run
                         const uint32_t bsz = p.spp >= 64 ? (uint32_t)CPT_TAKE_BATCH_LONG : (uint32_t)CPT_TAKE_BATCH;
-                        // the consolidating kernel (frames of <= 4 pixels per lane) takes exactly what it needs
-                        const uint32_t grab = (!CONS || CPT_TAKE_BATCH_CONS) && n_work - res_seen > n_static && bsz > want ? bsz : want;
+                        // the consolidating kernel (frames of <= 4 pixels per lane) takes exactly what it needs.
+                        // Near the end of the image (less than one id per lane of the grid left) a
+                        // wave draws only what it needs.  `res_seen` is the counter as this wave saw
+                        // it at its last draw; a wave on long chains draws rarely, so with
+                        // CPT_TAKE_FRESH its leader reads the counter's current value first (one
+                        // relaxed load per draw, i.e. per ~64 takes at spp >= 64).
+                        uint32_t seen = res_seen;
+#if CPT_TAKE_FRESH
+                        if (p.spp >= 64) {
+                            uint32_t cur = 0;
+                            if (lane == leader) cur = __hip_atomic_load(p.work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            seen = __builtin_amdgcn_readfirstlane(__shfl(cur, leader)) + off;
+                        }
+#endif
+                        const uint32_t grab = (!CONS || CPT_TAKE_BATCH_CONS) && n_work - seen > n_static && bsz > want ? bsz : want;
                         if (lane == leader) nb = atomicAdd(p.work, grab);
                         nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader)) + off;
                         ncnt = grab;
@@ -912,6 +925,12 @@ __device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b, 
 #ifndef CPT_DN_TY
 #define CPT_DN_TY 8
 #endif
+#ifndef CPT_DN_TILE          // 1: the round-4 tile kernel (A/B); 0: k_denoise_strip
+#define CPT_DN_TILE 0
+#endif
+#ifndef CPT_DN_WAVES_PER_CU  // k_denoise_strip's waves per CU (LDS: 19.5 KB per wave)
+#define CPT_DN_WAVES_PER_CU 8
+#endif
 constexpr int DN_TX = 64, DN_TY = CPT_DN_TY, DN_THREADS = DN_TX * DN_TY;
 constexpr int DN_BX = DN_TX + 4, DN_BY = DN_TY + 4;   // staged box (2-pixel halo each side)
 // forward offsets (dx, dy), k = 0..11: dy = 0, dx = 1, 2; dy = 1, dx = -2..2; dy = 2, dx = -2..2
@@ -1077,15 +1096,272 @@ __global__ void __launch_bounds__(DN_THREADS, CPT_DN_MINWAVES) k_denoise_mix(con
     if (out_host) reinterpret_cast<uint32_t*>(out_host)[bself] = bgr;
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_denoise_strip (round 5, the default): the same Denoising + Mix, bit for bit, as a per-wave
+// sliding window with no block barrier.  A wave owns a strip of 60 output columns (lanes 2..61;
+// lanes 0, 1, 62, 63 carry the two halo columns each side) and a run of output rows, and walks down
+// it one row per step:
+//  * lane j at row Y holds the pixel of LINEAR index L = Y W' + c0 - 2 + j (the stencil's v W' + u
+//    offsets, path_tracer.cu:205-216: columns past either edge wrap into the adjacent row, exactly as
+//    the reference); row Y enters a 5-row ring in the wave's LDS (radiance, normal, depth, validity);
+//  * at step Y the lane computes the 12 pair weights whose later pixel is its own (Y, j): the two
+//    same-row forward pairs (Y, j+1), (Y, j+2) and the pairs with rows Y-1 and Y-2 at columns
+//    j-2..j+2 -- every unordered pair of the stencil exactly once, as the tile kernel's forward
+//    pairs -- into a 3-step ring of weights in LDS;
+//  * row O = Y - 2 is then complete: each output lane sums its 25 taps in the reference's order,
+//    reading the weights it needs from the ring (its own, or its neighbours' at lane j +- u).
+// The weights are evaluated in batches of 6 with one wave-wide fallback branch (dn_weight's guard),
+// so the six exp chains overlap.  Global reads: one coalesced row of accumulator / normal / depth
+// per step, prefetched a step ahead; no barrier after the table load (one wave never races itself:
+// its LDS operations complete in order; wave_fence keeps the compiler from reordering them).
+constexpr int DNS_LANES = 64, DNS_COLS = 60, DNS_WAVES = 4;
+struct DnsPix { float4 rgbv; float4 nd; };   // (r, g, b, valid), (nx, ny, nz, depth)
+
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Pair weights c_w * n_w * p_w of N pairs (path_tracer.cu:219-233; dn_pair_weight's factors, in
+// the same order), batched: N short exps in flight, and the guard's rare fallback as one branch.
+template <int N>
+__device__ __forceinline__ void dn_weights(const float d2[N], float w[N], const double* __restrict__ tab) {
+    uint32_t slow = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const double e = dn_exp_short(d2[i], tab);
+        const float f_lo = (float)(e * (1.0 - 0x1p-44)), f_hi = (float)(e * (1.0 + 0x1p-44));
+        w[i] = f_hi;
+        slow |= (f_lo != f_hi && !(d2[i] >= 330.0f)) ? 1u << i : 0u;
+    }
+    if (__builtin_expect(slow != 0, 0)) {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if ((slow >> i) & 1u) w[i] = dn_weight_slow(d2[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        w[i] = d2[i] >= 330.0f ? 0.0f : w[i];
+        w[i] = d2[i] == 0.0f ? 1.0f : w[i];
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void dn_pair_weights(const DnsPix a[N], const DnsPix& b, float out[N],
+                                                const double* __restrict__ tab) {
+    float c2[N], n2[N], p2[N];
+    bool any_n = false, any_p = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        v3 t = mk(a[i].rgbv.x, a[i].rgbv.y, a[i].rgbv.z) - mk(b.rgbv.x, b.rgbv.y, b.rgbv.z);
+        c2[i] = dot(t, t);
+        t = mk(a[i].nd.x, a[i].nd.y, a[i].nd.z) - mk(b.nd.x, b.nd.y, b.nd.z);
+        const float dn = dot(t, t);
+        n2[i] = dn > 0.0f ? dn : 0.0f;   // (float)max((double)dn, 0.0): the reference's clamp in double
+        p2[i] = (a[i].nd.w - b.nd.w) * (a[i].nd.w - b.nd.w);
+        any_n |= n2[i] != 0.0f;
+        any_p |= p2[i] != 0.0f;
+    }
+    float cw[N], nw[N], pw[N];
+    dn_weights<N>(c2, cw, tab);
+    // a zero normal (depth) difference gives exactly 1 (dn_weight(0)); equal normals (the floor)
+    // and the constant depth (a18) make whole batches of the wave skip the sequence
+#pragma unroll
+    for (int i = 0; i < N; ++i) nw[i] = pw[i] = 1.0f;
+    if (__builtin_amdgcn_ballot_w64(any_n)) dn_weights<N>(n2, nw, tab);
+    if (__builtin_amdgcn_ballot_w64(any_p)) dn_weights<N>(p2, pw, tab);
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = cw[i] * nw[i] * pw[i];
+}
+
+__global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
+    const float4* __restrict__ accum, const float* __restrict__ normal, const float* __restrict__ depth,
+    float* __restrict__ mix, uint8_t* __restrict__ out, uint8_t* __restrict__ out_host, int width, int row0, int y0,
+    int y1, int w_eff, int h_eff, int n_strips, int per_strip, float inv_idx) {
+    __shared__ double s_tab[256];
+    __shared__ DnsPix s_ring[DNS_WAVES][5][DNS_LANES];
+    __shared__ float s_w[DNS_WAVES][3][12][DNS_LANES];
+    for (int i = threadIdx.x; i < 256; i += DNS_LANES * DNS_WAVES) s_tab[i] = g_dn_exp_table[i];
+    __syncthreads();
+    const int wv = (int)(threadIdx.x >> 6), j = (int)(threadIdx.x & 63);
+    const int wid = (int)blockIdx.x * DNS_WAVES + wv;
+    if (wid >= n_strips * per_strip) return;
+    const int strip = wid % n_strips, part = wid / n_strips;
+    const int nrow = y1 - y0;
+    const int ra = y0 + (int)((long long)nrow * part / per_strip), rb = y0 + (int)((long long)nrow * (part + 1) / per_strip);
+    if (ra >= rb) return;
+    const int c0 = strip * DNS_COLS;
+    const int col = c0 - 2 + j;                     // this lane's column of the linear run (may be < 0 or >= W')
+    const int limit = w_eff * h_eff;
+    const bool out_lane = j >= 2 && j < 2 + DNS_COLS && col < w_eff;
+    DnsPix (*ring)[DNS_LANES] = s_ring[wv];
+    float (*W)[12][DNS_LANES] = s_w[wv];
+    // (lane indices of partners, clamped into the wave: edge lanes compute pairs nobody reads)
+    auto cl = [](int l) { return l < 0 ? 0 : (l > 63 ? 63 : l); };
+    // pixel of row Y at this lane: L = Y W' + col
+    auto load = [&](int Y, float4& a, float3& n, float& d, bool& valid) {
+        const int L = Y * w_eff + col;
+        valid = L >= 0 && L < limit;
+        if (valid) {
+            const int yy = col < 0 ? Y - 1 : (col >= w_eff ? Y + 1 : Y);
+            const int xx = L - yy * w_eff;
+            const size_t px = (size_t)(yy - row0) * width + xx;
+            a = accum[px];
+            n = make_float3(normal[3 * px], normal[3 * px + 1], normal[3 * px + 2]);
+            d = depth[px];
+        } else {
+            a = make_float4(0.f, 0.f, 0.f, 0.f);
+            n = make_float3(0.f, 0.f, 0.f);
+            d = 0.f;
+        }
+    };
+    float4 na;
+    float3 nn;
+    float nd;
+    bool nvalid;
+    load(ra - 2, na, nn, nd, nvalid);
+    float3 mix_next = make_float3(0.f, 0.f, 0.f);
+    constexpr float kernel5[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
+                                     {4.f, 16.f, 26.f, 16.f, 4.f},
+                                     {7.f, 26.f, 41.f, 26.f, 7.f},
+                                     {4.f, 16.f, 26.f, 16.f, 4.f},
+                                     {1.f, 4.f, 7.f, 4.f, 1.f}};
+#pragma unroll 1
+    for (int Y = ra - 2; Y < rb + 2; ++Y) {
+        // ---- row Y into the ring; prefetch row Y + 1 and the mix of the next output row --------
+        DnsPix me;
+        {
+            const v3 c = na.w != 0.f ? mk(na.x, na.y, na.z) / na.w : mk(na.x, na.y, na.z);
+            me.rgbv = make_float4(c.x, c.y, c.z, nvalid ? 1.f : 0.f);
+            me.nd = make_float4(nn.x, nn.y, nn.z, nd);
+        }
+        const int slot = (Y + 10) % 5;
+        ring[slot][j] = me;
+        if (Y + 1 < rb + 2) load(Y + 1, na, nn, nd, nvalid);
+        const int O = Y - 2;                     // the output row this step completes
+        float3 mix_cur = mix_next;
+        if (O + 1 >= ra && O + 1 < rb && out_lane) {
+            const size_t b = (size_t)(O + 1 - y0) * width + col;
+            mix_next = make_float3(mix[3 * b], mix[3 * b + 1], mix[3 * b + 2]);
+        }
+        wave_fence();
+        // ---- the 12 pair weights whose later pixel is (Y, j) -----------------------------------
+        // needed for output rows Y - 2 .. Y only while Y >= ra; the last two steps need only the
+        // pairs reaching back into rows < rb (the same-row pairs of rows >= rb are never read)
+        if (Y >= ra) {
+            const int s1 = (Y + 9) % 5, s2 = (Y + 8) % 5;
+            float w12[12];
+            {
+                DnsPix a[6];
+                a[0] = ring[slot][cl(j + 1)];
+                a[1] = ring[slot][cl(j + 2)];
+#pragma unroll
+                for (int dx = -2; dx <= 1; ++dx) a[2 + dx + 2] = ring[s1][cl(j + dx)];
+                dn_pair_weights<6>(a, me, w12, s_tab);   // k = 0, 1 (dy 0), 2..5 (dy 1, dx -2..1)
+            }
+            {
+                DnsPix a[6];
+                a[0] = ring[s1][cl(j + 2)];
+#pragma unroll
+                for (int dx = -2; dx <= 2; ++dx) a[1 + dx + 2] = ring[s2][cl(j + dx)];
+                dn_pair_weights<6>(a, me, w12 + 6, s_tab);   // k = 6 (dy 1, dx 2), 7..11 (dy 2)
+            }
+            // forward index k of the pair (Y - dy, j + dx) -> (Y, j): here the later pixel is
+            // this lane's, so the pair is the EARLIER pixel's forward (dx' = -dx, dy' = dy);
+            // store it under the earlier pixel's forward index k(dy, -dx) at this lane
+            const int ws = (Y + 9) % 3;
+#pragma unroll
+            for (int k = 0; k < 12; ++k) W[ws][k][j] = w12[k];
+        }
+        wave_fence();
+        // ---- output row O: the 25 taps in the reference's order (i = dx outer, j = dy inner) -------
+        if (O >= ra && O < rb && out_lane) {
+            const int wO = (O + 9) % 3, wO1 = (O + 10) % 3, wO2 = (O + 11) % 3;
+            const DnsPix p = ring[(O + 10) % 5][j];
+            const bool finite = __builtin_isfinite(p.rgbv.x) && __builtin_isfinite(p.rgbv.y) &&
+                                __builtin_isfinite(p.rgbv.z) && __builtin_isfinite(p.nd.x) &&
+                                __builtin_isfinite(p.nd.y) && __builtin_isfinite(p.nd.z) && __builtin_isfinite(p.nd.w);
+            float w_self = 1.0f;
+            if (!finite) {
+                float ws1[1];
+                dn_pair_weights<1>(&p, p, ws1, s_tab);
+                w_self = ws1[0];
+            }
+            v3 sum = mk1(0.f);
+            float cum_w = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+#pragma unroll
+                for (int jj = 0; jj < 5; ++jj) {
+                    const int u = i - 2, v = jj - 2;
+                    const DnsPix q = ring[(O + v + 10) % 5][j + u];
+                    float weight;
+                    v3 ctmp;
+                    if (q.rgbv.w == 0.f) {
+                        weight = 0.f * 0.f * 0.f;
+                        ctmp = mk1(0.f);
+                    } else {
+                        ctmp = mk(q.rgbv.x, q.rgbv.y, q.rgbv.z);
+                        // where the pair (O, j) - (O + v, j + u) was stored: same row -- by the lane
+                        // of its left pixel at step O, as that pixel's forward pair |u| - 1; other
+                        // rows -- by the lane of its lower pixel at that pixel's step, at index
+                        // 2 + dx + 2 (dy 1) or 7 + dx + 2 (dy 2), dx = upper column - lower column
+                        if (u == 0 && v == 0) weight = w_self;
+                        else if (v == 0 && u > 0) weight = W[wO][u - 1][j];
+                        else if (v == 0) weight = W[wO][-u - 1][j + u];
+                        else if (v < 0) weight = W[wO][v == -1 ? 2 + (u + 2) : 7 + (u + 2)][j];
+                        else weight = W[v == 1 ? wO1 : wO2][v == 1 ? 2 + (-u + 2) : 7 + (-u + 2)][j + u];
+                    }
+                    sum = sum + (weight * kernel5[i][jj]) * ctmp;
+                    cum_w += weight * kernel5[i][jj];
+                }
+            }
+            const v3 dn = sum / cum_w;
+            const v3 clp = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),
+                              __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));
+            const size_t bself = (size_t)(O - y0) * width + col;
+            v3 m = mk(mix_cur.x, mix_cur.y, mix_cur.z);   // (prefetched a step ago)
+            m = m + inv_idx * (clp - m);   // lerp (helper_math.h:1154-1157)
+            mix[3 * bself] = m.x;
+            mix[3 * bself + 1] = m.y;
+            mix[3 * bself + 2] = m.z;
+            const uint32_t bgr = (uint32_t)(uint8_t)(255.99f * m.z) | ((uint32_t)(uint8_t)(255.99f * m.y) << 8) |
+                                 ((uint32_t)(uint8_t)(255.99f * m.x) << 16);
+            reinterpret_cast<uint32_t*>(out)[bself] = bgr;
+            if (out_host) reinterpret_cast<uint32_t*>(out_host)[bself] = bgr;
+        }
+    }
+}
+
 hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
                               uint8_t* out_host, int width, int height, int row0, int y0, int y1, uint32_t cur_sample_idx,
                               hipStream_t stream) {
     const int w_eff = 16 * (width / 16), h_eff = 16 * (height / 16);
     if (w_eff == 0 || h_eff == 0 || y1 <= y0) return hipSuccess;
     const float inv_idx = 1.f / float(cur_sample_idx);
+#if CPT_DN_TILE
     const int n_tiles = ((w_eff + DN_TX - 1) / DN_TX) * ((y1 - y0 + DN_TY - 1) / DN_TY);
     hipLaunchKernelGGL(k_denoise_mix, dim3((unsigned)n_tiles), dim3(DN_THREADS), 0, stream, accum, normal, depth, mix, out, out_host, width,
                        row0, y0, y1, w_eff, h_eff, inv_idx);
+#else
+    // waves: CPT_DN_WAVES_PER_CU per CU, whole strips (each wave owns one strip's run of rows)
+    static int cus[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (cus[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n;
+    }
+    const int n_strips = (w_eff + DNS_COLS - 1) / DNS_COLS;
+    const int rows = y1 - y0;
+    int per_strip = (cus[dev] * CPT_DN_WAVES_PER_CU + n_strips - 1) / n_strips;
+    per_strip = per_strip < 1 ? 1 : (per_strip > rows ? rows : per_strip);
+    const int waves = n_strips * per_strip;
+    hipLaunchKernelGGL(k_denoise_strip, dim3((unsigned)((waves + DNS_WAVES - 1) / DNS_WAVES)), dim3(DNS_LANES * DNS_WAVES), 0, stream,
+                       accum, normal, depth, mix, out, out_host, width, row0, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
+#endif
     return hipGetLastError();
 }
 

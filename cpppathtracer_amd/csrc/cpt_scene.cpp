@@ -52,6 +52,27 @@ int material_slot(cpt_ctx* c, const cpt_material& m) {
     return (int)c->mats_h.size() - 1;
 }
 
+// Drops the material slots no object references any more and renumbers the rest (order kept).
+// Leaves carry their slot in `code`, so the caller re-linearises and uploads the scene after it.
+static void compact_materials(cpt_ctx* c) {
+    std::vector<int> remap(c->mats_h.size(), -1);
+    for (int m : c->mat_of_obj) remap[m] = 0;
+    std::vector<Mat> mats;
+    std::vector<int> have;
+    std::vector<uint64_t> tex;
+    for (size_t i = 0; i < remap.size(); ++i) {
+        if (remap[i] < 0) continue;
+        remap[i] = (int)mats.size();
+        mats.push_back(c->mats_h[i]);
+        have.push_back(c->mat_have_tex[i]);
+        tex.push_back(c->mat_tex[i]);
+    }
+    for (int& m : c->mat_of_obj) m = remap[m];
+    c->mats_h.swap(mats);
+    c->mat_have_tex.swap(have);
+    c->mat_tex.swap(tex);
+}
+
 // Returns the walk tree's root (-1: no bounded primitive); `unbounded` = its platform leaves
 // by reference rank; `rank` = the reference rank of every walk-tree leaf.
 static int build_walk_tree(const cpt_ctx* c, HostBvh& w, std::vector<int>& unbounded, std::vector<int>& rank);
@@ -339,6 +360,21 @@ static int update_objects(cpt_ctx* c, int n, const int* indices, const cpt_objec
             ni = nd.parent;
         }
     }
+    // The device refit appends a slot per new material and never frees one, so a scene that edits
+    // a material every frame would grow the table (and its per-batch dedup scan and upload)
+    // without bound.  Once the table holds more than twice the slots the objects reference (+ 16),
+    // the unreferenced ones are dropped and the scene is re-linearised with the new numbering (a
+    // rebuild, amortised over the batches that grew the table).
+    if (c->mats_h.size() > n_mats) {
+        std::vector<char> used(c->mats_h.size(), 0);
+        size_t n_used = 0;
+        for (int m : c->mat_of_obj)
+            if (!used[m]) { used[m] = 1; ++n_used; }
+        if (c->mats_h.size() > 2 * n_used + 16) {
+            compact_materials(c);
+            rebuild = true;
+        }
+    }
     int rc;
     if (rebuild) {
         // the reference tree keeps its topology (refit above); the walk tree is rebuilt from the
@@ -358,6 +394,12 @@ int cpt_update_objects(cpt_ctx* c, int n, const int* indices, const cpt_object* 
 
 int cpt_update_objects_rebuild(cpt_ctx* c, int n, const int* indices, const cpt_object* objs) {
     return update_objects(c, n, indices, objs, true);
+}
+
+int cpt_get_material_count(cpt_ctx* c, int* n) {
+    if (!c || !n) return CPT_ERR_INVALID_ARG;
+    *n = (int)c->mats_h.size();
+    return CPT_OK;
 }
 
 int cpt_last_update_ms(cpt_ctx* c, float* ms) {

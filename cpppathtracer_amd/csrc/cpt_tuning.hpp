@@ -60,6 +60,12 @@ namespace cpt {
 #ifndef CPT_TAKE_BATCH_CONS
 #define CPT_TAKE_BATCH_CONS 0
 #endif
+// Long chains: the leader reads the pixel counter before sizing a draw, so the tail rule (draw
+// only what is needed once less than one id per lane of the grid is left) sees the counter's
+// current value rather than the wave's last draw (advisor r04; A/B in DESIGN.md).
+#ifndef CPT_TAKE_FRESH
+#define CPT_TAKE_FRESH 1
+#endif
 
 constexpr int SUSPEND_AT = CPT_SUSPEND_AT;
 constexpr int SUSPEND_MIN_DONE = CPT_SUSPEND_MIN_DONE;

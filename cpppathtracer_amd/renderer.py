@@ -92,6 +92,12 @@ class Renderer:
         fn = self._L.cpt_update_objects_rebuild if rebuild else self._L.cpt_update_objects
         self._check(fn(self._ctx, int(idx.size), _p(idx), _p(o)))
 
+    def material_count(self) -> int:
+        """Material slots the scene holds (cpt_get_material_count)."""
+        n = ctypes.c_int(0)
+        self._check(self._L.cpt_get_material_count(self._ctx, ctypes.byref(n)))
+        return n.value
+
     def last_update_ms(self) -> float:
         ms = ctypes.c_float(0)
         self._check(self._L.cpt_last_update_ms(self._ctx, ctypes.byref(ms)))

@@ -205,6 +205,10 @@ int cpt_update_objects(cpt_ctx* ctx, int n, const int* indices, const cpt_object
  * and all orders re-linearised and uploaded (the reference order is refit either way): restores
  * the walk tree's quality after large motions.  Same images. */
 int cpt_update_objects_rebuild(cpt_ctx* ctx, int n, const int* indices, const cpt_object* objs);
+/* Material slots the scene holds (deduplicated per value, cpt_set_scene; a device refit that
+ * gives objects new materials appends slots, and once more than twice the referenced ones
+ * (+ 16) are held, the unreferenced slots are dropped with a rebuild). */
+int cpt_get_material_count(cpt_ctx* ctx, int* n);
 /* Host wall time of the last cpt_update_objects[_rebuild] call, ms. */
 int cpt_last_update_ms(cpt_ctx* ctx, float* ms);
 /* Exports the BVH in the reference's node order (Divide creation order): per node

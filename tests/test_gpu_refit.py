@@ -130,6 +130,37 @@ def test_device_refit_new_materials(gpu, oracle_mod, sky, path):
     _render_edited(gpu, oracle_mod, sky, objs, more, 48, 32, 2, 8, path, rebuild=False, batch=False)
 
 
+def test_device_refit_material_table_bounded(gpu, oracle_mod, sky):
+    """Advisor r04: an object whose material changes every frame (a device refit per frame) must
+    not grow the material table without bound -- unreferenced slots are dropped with a rebuild
+    once the table holds more than 2x the referenced slots + 16 -- and the image after 100 such
+    frames is still the oracle's."""
+    objs = scenes.scene_s1000(n=120)
+    W, H = 48, 32
+    cam = camera_get_copy(scenes.camera_for(W, H))
+    gpu.set_scene(objs)
+    gpu.set_env(sky)
+    gpu.set_frame(W, H)
+    n0 = gpu.material_count()
+    i = int(np.flatnonzero(objs["type"] == 0)[3])
+    cur = objs.copy()
+    peak = 0
+    for f in range(100):
+        o = cur[i].copy()
+        o["material"] = _new_material(objs[i]["material"], 100 + f)
+        cur[i] = o
+        gpu.update_objects([i], o.reshape(1))
+        peak = max(peak, gpu.material_count())
+    assert peak <= 2 * (n0 + 1) + 17, (n0, peak)
+    gpu.init_rng(3)
+    gpu.render(cam, 2, 8, ordered=True, sync=True)
+    rows = np.arange(H, dtype=np.int32)
+    orng = oracle_mod.init_rng(3, W, rows, threads=8)
+    # (only the material changed: the refit tree's boxes are the original ones)
+    oacc, _ = oracle_mod.render_edited(objs, [(i, cur[i])], cam, sky, rows, 2, 8, orng, threads=8, walk_rebuild=False)
+    np.testing.assert_array_equal(gpu.read_accum().view(np.uint32), oacc.view(np.uint32))
+
+
 @pytest.mark.parametrize("path", ["megakernel:ordered", "megakernel", "megakernel:plain"])
 def test_device_refit_platform_height(gpu, oracle_mod, sky, path):
     """A platform that stays a platform with a new y_pos (and a new material): its copies at the
