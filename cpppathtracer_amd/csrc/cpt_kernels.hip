@@ -809,23 +809,25 @@ __device__ __noinline__ float dn_weight_slow(float dist2) {
 
 
 // The weight's short form (round 5): the same float, from a double approximation E' of
-// exp(-dist2/pi) that is within 2^-46.8 (relative) of the oracle's double E, rounded to float
+// exp(-dist2/pi) that is within 2^-46.3 (relative) of the oracle's double E, rounded to float
 // only where that cannot matter:
-//  * E' = 2^-(n>>8) * T[n & 255] * P(r):  z = dist2 * 256/(pi ln2) (KN_HI + KN_LO), n = round(z)
+//  * E' = 2^-(n>>5) * T[n & 31] * P(r):  z = dist2 * 32/(pi ln2) (KN_HI + KN_LO), n = round(z)
 //    by the 1.5*2^52 shifter (n is t's low word), r = z - n in [-1/2, 1/2] (one fma against the
-//    exact product dist2 * KN_HI, then the low part), T[j] = 2^(-j/256) correctly rounded from the
-//    LDS table, P = the degree-4 Taylor polynomial of 2^(-r/256) (truncation 2^-54.6), and the
-//    2^-(n>>8) applied to T's exponent field (T >= 1/2 and n>>8 <= 151: stays normal).  E' is
-//    within ~2^-51 of exp(-dist2/pi); the oracle's E = dm_exp(RN(-dist2/pi)) is within 2^-47 (the
-//    quotient's rounding, |x| < 105.05) + 2^-52 of it.
-//  * Guard: if E'(1 - 2^-44) and E'(1 + 2^-44) round to the same float, every double in between
-//    does, E included (rounding is monotone), so that float is the oracle's.  Otherwise (about 2
-//    in 10^6 weights, and NaN) the slow form decides.  dist2 = 0 and dist2 >= 330 keep their
-//    shortcuts.
+//    exact product dist2 * KN_HI, then the low part), T[j] = 2^(-j/32) correctly rounded from the
+//    LDS table (cpt_dn_exp.hpp: 256 B, one bank pair per entry, so a wave's table read never
+//    conflicts), P = the degree-5 Taylor polynomial of 2^(-r/32) (truncation < 2^-48.7), and
+//    the 2^-(n>>5) applied to T's exponent field (T >= 1/2 and n>>5 <= 151: stays normal).  E'
+//    is within ~2^-48.5 of exp(-dist2/pi); the oracle's E = dm_exp(RN(-dist2/pi)) is within 2^-47
+//    (the quotient's rounding, |x| < 105.05) + 2^-52 of it.
+//  * Guard (dn_near_midpoint): if no float rounding boundary lies within 2^-44 E' of E' (its
+//    bits below float precision are not within 2^9 of the half-way pattern), every double in
+//    between rounds alike, E included (rounding is monotone), so (float)E' is the oracle's float.
+//    Otherwise (about 1 in 10^6 weights; also subnormal float results and NaN) the slow form
+//    decides.  dist2 = 0 and dist2 >= 330 keep their shortcuts.
 // tests/test_exact_identities.py restates it on the host against the oracle for every float in
 // [0, 2341]; test_gpu_parity.py::test_dn_weight_exhaustive runs this device code against
 // dn_weight_slow for all 2^31 non-negative float patterns.
-__device__ const double g_dn_exp_table[256] = CPT_DN_EXP_TABLE_INIT;
+__device__ const double g_dn_exp_table[DN_EXP_N] = CPT_DN_EXP_TABLE_INIT;
 
 __device__ __forceinline__ double dn_exp_short(float dist2, const double* __restrict__ tab) {
     constexpr double SHIFT = 0x1.8p52;
@@ -835,13 +837,26 @@ __device__ __forceinline__ double dn_exp_short(float dist2, const double* __rest
     const uint32_t n = (uint32_t)__double2loint(t);
     double r = __builtin_fma(a, DN_KN_HI, -nd);
     r = __builtin_fma(a, DN_KN_LO, r);
-    double p = __builtin_fma(r, DN_C4, DN_C3);
+    double p = __builtin_fma(r, DN_C5, DN_C4);
+    p = __builtin_fma(r, p, DN_C3);
     p = __builtin_fma(r, p, DN_C2);
     p = __builtin_fma(r, p, DN_C1);
     p = __builtin_fma(r, p, 1.0);
-    const double T = tab[n & 255u];
-    const double Ts = __hiloint2double(__double2hiint(T) - (int)((n >> 8) << 20), __double2loint(T));
+    const double T = tab[n & (uint32_t)(DN_EXP_N - 1)];
+    const double Ts = __hiloint2double(__double2hiint(T) - (int)((n >> DN_EXP_SHIFT) << 20), __double2loint(T));
     return Ts * p;
+}
+
+// The guard on the bits of e: for e in [2^-126, 1] (a normal float result) rounding to float looks
+// at the 29 mantissa bits below float precision, all in e's low word; e rounds like every double
+// within 2^-44 e of it unless those bits lie within 2^9 (> 2^-44 / 2^-52 = 2^8 double ulps, with
+// margin) of the half-way pattern 2^28.  Smaller e (a subnormal float result, dist2 > 274.5),
+// larger e, NaN and inf are sent to the slow form, whose dist2 >= 330 shortcut the caller applies.
+__device__ __forceinline__ bool dn_near_midpoint(double e) {
+    const uint32_t lo = (uint32_t)__double2loint(e), hi = (uint32_t)__double2hiint(e);
+    const int d = (int)(lo & 0x1fffffffu) - (1 << 28);
+    const bool normal_f = hi >= 0x38100000u && hi <= 0x3ff00000u;   // 2^-126 <= e <= 1 (e > 0 here)
+    return !normal_f || (d < 512 && d > -512);
 }
 
 __device__ __forceinline__ float dn_weight(float dist2, const double* __restrict__ tab) {
@@ -849,9 +864,8 @@ __device__ __forceinline__ float dn_weight(float dist2, const double* __restrict
     return dn_weight_slow(dist2);
 #endif
     const double e = dn_exp_short(dist2, tab);
-    const float f_lo = (float)(e * (1.0 - 0x1p-44)), f_hi = (float)(e * (1.0 + 0x1p-44));
-    float f = f_hi;
-    if (f_lo != f_hi && !(dist2 >= 330.0f)) f = dn_weight_slow(dist2);   // near a midpoint, or NaN
+    float f = (float)e;
+    if (dn_near_midpoint(e) && !(dist2 >= 330.0f)) f = dn_weight_slow(dist2);   // near a midpoint, or NaN
     f = dist2 >= 330.0f ? 0.0f : f;
     return dist2 == 0.0f ? 1.0f : f;
 }
@@ -868,7 +882,7 @@ __global__ void k_selftest_dn_weight(int which, uint64_t n, unsigned long long* 
             flag = __float_as_uint(w) != __float_as_uint(w_ref);
         } else {
             const double e = dn_exp_short(d, g_dn_exp_table);
-            flag = (float)(e * (1.0 - 0x1p-44)) != (float)(e * (1.0 + 0x1p-44)) && !(d >= 330.0f);
+            flag = dn_near_midpoint(e) && !(d >= 330.0f);
         }
         if (flag) {
             unsigned long long k = atomicAdd(&out[0], 1ull);
@@ -948,7 +962,7 @@ __global__ void __launch_bounds__(DN_THREADS, CPT_DN_MINWAVES) k_denoise_mix(con
                                                            float inv_idx) {
     __shared__ DnPix s_pix[DN_BY * DN_BX];
     __shared__ float s_wb[DN_THREADS * 12];   // backward weight k of tile pixel (ty, tx): w(p - d_k, p)
-    __shared__ double s_tab[256];             // dn_weight's 2^(-j/256) table
+    __shared__ double s_tab[DN_EXP_N];        // dn_weight's 2^(-j/32) table
     // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs (each with its own
     // L2; MI355X_MICROARCH.md §Workgroup dispatch), so block b runs on the XCD of b mod 8.  Each
     // XCD takes one contiguous run of tiles in column-major order, so consecutive tiles on an
@@ -963,7 +977,7 @@ __global__ void __launch_bounds__(DN_THREADS, CPT_DN_MINWAVES) k_denoise_mix(con
     const int tw = min(DN_TX, w_eff - x0), th = min(DN_TY, y1 - ty0);   // the tile's extent
     const int limit = w_eff * h_eff;
     // ---- stage the box: linear pixels (ty0 - 2 + by) * W' + x0 - 2 + bx ----------------
-    for (int i = threadIdx.x; i < 256; i += DN_THREADS) s_tab[i] = g_dn_exp_table[i];
+    for (int i = threadIdx.x; i < DN_EXP_N; i += DN_THREADS) s_tab[i] = g_dn_exp_table[i];
 #pragma unroll 1
     for (int i = threadIdx.x; i < DN_BY * DN_BX; i += DN_THREADS) {
         const int by = i / DN_BX, bx = i - by * DN_BX;
@@ -1116,6 +1130,9 @@ __global__ void __launch_bounds__(DN_THREADS, CPT_DN_MINWAVES) k_denoise_mix(con
 // its LDS operations complete in order; wave_fence keeps the compiler from reordering them).
 constexpr int DNS_LANES = 64, DNS_COLS = 60, DNS_WAVES = 4;
 struct DnsPix { float4 rgbv; float4 nd; };   // (r, g, b, valid), (nx, ny, nz, depth)
+// The ring is two SoA arrays of float4 (16-B lane stride): a wave's ds_read_b128 at consecutive
+// lanes then covers all 64 banks once per 16-lane group (MI355X_MICROARCH.md §LDS), where the
+// 32-B pixel struct put two lanes of a group on the same banks (57% of LDS cycles were conflicts).
 
 __device__ __forceinline__ void wave_fence() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1130,14 +1147,20 @@ __device__ __forceinline__ void dn_weights(const float d2[N], float w[N], const 
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const double e = dn_exp_short(d2[i], tab);
-        const float f_lo = (float)(e * (1.0 - 0x1p-44)), f_hi = (float)(e * (1.0 + 0x1p-44));
-        w[i] = f_hi;
-        slow |= (f_lo != f_hi && !(d2[i] >= 330.0f)) ? 1u << i : 0u;
+        w[i] = (float)e;
+        slow |= dn_near_midpoint(e) && !(d2[i] >= 330.0f) ? 1u << i : 0u;
     }
-    if (__builtin_expect(slow != 0, 0)) {
+    // the fallback, one call site per batch: each trip serves every lane's lowest pending weight
+    while (__builtin_expect(__builtin_amdgcn_ballot_w64(slow != 0) != 0, 0)) {
+        const int k = slow ? __builtin_ctz(slow) : -1;
+        float x = 0.0f;
 #pragma unroll
-        for (int i = 0; i < N; ++i)
-            if ((slow >> i) & 1u) w[i] = dn_weight_slow(d2[i]);
+        for (int i = 0; i < N; ++i) x = k == i ? d2[i] : x;
+        float r = 0.0f;
+        if (k >= 0) r = dn_weight_slow(x);
+#pragma unroll
+        for (int i = 0; i < N; ++i) w[i] = k == i ? r : w[i];
+        slow &= slow - 1u;
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) {
@@ -1178,10 +1201,11 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
     const float4* __restrict__ accum, const float* __restrict__ normal, const float* __restrict__ depth,
     float* __restrict__ mix, uint8_t* __restrict__ out, uint8_t* __restrict__ out_host, int width, int row0, int y0,
     int y1, int w_eff, int h_eff, int n_strips, int per_strip, float inv_idx) {
-    __shared__ double s_tab[256];
-    __shared__ DnsPix s_ring[DNS_WAVES][5][DNS_LANES];
+    __shared__ double s_tab[DN_EXP_N];
+    __shared__ float4 s_rgbv[DNS_WAVES][5][DNS_LANES];
+    __shared__ float4 s_nd[DNS_WAVES][5][DNS_LANES];
     __shared__ float s_w[DNS_WAVES][3][12][DNS_LANES];
-    for (int i = threadIdx.x; i < 256; i += DNS_LANES * DNS_WAVES) s_tab[i] = g_dn_exp_table[i];
+    for (int i = threadIdx.x; i < DN_EXP_N; i += DNS_LANES * DNS_WAVES) s_tab[i] = g_dn_exp_table[i];
     __syncthreads();
     const int wv = (int)(threadIdx.x >> 6), j = (int)(threadIdx.x & 63);
     const int wid = (int)blockIdx.x * DNS_WAVES + wv;
@@ -1194,7 +1218,9 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
     const int col = c0 - 2 + j;                     // this lane's column of the linear run (may be < 0 or >= W')
     const int limit = w_eff * h_eff;
     const bool out_lane = j >= 2 && j < 2 + DNS_COLS && col < w_eff;
-    DnsPix (*ring)[DNS_LANES] = s_ring[wv];
+    float4 (*rgbv)[DNS_LANES] = s_rgbv[wv];
+    float4 (*ndr)[DNS_LANES] = s_nd[wv];
+    auto ring = [&](int slot, int lane) { return DnsPix{rgbv[slot][lane], ndr[slot][lane]}; };
     float (*W)[12][DNS_LANES] = s_w[wv];
     // (lane indices of partners, clamped into the wave: edge lanes compute pairs nobody reads)
     auto cl = [](int l) { return l < 0 ? 0 : (l > 63 ? 63 : l); };
@@ -1236,7 +1262,8 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
             me.nd = make_float4(nn.x, nn.y, nn.z, nd);
         }
         const int slot = (Y + 10) % 5;
-        ring[slot][j] = me;
+        rgbv[slot][j] = me.rgbv;
+        ndr[slot][j] = me.nd;
         if (Y + 1 < rb + 2) load(Y + 1, na, nn, nd, nvalid);
         const int O = Y - 2;                     // the output row this step completes
         float3 mix_cur = mix_next;
@@ -1253,17 +1280,17 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
             float w12[12];
             {
                 DnsPix a[6];
-                a[0] = ring[slot][cl(j + 1)];
-                a[1] = ring[slot][cl(j + 2)];
+                a[0] = ring(slot, cl(j + 1));
+                a[1] = ring(slot, cl(j + 2));
 #pragma unroll
-                for (int dx = -2; dx <= 1; ++dx) a[2 + dx + 2] = ring[s1][cl(j + dx)];
+                for (int dx = -2; dx <= 1; ++dx) a[2 + dx + 2] = ring(s1, cl(j + dx));
                 dn_pair_weights<6>(a, me, w12, s_tab);   // k = 0, 1 (dy 0), 2..5 (dy 1, dx -2..1)
             }
             {
                 DnsPix a[6];
-                a[0] = ring[s1][cl(j + 2)];
+                a[0] = ring(s1, cl(j + 2));
 #pragma unroll
-                for (int dx = -2; dx <= 2; ++dx) a[1 + dx + 2] = ring[s2][cl(j + dx)];
+                for (int dx = -2; dx <= 2; ++dx) a[1 + dx + 2] = ring(s2, cl(j + dx));
                 dn_pair_weights<6>(a, me, w12 + 6, s_tab);   // k = 6 (dy 1, dx 2), 7..11 (dy 2)
             }
             // forward index k of the pair (Y - dy, j + dx) -> (Y, j): here the later pixel is
@@ -1277,7 +1304,7 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
         // ---- output row O: the 25 taps in the reference's order (i = dx outer, j = dy inner) -------
         if (O >= ra && O < rb && out_lane) {
             const int wO = (O + 9) % 3, wO1 = (O + 10) % 3, wO2 = (O + 11) % 3;
-            const DnsPix p = ring[(O + 10) % 5][j];
+            const DnsPix p = ring((O + 10) % 5, j);
             const bool finite = __builtin_isfinite(p.rgbv.x) && __builtin_isfinite(p.rgbv.y) &&
                                 __builtin_isfinite(p.rgbv.z) && __builtin_isfinite(p.nd.x) &&
                                 __builtin_isfinite(p.nd.y) && __builtin_isfinite(p.nd.z) && __builtin_isfinite(p.nd.w);
@@ -1294,14 +1321,14 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
 #pragma unroll
                 for (int jj = 0; jj < 5; ++jj) {
                     const int u = i - 2, v = jj - 2;
-                    const DnsPix q = ring[(O + v + 10) % 5][j + u];
+                    const float4 q = rgbv[(O + v + 10) % 5][j + u];
                     float weight;
                     v3 ctmp;
-                    if (q.rgbv.w == 0.f) {
+                    if (q.w == 0.f) {
                         weight = 0.f * 0.f * 0.f;
                         ctmp = mk1(0.f);
                     } else {
-                        ctmp = mk(q.rgbv.x, q.rgbv.y, q.rgbv.z);
+                        ctmp = mk(q.x, q.y, q.z);
                         // where the pair (O, j) - (O + v, j + u) was stored: same row -- by the lane
                         // of its left pixel at step O, as that pixel's forward pair |u| - 1; other
                         // rows -- by the lane of its lower pixel at that pixel's step, at index

@@ -88,7 +88,7 @@ def test_exact_identities(tmp_path):
 # stored to float (oracle or_exp = dm_exp, path_tracer.cu:224,228,231), for every float d2 in
 # [0, 2341] and the special values: the round-4 branch-free form (cpt_kernels.hip dn_weight_slow:
 # the quotient, dm_exp's steps with a plain ldexp below x = -105.05, the shortcuts 0 -> 1,
-# >= 330 -> 0), and the round-5 short form (dn_weight: the 2^(-j/256) table exp of
+# >= 330 -> 0), and the round-5 short form (dn_weight: the 2^(-j/32) table exp of
 # cpt_dn_exp.hpp and the rounding guard that falls back to the slow form).  The harness calls the
 # oracle library (test infrastructure).
 DN_SRC = r"""
@@ -123,7 +123,7 @@ static float fast_w(float d2) {   /* cpt_kernels.hip dn_weight, operation for op
     f = d2 >= 330.0f ? 0.0f : f;
     return d2 == 0.0f ? 1.0f : f;
 }
-static const double DN_TAB[256] = CPT_DN_EXP_TABLE_INIT;
+static const double DN_TAB[cpt::DN_EXP_N] = CPT_DN_EXP_TABLE_INIT;
 static int g_guard_fallbacks[8];
 static float short_w(float d2, int t) {   /* cpt_kernels.hip dn_exp_short + dn_weight */
     const double SHIFT = 0x1.8p52, a = (double)d2;
@@ -132,19 +132,24 @@ static float short_w(float d2, int t) {   /* cpt_kernels.hip dn_exp_short + dn_w
     const uint32_t n = (uint32_t)tb;
     double r = fma(a, cpt::DN_KN_HI, -nd);
     r = fma(a, cpt::DN_KN_LO, r);
-    double p = fma(r, cpt::DN_C4, cpt::DN_C3);
+    double p = fma(r, cpt::DN_C5, cpt::DN_C4);
+    p = fma(r, p, cpt::DN_C3);
     p = fma(r, p, cpt::DN_C2);
     p = fma(r, p, cpt::DN_C1);
     p = fma(r, p, 1.0);
-    double T = DN_TAB[n & 255u];
+    double T = DN_TAB[n & (uint32_t)(cpt::DN_EXP_N - 1)];
     uint64_t Tb; memcpy(&Tb, &T, 8);
-    const uint32_t hi = (uint32_t)(Tb >> 32) - ((n >> 8) << 20);
+    const uint32_t hi = (uint32_t)(Tb >> 32) - ((n >> cpt::DN_EXP_SHIFT) << 20);
     Tb = ((uint64_t)hi << 32) | (Tb & 0xffffffffull);
     memcpy(&T, &Tb, 8);
     const double e = T * p;
-    const float f_lo = (float)(e * (1.0 - 0x1p-44)), f_hi = (float)(e * (1.0 + 0x1p-44));
-    float f = f_hi;
-    if (f_lo != f_hi && !(d2 >= 330.0f)) { f = fast_w(d2); if (t >= 0) g_guard_fallbacks[t]++; }
+    uint64_t eb; memcpy(&eb, &e, 8);
+    const uint32_t elo = (uint32_t)eb, ehi = (uint32_t)(eb >> 32);
+    const int dm = (int)(elo & 0x1fffffffu) - (1 << 28);
+    const bool normal_f = ehi >= 0x38100000u && ehi <= 0x3ff00000u;
+    const bool near = !normal_f || (dm < 512 && dm > -512);
+    float f = (float)e;
+    if (near && !(d2 >= 330.0f)) { f = fast_w(d2); if (t >= 0) g_guard_fallbacks[t]++; }
     f = d2 >= 330.0f ? 0.0f : f;
     return d2 == 0.0f ? 1.0f : f;
 }

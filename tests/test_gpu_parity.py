@@ -106,9 +106,11 @@ def test_dn_weight_exhaustive(gpu):
     every NaN.  Also records how rarely the guard falls back (path_tracer.cu:219-233)."""
     cnt, pairs = gpu.selftest_qdiv(6, 1 << 31)
     assert cnt == 0, [float(a) for a, _ in pairs]
-    fallbacks, _ = gpu.selftest_qdiv(7, 0x43A50000)   # [0, 330): the guard's fallbacks
-    nan_free = 0x43A50000
-    assert fallbacks < 1e-5 * nan_free, fallbacks
+    # the guard's fallbacks over [0, 274): the normal-float results (above 274.5 the weight is a
+    # subnormal float and always takes the slow form)
+    lim = int(np.float32(274.0).view(np.uint32))
+    fallbacks, _ = gpu.selftest_qdiv(7, lim)
+    assert fallbacks < 1e-5 * lim, fallbacks
 
 
 # ------------------------------------------------------------------------------- rng
