@@ -68,6 +68,7 @@ void free_frame(cpt_ctx* c) {
     (void)hipFree(c->wf.counts); c->wf.counts = nullptr;
     c->wf_ready = false;
     (void)hipFree(c->d_bgra); c->d_bgra = nullptr;
+    (void)hipFree(c->d_dn_sink); c->d_dn_sink = nullptr;
     c->band_y0 = c->band_y1 = -1;
     (void)hipFree(c->d_scratch_w); c->d_scratch_w = nullptr;
     (void)hipFree(c->d_scratch_m); c->d_scratch_m = nullptr;
@@ -826,8 +827,9 @@ static int denoise_band(cpt_ctx* c, uint32_t cur_sample_idx, int y0, int y1, uin
         else
             (void)hipGetLastError();   // pageable: not an error
     }
+    if (!c->d_dn_sink) HIP_TRY(c, hipMalloc((void**)&c->d_dn_sink, cpt::DN_SINK_SLOTS * sizeof(float4)));
     HIP_TRY(c, hipEventRecord(c->ev_dn0, s));
-    HIP_TRY(c, cpt::launch_denoise_mix(c->d_accum, c->d_normal, c->d_depth, c->d_mix, c->d_bgra, host_alias, c->width,
+    HIP_TRY(c, cpt::launch_denoise_mix(c->d_accum, c->d_normal, c->d_depth, c->d_mix, c->d_bgra, host_alias, c->d_dn_sink, c->width,
                                       c->height, row0, y0, y1, cur_sample_idx, s));
     HIP_TRY(c, hipEventRecord(c->ev_dn1, s));
     c->have_dn_timing = true;

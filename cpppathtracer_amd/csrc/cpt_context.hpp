@@ -107,6 +107,7 @@ struct cpt_ctx {
     bool wf_ready = false;
     float* d_mix = nullptr;      // display running mean (Mix), rgb per pixel of the display band
     uint8_t* d_bgra = nullptr;   // display frame (band rows)
+    float4* d_dn_sink = nullptr; // k_denoise_strip: where lanes without an output pixel store (DN_SINK_SLOTS)
     int band_y0 = -1, band_y1 = -1;   // display band the buffers hold
     float last_kernel_ms = 0.f;
     int last_launches = 0;

@@ -942,6 +942,9 @@ __device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b, 
 #ifndef CPT_DN_TILE          // 1: the round-4 tile kernel (A/B); 0: k_denoise_strip
 #define CPT_DN_TILE 0
 #endif
+#ifndef CPT_DN_PROBE         // DIAGNOSTIC timing probes of k_denoise_strip (wrong images; never shipped)
+#define CPT_DN_PROBE 0
+#endif
 #ifndef CPT_DN_WAVES_PER_CU  // k_denoise_strip's waves per CU (LDS: 19.5 KB per wave)
 #define CPT_DN_WAVES_PER_CU 8
 #endif
@@ -1186,21 +1189,33 @@ __device__ __forceinline__ void dn_pair_weights(const DnsPix a[N], const DnsPix&
         any_p |= p2[i] != 0.0f;
     }
     float cw[N], nw[N], pw[N];
+#if CPT_DN_PROBE == 2   // DIAGNOSTIC timing probe (wrong images): no exps at all
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = c2[i] * n2[i] + p2[i];
+    return;
+#endif
     dn_weights<N>(c2, cw, tab);
     // a zero normal (depth) difference gives exactly 1 (dn_weight(0)); equal normals (the floor)
     // and the constant depth (a18) make whole batches of the wave skip the sequence
 #pragma unroll
     for (int i = 0; i < N; ++i) nw[i] = pw[i] = 1.0f;
+#if CPT_DN_PROBE != 1   // (1: DIAGNOSTIC timing probe without the normal factor's exps)
     if (__builtin_amdgcn_ballot_w64(any_n)) dn_weights<N>(n2, nw, tab);
+#endif
     if (__builtin_amdgcn_ballot_w64(any_p)) dn_weights<N>(p2, pw, tab);
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = cw[i] * nw[i] * pw[i];
 }
 
+// Global memory: every load of a step is issued, unconditionally (out-of-frame lanes read a valid
+// address and discard it), before the step's stores, and the stores sit in a branch-free tail, so
+// the next step's wait for its prefetched row counts only those loads (vmcnt(#stores)) instead of
+// draining the stores (gfx9's one vector-memory counter; a pinned host frame's stores cross PCIe).
+template <bool HOST>
 __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
     const float4* __restrict__ accum, const float* __restrict__ normal, const float* __restrict__ depth,
-    float* __restrict__ mix, uint8_t* __restrict__ out, uint8_t* __restrict__ out_host, int width, int row0, int y0,
-    int y1, int w_eff, int h_eff, int n_strips, int per_strip, float inv_idx) {
+    float* __restrict__ mix, uint8_t* __restrict__ out, uint8_t* __restrict__ out_host, float4* __restrict__ sink,
+    int width, int row0, int y0, int y1, int w_eff, int h_eff, int n_strips, int per_strip, float inv_idx) {
     __shared__ double s_tab[DN_EXP_N];
     __shared__ float4 s_rgbv[DNS_WAVES][5][DNS_LANES];
     __shared__ float4 s_nd[DNS_WAVES][5][DNS_LANES];
@@ -1218,6 +1233,7 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
     const int col = c0 - 2 + j;                     // this lane's column of the linear run (may be < 0 or >= W')
     const int limit = w_eff * h_eff;
     const bool out_lane = j >= 2 && j < 2 + DNS_COLS && col < w_eff;
+    float4* const sink_lane = sink + (((uint32_t)wid & 1023u) * 64u + (uint32_t)j);
     float4 (*rgbv)[DNS_LANES] = s_rgbv[wv];
     float4 (*ndr)[DNS_LANES] = s_nd[wv];
     auto ring = [&](int slot, int lane) { return DnsPix{rgbv[slot][lane], ndr[slot][lane]}; };
@@ -1228,25 +1244,27 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
     auto load = [&](int Y, float4& a, float3& n, float& d, bool& valid) {
         const int L = Y * w_eff + col;
         valid = L >= 0 && L < limit;
-        if (valid) {
-            const int yy = col < 0 ? Y - 1 : (col >= w_eff ? Y + 1 : Y);
-            const int xx = L - yy * w_eff;
-            const size_t px = (size_t)(yy - row0) * width + xx;
-            a = accum[px];
-            n = make_float3(normal[3 * px], normal[3 * px + 1], normal[3 * px + 2]);
-            d = depth[px];
-        } else {
-            a = make_float4(0.f, 0.f, 0.f, 0.f);
-            n = make_float3(0.f, 0.f, 0.f);
-            d = 0.f;
-        }
+        const int yy = col < 0 ? Y - 1 : (col >= w_eff ? Y + 1 : Y);
+        const int xx = L - yy * w_eff;
+        const size_t px = valid ? (size_t)(yy - row0) * width + xx : (size_t)0;   // (a valid address)
+        // raw values: an out-of-frame lane's are replaced by zeros where they are used (a select
+        // here would make the compiler wait for the loads at once)
+#if CPT_DN_PROBE == 4   // DIAGNOSTIC timing probe: no global loads (synthetic pixels)
+        a = make_float4((float)(L & 7), (float)(L & 3), 0.5f, 1.0f);
+        n = make_float3(0.f, (float)(L & 1), 0.f);
+        d = 1e30f;
+        (void)px;
+#else
+        a = accum[px];
+        n = make_float3(normal[3 * px], normal[3 * px + 1], normal[3 * px + 2]);
+        d = depth[px];
+#endif
     };
     float4 na;
     float3 nn;
     float nd;
     bool nvalid;
     load(ra - 2, na, nn, nd, nvalid);
-    float3 mix_next = make_float3(0.f, 0.f, 0.f);
     constexpr float kernel5[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
                                      {4.f, 16.f, 26.f, 16.f, 4.f},
                                      {7.f, 26.f, 41.f, 26.f, 7.f},
@@ -1254,23 +1272,32 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
                                      {1.f, 4.f, 7.f, 4.f, 1.f}};
 #pragma unroll 1
     for (int Y = ra - 2; Y < rb + 2; ++Y) {
-        // ---- row Y into the ring; prefetch row Y + 1 and the mix of the next output row --------
+        const int O = Y - 2;                     // the output row this step completes
+        // ---- the mix of row O (used at the step's end), row Y into the ring, row Y + 1 ahead ----
+        // (issued in this order so that each wait names only the loads it needs: the mix is
+        // waited for behind the row loads issued after it, the row behind the step's stores)
+        float3 mix_cur;
+        {
+            const int orow = min(max(O, ra), rb - 1);
+            const int ocol = min(max(col, 0), w_eff - 1);
+            const size_t b = (size_t)(orow - y0) * width + ocol;
+#if CPT_DN_PROBE == 4
+            mix_cur = make_float3(0.25f, 0.5f, (float)(b & 1));
+#else
+            mix_cur = make_float3(mix[3 * b], mix[3 * b + 1], mix[3 * b + 2]);
+#endif
+        }
         DnsPix me;
         {
-            const v3 c = na.w != 0.f ? mk(na.x, na.y, na.z) / na.w : mk(na.x, na.y, na.z);
+            const float4 a = nvalid ? na : make_float4(0.f, 0.f, 0.f, 0.f);
+            const v3 c = a.w != 0.f ? mk(a.x, a.y, a.z) / a.w : mk(a.x, a.y, a.z);
             me.rgbv = make_float4(c.x, c.y, c.z, nvalid ? 1.f : 0.f);
-            me.nd = make_float4(nn.x, nn.y, nn.z, nd);
+            me.nd = nvalid ? make_float4(nn.x, nn.y, nn.z, nd) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
         const int slot = (Y + 10) % 5;
         rgbv[slot][j] = me.rgbv;
         ndr[slot][j] = me.nd;
-        if (Y + 1 < rb + 2) load(Y + 1, na, nn, nd, nvalid);
-        const int O = Y - 2;                     // the output row this step completes
-        float3 mix_cur = mix_next;
-        if (O + 1 >= ra && O + 1 < rb && out_lane) {
-            const size_t b = (size_t)(O + 1 - y0) * width + col;
-            mix_next = make_float3(mix[3 * b], mix[3 * b + 1], mix[3 * b + 2]);
-        }
+        load(Y + 1, na, nn, nd, nvalid);        // (past rb + 1: read and never used)
         wave_fence();
         // ---- the 12 pair weights whose later pixel is (Y, j) -----------------------------------
         // needed for output rows Y - 2 .. Y only while Y >= ra; the last two steps need only the
@@ -1302,9 +1329,15 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
         }
         wave_fence();
         // ---- output row O: the 25 taps in the reference's order (i = dx outer, j = dy inner) -------
-        if (O >= ra && O < rb && out_lane) {
+        // the step's stores, issued on every step by every lane (branch-free, see above): lanes
+        // and steps without an output pixel store to the sink
+        v3 st_m = mk1(0.f);
+        uint32_t st_bgr = 0;
+        bool st_real = false;
+        if (O >= ra && O < rb) {                 // (wave-uniform; every lane computes, out_lane stores)
             const int wO = (O + 9) % 3, wO1 = (O + 10) % 3, wO2 = (O + 11) % 3;
-            const DnsPix p = ring((O + 10) % 5, j);
+            const int jc = min(max(j, 2), 61);    // edge lanes: a clamped (discarded) tap window
+            const DnsPix p = ring((O + 10) % 5, jc);
             const bool finite = __builtin_isfinite(p.rgbv.x) && __builtin_isfinite(p.rgbv.y) &&
                                 __builtin_isfinite(p.rgbv.z) && __builtin_isfinite(p.nd.x) &&
                                 __builtin_isfinite(p.nd.y) && __builtin_isfinite(p.nd.z) && __builtin_isfinite(p.nd.w);
@@ -1321,7 +1354,7 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
 #pragma unroll
                 for (int jj = 0; jj < 5; ++jj) {
                     const int u = i - 2, v = jj - 2;
-                    const float4 q = rgbv[(O + v + 10) % 5][j + u];
+                    const float4 q = rgbv[(O + v + 10) % 5][jc + u];
                     float weight;
                     v3 ctmp;
                     if (q.w == 0.f) {
@@ -1334,10 +1367,10 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
                         // rows -- by the lane of its lower pixel at that pixel's step, at index
                         // 2 + dx + 2 (dy 1) or 7 + dx + 2 (dy 2), dx = upper column - lower column
                         if (u == 0 && v == 0) weight = w_self;
-                        else if (v == 0 && u > 0) weight = W[wO][u - 1][j];
-                        else if (v == 0) weight = W[wO][-u - 1][j + u];
-                        else if (v < 0) weight = W[wO][v == -1 ? 2 + (u + 2) : 7 + (u + 2)][j];
-                        else weight = W[v == 1 ? wO1 : wO2][v == 1 ? 2 + (-u + 2) : 7 + (-u + 2)][j + u];
+                        else if (v == 0 && u > 0) weight = W[wO][u - 1][jc];
+                        else if (v == 0) weight = W[wO][-u - 1][jc + u];
+                        else if (v < 0) weight = W[wO][v == -1 ? 2 + (u + 2) : 7 + (u + 2)][jc];
+                        else weight = W[v == 1 ? wO1 : wO2][v == 1 ? 2 + (-u + 2) : 7 + (-u + 2)][jc + u];
                     }
                     sum = sum + (weight * kernel5[i][jj]) * ctmp;
                     cum_w += weight * kernel5[i][jj];
@@ -1346,23 +1379,39 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
             const v3 dn = sum / cum_w;
             const v3 clp = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),
                               __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));
-            const size_t bself = (size_t)(O - y0) * width + col;
-            v3 m = mk(mix_cur.x, mix_cur.y, mix_cur.z);   // (prefetched a step ago)
+            v3 m = mk(mix_cur.x, mix_cur.y, mix_cur.z);
             m = m + inv_idx * (clp - m);   // lerp (helper_math.h:1154-1157)
-            mix[3 * bself] = m.x;
-            mix[3 * bself + 1] = m.y;
-            mix[3 * bself + 2] = m.z;
             const uint32_t bgr = (uint32_t)(uint8_t)(255.99f * m.z) | ((uint32_t)(uint8_t)(255.99f * m.y) << 8) |
                                  ((uint32_t)(uint8_t)(255.99f * m.x) << 16);
-            reinterpret_cast<uint32_t*>(out)[bself] = bgr;
-            if (out_host) reinterpret_cast<uint32_t*>(out_host)[bself] = bgr;
+            st_m = m;
+            st_bgr = bgr;
+            st_real = out_lane;
+        }
+        {
+            const size_t bself = st_real ? (size_t)(O - y0) * width + col : 0;
+            float* const pm = st_real ? mix + 3 * bself : reinterpret_cast<float*>(sink_lane);
+            uint32_t* const po = st_real ? reinterpret_cast<uint32_t*>(out) + bself : reinterpret_cast<uint32_t*>(sink_lane) + 3;
+#if CPT_DN_PROBE == 3   // DIAGNOSTIC timing probe: the stores of all but the last step skipped
+            if (Y == rb + 1) {
+#endif
+            pm[0] = st_m.x;
+            pm[1] = st_m.y;
+            pm[2] = st_m.z;
+            *po = st_bgr;
+#if CPT_DN_PROBE == 3
+            }
+#endif
+            if (HOST) {
+                uint32_t* const ph = st_real ? reinterpret_cast<uint32_t*>(out_host) + bself : reinterpret_cast<uint32_t*>(sink_lane) + 3;
+                *ph = st_bgr;
+            }
         }
     }
 }
 
 hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
-                              uint8_t* out_host, int width, int height, int row0, int y0, int y1, uint32_t cur_sample_idx,
-                              hipStream_t stream) {
+                              uint8_t* out_host, float4* sink, int width, int height, int row0, int y0, int y1,
+                              uint32_t cur_sample_idx, hipStream_t stream) {
     const int w_eff = 16 * (width / 16), h_eff = 16 * (height / 16);
     if (w_eff == 0 || h_eff == 0 || y1 <= y0) return hipSuccess;
     const float inv_idx = 1.f / float(cur_sample_idx);
@@ -1386,8 +1435,14 @@ hipError_t launch_denoise_mix(const float4* accum, const float* normal, const fl
     int per_strip = (cus[dev] * CPT_DN_WAVES_PER_CU + n_strips - 1) / n_strips;
     per_strip = per_strip < 1 ? 1 : (per_strip > rows ? rows : per_strip);
     const int waves = n_strips * per_strip;
-    hipLaunchKernelGGL(k_denoise_strip, dim3((unsigned)((waves + DNS_WAVES - 1) / DNS_WAVES)), dim3(DNS_LANES * DNS_WAVES), 0, stream,
-                       accum, normal, depth, mix, out, out_host, width, row0, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
+    if (out_host)
+        hipLaunchKernelGGL(k_denoise_strip<true>, dim3((unsigned)((waves + DNS_WAVES - 1) / DNS_WAVES)), dim3(DNS_LANES * DNS_WAVES), 0,
+                           stream, accum, normal, depth, mix, out, out_host, sink, width, row0, y0, y1, w_eff, h_eff, n_strips, per_strip,
+                           inv_idx);
+    else
+        hipLaunchKernelGGL(k_denoise_strip<false>, dim3((unsigned)((waves + DNS_WAVES - 1) / DNS_WAVES)), dim3(DNS_LANES * DNS_WAVES), 0,
+                           stream, accum, normal, depth, mix, out, out_host, sink, width, row0, y0, y1, w_eff, h_eff, n_strips, per_strip,
+                           inv_idx);
 #endif
     return hipGetLastError();
 }
