@@ -107,6 +107,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     constexpr bool COUNT = STATS || PROBE;
     constexpr int BLK = mk_block<LDST>();
     __shared__ uint4 s_tree[LDST ? LDS_TREE_NODES * 7 : 1];
+    pooldiag::init();
     if (LDST) {
         const uint4* src = reinterpret_cast<const uint4*>(p.nodes + wide_image_base(p));
         for (int i = threadIdx.x; i < 7 * lds_tree_nodes(p.n_wide); i += BLK) s_tree[i] = src[i];
@@ -293,7 +294,8 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                             seen = __builtin_amdgcn_readfirstlane(__shfl(cur, leader)) + off;
                         }
 #endif
-                        const uint32_t grab = (!CONS || CPT_TAKE_BATCH_CONS) && n_work - seen > n_static && bsz > want ? bsz : want;
+                        const uint32_t bsz_k = CONS ? (uint32_t)CPT_TAKE_BATCH_CONS_SIZE : bsz;
+                        const uint32_t grab = (!CONS || CPT_TAKE_BATCH_CONS) && n_work - seen > n_static && bsz_k > want ? bsz_k : want;
                         if (lane == leader) nb = atomicAdd(p.work, grab);
                         nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader)) + off;
                         ncnt = grab;
@@ -574,6 +576,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         }
     }
     stamps::flush(p.stats + 16);
+    pooldiag::flush(p.stats + 64);
     if (STATS && !PROBE) {
         uint64_t a = wave_sum(cnt.segments), b = wave_sum(cnt.nodes), c = wave_sum(cnt.prims);
         uint64_t d = wave_sum(cnt.hits), e = wave_sum(cnt.misses);

@@ -758,6 +758,9 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
     constexpr int NONE = -1;
     const uint64_t participants = __ballot(1);
     stamps::lap(6);
+#ifdef CPT_POOLDIAG
+    pooldiag::resumed(wave_count(__builtin_amdgcn_ballot_w64(ws.active)));
+#endif
     if (!ws.active) {
         // a new walk: the platforms (every ray tests them) first, by the whole wave at once,
         // so the walk starts with their tmax; same rank rule, so the order does not matter
@@ -855,6 +858,9 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
             // wave-uniform counts as 32-bit SGPR values: SALU compares (the compiler otherwise
             // compares the 64-bit popcount with VALU v_cmp_*_u64)
             const uint32_t n_w = wave_count(w);
+#ifdef CPT_POOLDIAG
+            pooldiag::iteration(wave_count(participants & ~w), n_w);
+#endif
             const bool tail = n_w <= 8u;   // stamps only: the walk's tail (few lanes left)
             stamps::lap(tail ? 11 : 1);
             if (tail) stamps::count(13);
@@ -889,6 +895,9 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
         stamps::lap(2);
     }
     const bool working = parked >= 0 || cur != NONE;
+#ifdef CPT_POOLDIAG
+    pooldiag::suspended(wave_count(__builtin_amdgcn_ballot_w64(working)));
+#endif
     ws.active = working;
     if (working) return 2;   // suspended
     if (best < 0) return 0;

@@ -74,4 +74,62 @@ __device__ __forceinline__ void lanes(unsigned long long* out, int r) {
 __device__ __forceinline__ void lanes(unsigned long long*, int) {}
 #endif
 }  // namespace execdiag
+
+// DIAGNOSTIC supply / demand of a cross-wave walk pool (CPT_POOLDIAG builds only; never the timed
+// library; exclusive with CPT_EXECDIAG, whose counters it reuses): would the lanes of a wave that
+// have finished their walk while others of the wave still walk find a suspended walk of another
+// wave of the workgroup to continue?  A workgroup LDS count of the walks suspended right now
+// (trace_wide returns 2 for them; they resume in their own wave's next round); in every node-visit
+// iteration of the wide walk: idle = lanes of the call whose walk has ended, supply = that count.
+// out[0] iterations, [1] sum idle, [2] sum min(idle, supply), [3] sum working lanes, [4] sum
+// supply, [5] walks suspended, [6] walk calls (per wave).
+namespace pooldiag {
+#ifdef CPT_POOLDIAG
+__device__ __forceinline__ uint32_t* susp() {
+    __shared__ uint32_t s;
+    return &s;
+}
+__device__ __forceinline__ unsigned long long* wave_acc() {
+    __shared__ unsigned long long a[16 * 8];
+    return a + (threadIdx.x >> 6) * 8;
+}
+__device__ __forceinline__ void init() {   // before the block's first barrier
+    if (threadIdx.x == 0) *susp() = 0;
+    if ((threadIdx.x & 63) < 8) wave_acc()[threadIdx.x & 63] = 0;
+}
+__device__ __forceinline__ bool leader() {
+    return (int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1;
+}
+__device__ __forceinline__ void resumed(uint32_t n) {
+    if (n && leader()) atomicSub(susp(), n);
+    if (leader()) wave_acc()[6] += 1;
+}
+__device__ __forceinline__ void suspended(uint32_t n) {
+    if (n && leader()) {
+        atomicAdd(susp(), n);
+        wave_acc()[5] += n;
+    }
+}
+__device__ __forceinline__ void iteration(uint32_t idle, uint32_t working) {
+    if (leader()) {
+        const uint32_t sup = *(volatile uint32_t*)susp();
+        unsigned long long* a = wave_acc();
+        a[0] += 1;
+        a[1] += idle;
+        a[2] += idle < sup ? idle : sup;
+        a[3] += working;
+        a[4] += sup;
+    }
+}
+__device__ __forceinline__ void flush(unsigned long long* out) {   // whole wave active
+    if ((threadIdx.x & 63) < 8) atomicAdd(out + (threadIdx.x & 63), wave_acc()[threadIdx.x & 63]);
+}
+#else
+__device__ __forceinline__ void init() {}
+__device__ __forceinline__ void resumed(uint32_t) {}
+__device__ __forceinline__ void suspended(uint32_t) {}
+__device__ __forceinline__ void iteration(uint32_t, uint32_t) {}
+__device__ __forceinline__ void flush(unsigned long long*) {}
+#endif
+}  // namespace pooldiag
 }  // namespace cpt

@@ -60,6 +60,12 @@ namespace cpt {
 #ifndef CPT_TAKE_BATCH_CONS
 #define CPT_TAKE_BATCH_CONS 0
 #endif
+// The consolidating kernel's range size when CPT_TAKE_BATCH_CONS is set.  Round 5, C5 N = 8
+// rehearsal (slowest rank, two interleaved rounds; exact takes 2542 / 2590 ms): 4 ids 2635 / 2597,
+// 8 ids 2618 / 2582, 16 ids 2682 / 2622 (profiles/r05/reh_cons_take_sizes.log).  Exact stays.
+#ifndef CPT_TAKE_BATCH_CONS_SIZE
+#define CPT_TAKE_BATCH_CONS_SIZE 64
+#endif
 // Long chains: the leader reads the pixel counter before sizing a draw, so the tail rule (draw
 // only what is needed once less than one id per lane of the grid is left) sees the counter's
 // current value rather than the wave's last draw (advisor r04; A/B in DESIGN.md).
