@@ -783,7 +783,7 @@ __global__ void k_rng_pixels(const uint32_t* __restrict__ rowmats, const uint32_
 //    float 0;  NaN: exp(NaN) = NaN, and `w < 1.0 ? w : 1.0` gives 1.
 // tests/test_exact_identities.py checks the whole function against the oracle's expression
 // for every float in [0, 2341] and the special values.
-__device__ __noinline__ float dn_weight_slow(float dist2) {
+__device__ __forceinline__ float dn_weight_slow_inl(float dist2) {
     constexpr double INV_PI = 1.0 / REF_PI;
     const double a = (double)dist2;
     const double q = a * INV_PI;
@@ -809,6 +809,9 @@ __device__ __noinline__ float dn_weight_slow(float dist2) {
     f = dist2 >= 330.0f ? 0.0f : f;
     return dist2 == 0.0f ? 1.0f : f;
 }
+// (out of line where a weight is evaluated alone; inlined in the batched weights, whose kernels
+// would otherwise spill the caller-saved VGPRs live across the call)
+__device__ __noinline__ float dn_weight_slow(float dist2) { return dn_weight_slow_inl(dist2); }
 
 
 // The weight's short form (round 5): the same float, from a double approximation E' of
@@ -942,14 +945,14 @@ __device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b, 
 #ifndef CPT_DN_TY
 #define CPT_DN_TY 8
 #endif
-#ifndef CPT_DN_TILE          // 1: the round-4 tile kernel (A/B); 0: k_denoise_strip
+#ifndef CPT_DN_TILE          // 1: the round-4 tile kernel above (A/B); 0: k_denoise_rows (the default)
 #define CPT_DN_TILE 0
 #endif
-#ifndef CPT_DN_PROBE         // DIAGNOSTIC timing probes of k_denoise_strip (wrong images; never shipped)
-#define CPT_DN_PROBE 0
+#ifndef CPT_DNR_BLOCKS_PER_CU  // k_denoise_rows' blocks per CU (43 KB of LDS each; three waves per SIMD)
+#define CPT_DNR_BLOCKS_PER_CU 3
 #endif
-#ifndef CPT_DN_WAVES_PER_CU  // k_denoise_strip's waves per CU (LDS: 19.5 KB per wave)
-#define CPT_DN_WAVES_PER_CU 8
+#ifndef CPT_DN_BATCH           // pair weights evaluated together (a divisor of 12)
+#define CPT_DN_BATCH 6
 #endif
 constexpr int DN_TX = 64, DN_TY = CPT_DN_TY, DN_THREADS = DN_TX * DN_TY;
 constexpr int DN_BX = DN_TX + 4, DN_BY = DN_TY + 4;   // staged box (2-pixel halo each side)
@@ -1117,33 +1120,24 @@ __global__ void __launch_bounds__(DN_THREADS, CPT_DN_MINWAVES) k_denoise_mix(con
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_denoise_strip (round 5, the default): the same Denoising + Mix, bit for bit, as a per-wave
-// sliding window with no block barrier.  A wave owns a strip of 60 output columns (lanes 2..61;
-// lanes 0, 1, 62, 63 carry the two halo columns each side) and a run of output rows, and walks down
-// it one row per step:
-//  * lane j at row Y holds the pixel of LINEAR index L = Y W' + c0 - 2 + j (the stencil's v W' + u
-//    offsets, path_tracer.cu:205-216: columns past either edge wrap into the adjacent row, exactly as
-//    the reference); row Y enters a 5-row ring in the wave's LDS (radiance, normal, depth, validity);
-//  * at step Y the lane computes the 12 pair weights whose later pixel is its own (Y, j): the two
-//    same-row forward pairs (Y, j+1), (Y, j+2) and the pairs with rows Y-1 and Y-2 at columns
-//    j-2..j+2 -- every unordered pair of the stencil exactly once, as the tile kernel's forward
-//    pairs -- into a 3-step ring of weights in LDS;
-//  * row O = Y - 2 is then complete: each output lane sums its 25 taps in the reference's order,
-//    reading the weights it needs from the ring (its own, or its neighbours' at lane j +- u).
-// The weights are evaluated in batches of 6 with one wave-wide fallback branch (dn_weight's guard),
-// so the six exp chains overlap.  Global reads: one coalesced row of accumulator / normal / depth
-// per step, prefetched a step ahead; no barrier after the table load (one wave never races itself:
-// its LDS operations complete in order; wave_fence keeps the compiler from reordering them).
-constexpr int DNS_LANES = 64, DNS_COLS = 60, DNS_WAVES = 4;
+// k_denoise_rows (round 5, the default): the same Denoising + Mix, bit for bit, as a sliding
+// window down a strip of columns (path_tracer.cu:177-254).
+//  * A block owns a strip of 60 output columns (lanes 2..61 of each wave; lanes 0, 1, 62, 63 carry
+//    the two halo columns each side) and a run of output rows.  Lane j of row Y holds the pixel of
+//    LINEAR index L = Y W' + c0 - 2 + j: the stencil's v W' + u offsets (path_tracer.cu:205-216),
+//    so columns past either edge wrap into the adjacent row exactly as the reference's do.
+//  * When row R enters, the 12 pair weights whose later pixel is (R, j) are computed: the two
+//    same-row pairs (R, j+1), (R, j+2) and the pairs with rows R-1 and R-2 at columns j-2..j+2 --
+//    every unordered pair of the stencil exactly once -- into a ring of weights in LDS.
+//  * Row O = R - 2 is then complete: each output lane sums its 25 taps in the reference's order,
+//    reading the weights it needs from the ring (its own, or a neighbour's at lane j +- u).
+// The weights are evaluated in batches of CPT_DN_BATCH with one wave-wide fallback branch
+// (dn_weight's guard), so the batch's exp chains overlap.
+constexpr int DNS_LANES = 64, DNS_COLS = 60;
 struct DnsPix { float4 rgbv; float4 nd; };   // (r, g, b, valid), (nx, ny, nz, depth)
 // The ring is two SoA arrays of float4 (16-B lane stride): a wave's ds_read_b128 at consecutive
 // lanes then covers all 64 banks once per 16-lane group (MI355X_MICROARCH.md §LDS), where the
 // 32-B pixel struct put two lanes of a group on the same banks (57% of LDS cycles were conflicts).
-
-__device__ __forceinline__ void wave_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
 
 // Pair weights c_w * n_w * p_w of N pairs (path_tracer.cu:219-233; dn_pair_weight's factors, in
 // the same order), batched: N short exps in flight, and the guard's rare fallback as one branch.
@@ -1163,7 +1157,7 @@ __device__ __forceinline__ void dn_weights(const float d2[N], float w[N], const 
 #pragma unroll
         for (int i = 0; i < N; ++i) x = k == i ? d2[i] : x;
         float r = 0.0f;
-        if (k >= 0) r = dn_weight_slow(x);
+        if (k >= 0) r = dn_weight_slow_inl(x);
 #pragma unroll
         for (int i = 0; i < N; ++i) w[i] = k == i ? r : w[i];
         slow &= slow - 1u;
@@ -1192,155 +1186,143 @@ __device__ __forceinline__ void dn_pair_weights(const DnsPix a[N], const DnsPix&
         any_p |= p2[i] != 0.0f;
     }
     float cw[N], nw[N], pw[N];
-#if CPT_DN_PROBE == 2   // DIAGNOSTIC timing probe (wrong images): no exps at all
-#pragma unroll
-    for (int i = 0; i < N; ++i) out[i] = c2[i] * n2[i] + p2[i];
-    return;
-#endif
     dn_weights<N>(c2, cw, tab);
     // a zero normal (depth) difference gives exactly 1 (dn_weight(0)); equal normals (the floor)
     // and the constant depth (a18) make whole batches of the wave skip the sequence
 #pragma unroll
     for (int i = 0; i < N; ++i) nw[i] = pw[i] = 1.0f;
-#if CPT_DN_PROBE != 1   // (1: DIAGNOSTIC timing probe without the normal factor's exps)
     if (__builtin_amdgcn_ballot_w64(any_n)) dn_weights<N>(n2, nw, tab);
-#endif
     if (__builtin_amdgcn_ballot_w64(any_p)) dn_weights<N>(p2, pw, tab);
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = cw[i] * nw[i] * pw[i];
 }
 
-// Global memory: every load of a step is issued, unconditionally (out-of-frame lanes read a valid
-// address and discard it), before the step's stores, and the stores sit in a branch-free tail, so
-// the next step's wait for its prefetched row counts only those loads (vmcnt(#stores)) instead of
-// draining the stores (gfx9's one vector-memory counter; a pinned host frame's stores cross PCIe).
+// The block's four waves share the window: per super-step they take the next four rows, wave w
+// row R = B + w:
+//   1. each wave writes its row into the block's pixel ring (12 rows: the four new ones never alias
+//      the eight the other waves may still be reading for their taps) and prefetches row R + 4;
+//   barrier;
+//   2. each wave computes its row's 12 pair weights into the block's weight ring (6 rows);
+//   barrier;
+//   3. each wave finalizes output row O = R - 2 from the weights of rows O .. O + 2 and the pixel
+//      rows O - 2 .. O + 2, in the reference's tap order, and stores it.
+// Shared rings need 11 KB of LDS per wave, against 19.5 KB for one wave walking a strip alone (the
+// round-5 intermediate, k_denoise_strip: 0.127 ms at C4): three waves per SIMD (the VGPR limit,
+// 150) instead of two, 0.106 ms.  Loads: every load of a step is issued, unconditionally
+// (out-of-frame lanes read a valid address and discard it), before the step's stores, and the
+// stores sit in a branch-free tail (lanes without an output pixel store to `sink`), so the next
+// row's wait does not drain a branch's worth of uncertainty.  Eight-wave blocks at four waves per
+// SIMD spill 22 VGPRs and ran 0.117-0.124 ms.
+#ifndef CPT_DNR_WAVES
+#define CPT_DNR_WAVES 4
+#endif
+#ifndef CPT_DNR_MINWAVES   // __launch_bounds__ waves per SIMD (3: <= 168 VGPRs; 4: <= 128)
+#define CPT_DNR_MINWAVES 3
+#endif
+// pixel ring: the n new rows + the 2n + 4 - n rows a slower wave may still read for its taps;
+// weight ring: the n + 2 rows the taps of one super-step read
+constexpr int DNR_WAVES = CPT_DNR_WAVES, DNR_PIX_ROWS = 2 * DNR_WAVES + 4, DNR_W_ROWS = DNR_WAVES + 2;
+
 template <bool HOST>
-__global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
+__global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_denoise_rows(
     const float4* __restrict__ accum, const float* __restrict__ normal, const float* __restrict__ depth,
     float* __restrict__ mix, uint8_t* __restrict__ out, uint8_t* __restrict__ out_host, float4* __restrict__ sink,
     int width, int row0, int y0, int y1, int w_eff, int h_eff, int n_strips, int per_strip, float inv_idx) {
     __shared__ double s_tab[DN_EXP_N];
-    __shared__ float4 s_rgbv[DNS_WAVES][5][DNS_LANES];
-    __shared__ float4 s_nd[DNS_WAVES][5][DNS_LANES];
-    __shared__ float s_w[DNS_WAVES][3][12][DNS_LANES];
-    for (int i = threadIdx.x; i < DN_EXP_N; i += DNS_LANES * DNS_WAVES) s_tab[i] = g_dn_exp_table[i];
-    __syncthreads();
+    __shared__ float4 rgbv[DNR_PIX_ROWS][DNS_LANES];
+    __shared__ float4 ndr[DNR_PIX_ROWS][DNS_LANES];
+    __shared__ float W[DNR_W_ROWS][12][DNS_LANES];
+    for (int i = threadIdx.x; i < DN_EXP_N; i += DNS_LANES * DNR_WAVES) s_tab[i] = g_dn_exp_table[i];
     const int wv = (int)(threadIdx.x >> 6), j = (int)(threadIdx.x & 63);
-    const int wid = (int)blockIdx.x * DNS_WAVES + wv;
-    if (wid >= n_strips * per_strip) return;
-    const int strip = wid % n_strips, part = wid / n_strips;
+    const int strip = (int)blockIdx.x % n_strips, part = (int)blockIdx.x / n_strips;
     const int nrow = y1 - y0;
     const int ra = y0 + (int)((long long)nrow * part / per_strip), rb = y0 + (int)((long long)nrow * (part + 1) / per_strip);
-    if (ra >= rb) return;
     const int c0 = strip * DNS_COLS;
-    const int col = c0 - 2 + j;                     // this lane's column of the linear run (may be < 0 or >= W')
+    const int col = c0 - 2 + j;
     const int limit = w_eff * h_eff;
     const bool out_lane = j >= 2 && j < 2 + DNS_COLS && col < w_eff;
-    float4* const sink_lane = sink + (((uint32_t)wid & 1023u) * 64u + (uint32_t)j);
-    float4 (*rgbv)[DNS_LANES] = s_rgbv[wv];
-    float4 (*ndr)[DNS_LANES] = s_nd[wv];
-    auto ring = [&](int slot, int lane) { return DnsPix{rgbv[slot][lane], ndr[slot][lane]}; };
-    float (*W)[12][DNS_LANES] = s_w[wv];
-    // (lane indices of partners, clamped into the wave: edge lanes compute pairs nobody reads)
+    float4* const sink_lane = sink + ((((uint32_t)blockIdx.x * DNR_WAVES + (uint32_t)wv) & 1023u) * 64u + (uint32_t)j);
+    auto ring = [&](int row, int lane) {
+        const int sl = (row + 4 * DNR_PIX_ROWS) % DNR_PIX_ROWS;
+        return DnsPix{rgbv[sl][lane], ndr[sl][lane]};
+    };
     auto cl = [](int l) { return l < 0 ? 0 : (l > 63 ? 63 : l); };
-    // pixel of row Y at this lane: L = Y W' + col
     auto load = [&](int Y, float4& a, float3& n, float& d, bool& valid) {
         const int L = Y * w_eff + col;
         valid = L >= 0 && L < limit;
         const int yy = col < 0 ? Y - 1 : (col >= w_eff ? Y + 1 : Y);
         const int xx = L - yy * w_eff;
-        const size_t px = valid ? (size_t)(yy - row0) * width + xx : (size_t)0;   // (a valid address)
-        // raw values: an out-of-frame lane's are replaced by zeros where they are used (a select
-        // here would make the compiler wait for the loads at once)
-#if CPT_DN_PROBE == 4   // DIAGNOSTIC timing probe: no global loads (synthetic pixels)
-        a = make_float4((float)(L & 7), (float)(L & 3), 0.5f, 1.0f);
-        n = make_float3(0.f, (float)(L & 1), 0.f);
-        d = 1e30f;
-        (void)px;
-#else
+        const size_t px = valid ? (size_t)(yy - row0) * width + xx : (size_t)0;
         a = accum[px];
         n = make_float3(normal[3 * px], normal[3 * px + 1], normal[3 * px + 2]);
         d = depth[px];
-#endif
     };
-    float4 na;
-    float3 nn;
-    float nd;
-    bool nvalid;
-    load(ra - 2, na, nn, nd, nvalid);
+    auto put = [&](int Y, const float4& na, const float3& nn, float nd, bool nvalid) {
+        const float4 a = nvalid ? na : make_float4(0.f, 0.f, 0.f, 0.f);
+        const v3 c = a.w != 0.f ? mk(a.x, a.y, a.z) / a.w : mk(a.x, a.y, a.z);
+        const int sl = (Y + 4 * DNR_PIX_ROWS) % DNR_PIX_ROWS;
+        rgbv[sl][j] = make_float4(c.x, c.y, c.z, nvalid ? 1.f : 0.f);
+        ndr[sl][j] = nvalid ? make_float4(nn.x, nn.y, nn.z, nd) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
     constexpr float kernel5[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
                                      {4.f, 16.f, 26.f, 16.f, 4.f},
                                      {7.f, 26.f, 41.f, 26.f, 7.f},
                                      {4.f, 16.f, 26.f, 16.f, 4.f},
                                      {1.f, 4.f, 7.f, 4.f, 1.f}};
+    // rows ra - 2 and ra - 1 (waves 0, 1): the pairs of rows ra, ra + 1 reach back into them
+    float4 na;
+    float3 nn;
+    float nd;
+    bool nvalid;
+    if (wv < 2) {
+        load(ra - 2 + wv, na, nn, nd, nvalid);
+        put(ra - 2 + wv, na, nn, nd, nvalid);
+    }
+    load(ra + wv, na, nn, nd, nvalid);
 #pragma unroll 1
-    for (int Y = ra - 2; Y < rb + 2; ++Y) {
-        const int O = Y - 2;                     // the output row this step completes
-        // ---- the mix of row O (used at the step's end), row Y into the ring, row Y + 1 ahead ----
-        // (issued in this order so that each wait names only the loads it needs: the mix is
-        // waited for behind the row loads issued after it, the row behind the step's stores)
+    for (int B = ra; B - 2 < rb; B += DNR_WAVES) {
+        const int R = B + wv;           // this wave's new row
+        const int O = R - 2;            // the output row it finalizes
         float3 mix_cur;
         {
             const int orow = min(max(O, ra), rb - 1);
             const int ocol = min(max(col, 0), w_eff - 1);
             const size_t b = (size_t)(orow - y0) * width + ocol;
-#if CPT_DN_PROBE == 4
-            mix_cur = make_float3(0.25f, 0.5f, (float)(b & 1));
-#else
             mix_cur = make_float3(mix[3 * b], mix[3 * b + 1], mix[3 * b + 2]);
-#endif
         }
-        DnsPix me;
+        put(R, na, nn, nd, nvalid);
+        const DnsPix me = ring(R, j);   // (this lane's own write: ordered)
+        load(R + DNR_WAVES, na, nn, nd, nvalid);
+        __syncthreads();
+        // ---- the 12 pair weights whose later pixel is (R, j) ---------------------------------------
         {
-            const float4 a = nvalid ? na : make_float4(0.f, 0.f, 0.f, 0.f);
-            const v3 c = a.w != 0.f ? mk(a.x, a.y, a.z) / a.w : mk(a.x, a.y, a.z);
-            me.rgbv = make_float4(c.x, c.y, c.z, nvalid ? 1.f : 0.f);
-            me.nd = nvalid ? make_float4(nn.x, nn.y, nn.z, nd) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        const int slot = (Y + 10) % 5;
-        rgbv[slot][j] = me.rgbv;
-        ndr[slot][j] = me.nd;
-        load(Y + 1, na, nn, nd, nvalid);        // (past rb + 1: read and never used)
-        wave_fence();
-        // ---- the 12 pair weights whose later pixel is (Y, j) -----------------------------------
-        // needed for output rows Y - 2 .. Y only while Y >= ra; the last two steps need only the
-        // pairs reaching back into rows < rb (the same-row pairs of rows >= rb are never read)
-        if (Y >= ra) {
-            const int s1 = (Y + 9) % 5, s2 = (Y + 8) % 5;
             float w12[12];
-            {
-                DnsPix a[6];
-                a[0] = ring(slot, cl(j + 1));
-                a[1] = ring(slot, cl(j + 2));
+            // partner k of the 12 (k = 0, 1: (R, j + k + 1); 2..6: (R - 1, j + k - 4); 7..11:
+            // (R - 2, j + k - 9)), in batches of CPT_DN_BATCH pairs
+            auto partner = [&](int k) {
+                return k < 2 ? ring(R, cl(j + k + 1)) : (k < 7 ? ring(R - 1, cl(j + k - 4)) : ring(R - 2, cl(j + k - 9)));
+            };
 #pragma unroll
-                for (int dx = -2; dx <= 1; ++dx) a[2 + dx + 2] = ring(s1, cl(j + dx));
-                dn_pair_weights<6>(a, me, w12, s_tab);   // k = 0, 1 (dy 0), 2..5 (dy 1, dx -2..1)
-            }
-            {
-                DnsPix a[6];
-                a[0] = ring(s1, cl(j + 2));
+            for (int k0 = 0; k0 < 12; k0 += CPT_DN_BATCH) {
+                DnsPix a[CPT_DN_BATCH];
 #pragma unroll
-                for (int dx = -2; dx <= 2; ++dx) a[1 + dx + 2] = ring(s2, cl(j + dx));
-                dn_pair_weights<6>(a, me, w12 + 6, s_tab);   // k = 6 (dy 1, dx 2), 7..11 (dy 2)
+                for (int i = 0; i < CPT_DN_BATCH; ++i) a[i] = partner(k0 + i);
+                dn_pair_weights<CPT_DN_BATCH>(a, me, w12 + k0, s_tab);
             }
-            // forward index k of the pair (Y - dy, j + dx) -> (Y, j): here the later pixel is
-            // this lane's, so the pair is the EARLIER pixel's forward (dx' = -dx, dy' = dy);
-            // store it under the earlier pixel's forward index k(dy, -dx) at this lane
-            const int ws = (Y + 9) % 3;
+            const int ws = (R + 4 * DNR_W_ROWS) % DNR_W_ROWS;
 #pragma unroll
             for (int k = 0; k < 12; ++k) W[ws][k][j] = w12[k];
         }
-        wave_fence();
-        // ---- output row O: the 25 taps in the reference's order (i = dx outer, j = dy inner) -------
-        // the step's stores, issued on every step by every lane (branch-free, see above): lanes
-        // and steps without an output pixel store to the sink
+        __syncthreads();
+        // ---- output row O (wave-uniform condition; every lane computes, out_lane stores) --------
         v3 st_m = mk1(0.f);
         uint32_t st_bgr = 0;
         bool st_real = false;
-        if (O >= ra && O < rb) {                 // (wave-uniform; every lane computes, out_lane stores)
-            const int wO = (O + 9) % 3, wO1 = (O + 10) % 3, wO2 = (O + 11) % 3;
-            const int jc = min(max(j, 2), 61);    // edge lanes: a clamped (discarded) tap window
-            const DnsPix p = ring((O + 10) % 5, jc);
+        if (O >= ra && O < rb) {
+            const int wO = (O + 4 * DNR_W_ROWS) % DNR_W_ROWS, wO1 = (O + 1 + 4 * DNR_W_ROWS) % DNR_W_ROWS,
+                      wO2 = (O + 2 + 4 * DNR_W_ROWS) % DNR_W_ROWS;
+            const int jc = min(max(j, 2), 61);
+            const DnsPix p = ring(O, jc);
             const bool finite = __builtin_isfinite(p.rgbv.x) && __builtin_isfinite(p.rgbv.y) &&
                                 __builtin_isfinite(p.rgbv.z) && __builtin_isfinite(p.nd.x) &&
                                 __builtin_isfinite(p.nd.y) && __builtin_isfinite(p.nd.z) && __builtin_isfinite(p.nd.w);
@@ -1357,7 +1339,7 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
 #pragma unroll
                 for (int jj = 0; jj < 5; ++jj) {
                     const int u = i - 2, v = jj - 2;
-                    const float4 q = rgbv[(O + v + 10) % 5][jc + u];
+                    const float4 q = rgbv[(O + v + 4 * DNR_PIX_ROWS) % DNR_PIX_ROWS][jc + u];
                     float weight;
                     v3 ctmp;
                     if (q.w == 0.f) {
@@ -1366,9 +1348,9 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
                     } else {
                         ctmp = mk(q.x, q.y, q.z);
                         // where the pair (O, j) - (O + v, j + u) was stored: same row -- by the lane
-                        // of its left pixel at step O, as that pixel's forward pair |u| - 1; other
-                        // rows -- by the lane of its lower pixel at that pixel's step, at index
-                        // 2 + dx + 2 (dy 1) or 7 + dx + 2 (dy 2), dx = upper column - lower column
+                        // of its left pixel, as that pixel's forward pair |u| - 1; other rows -- by
+                        // the lane of its lower pixel, at index 2 + dx + 2 (dy 1) or 7 + dx + 2
+                        // (dy 2), dx = upper column - lower column
                         if (u == 0 && v == 0) weight = w_self;
                         else if (v == 0 && u > 0) weight = W[wO][u - 1][jc];
                         else if (v == 0) weight = W[wO][-u - 1][jc + u];
@@ -1384,26 +1366,19 @@ __global__ void __launch_bounds__(DNS_LANES * DNS_WAVES) k_denoise_strip(
                               __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));
             v3 m = mk(mix_cur.x, mix_cur.y, mix_cur.z);
             m = m + inv_idx * (clp - m);   // lerp (helper_math.h:1154-1157)
-            const uint32_t bgr = (uint32_t)(uint8_t)(255.99f * m.z) | ((uint32_t)(uint8_t)(255.99f * m.y) << 8) |
-                                 ((uint32_t)(uint8_t)(255.99f * m.x) << 16);
             st_m = m;
-            st_bgr = bgr;
+            st_bgr = (uint32_t)(uint8_t)(255.99f * m.z) | ((uint32_t)(uint8_t)(255.99f * m.y) << 8) |
+                     ((uint32_t)(uint8_t)(255.99f * m.x) << 16);
             st_real = out_lane;
         }
         {
             const size_t bself = st_real ? (size_t)(O - y0) * width + col : 0;
             float* const pm = st_real ? mix + 3 * bself : reinterpret_cast<float*>(sink_lane);
             uint32_t* const po = st_real ? reinterpret_cast<uint32_t*>(out) + bself : reinterpret_cast<uint32_t*>(sink_lane) + 3;
-#if CPT_DN_PROBE == 3   // DIAGNOSTIC timing probe: the stores of all but the last step skipped
-            if (Y == rb + 1) {
-#endif
             pm[0] = st_m.x;
             pm[1] = st_m.y;
             pm[2] = st_m.z;
             *po = st_bgr;
-#if CPT_DN_PROBE == 3
-            }
-#endif
             if (HOST) {
                 uint32_t* const ph = st_real ? reinterpret_cast<uint32_t*>(out_host) + bself : reinterpret_cast<uint32_t*>(sink_lane) + 3;
                 *ph = st_bgr;
@@ -1418,34 +1393,34 @@ hipError_t launch_denoise_mix(const float4* accum, const float* normal, const fl
     const int w_eff = 16 * (width / 16), h_eff = 16 * (height / 16);
     if (w_eff == 0 || h_eff == 0 || y1 <= y0) return hipSuccess;
     const float inv_idx = 1.f / float(cur_sample_idx);
-#if CPT_DN_TILE
+#if !CPT_DN_TILE
+    {
+        static int cus2[64] = {0};
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (dev < 0 || dev >= 64) dev = 0;
+        if (cus2[dev] == 0) {
+            int n = 0;
+            if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+            cus2[dev] = n;
+        }
+        const int n_strips = (w_eff + DNS_COLS - 1) / DNS_COLS;
+        const int rows = y1 - y0;
+        int per_strip = (cus2[dev] * CPT_DNR_BLOCKS_PER_CU + n_strips - 1) / n_strips;
+        per_strip = per_strip < 1 ? 1 : (per_strip > rows ? rows : per_strip);
+        const unsigned blocks = (unsigned)(n_strips * per_strip);
+        if (out_host)
+            hipLaunchKernelGGL(k_denoise_rows<true>, dim3(blocks), dim3(DNS_LANES * DNR_WAVES), 0, stream, accum, normal, depth, mix,
+                               out, out_host, sink, width, row0, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
+        else
+            hipLaunchKernelGGL(k_denoise_rows<false>, dim3(blocks), dim3(DNS_LANES * DNR_WAVES), 0, stream, accum, normal, depth, mix,
+                               out, out_host, sink, width, row0, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
+        return hipGetLastError();
+    }
+#else
     const int n_tiles = ((w_eff + DN_TX - 1) / DN_TX) * ((y1 - y0 + DN_TY - 1) / DN_TY);
     hipLaunchKernelGGL(k_denoise_mix, dim3((unsigned)n_tiles), dim3(DN_THREADS), 0, stream, accum, normal, depth, mix, out, out_host, width,
                        row0, y0, y1, w_eff, h_eff, inv_idx);
-#else
-    // waves: CPT_DN_WAVES_PER_CU per CU, whole strips (each wave owns one strip's run of rows)
-    static int cus[64] = {0};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (dev < 0 || dev >= 64) dev = 0;
-    if (cus[dev] == 0) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cus[dev] = n;
-    }
-    const int n_strips = (w_eff + DNS_COLS - 1) / DNS_COLS;
-    const int rows = y1 - y0;
-    int per_strip = (cus[dev] * CPT_DN_WAVES_PER_CU + n_strips - 1) / n_strips;
-    per_strip = per_strip < 1 ? 1 : (per_strip > rows ? rows : per_strip);
-    const int waves = n_strips * per_strip;
-    if (out_host)
-        hipLaunchKernelGGL(k_denoise_strip<true>, dim3((unsigned)((waves + DNS_WAVES - 1) / DNS_WAVES)), dim3(DNS_LANES * DNS_WAVES), 0,
-                           stream, accum, normal, depth, mix, out, out_host, sink, width, row0, y0, y1, w_eff, h_eff, n_strips, per_strip,
-                           inv_idx);
-    else
-        hipLaunchKernelGGL(k_denoise_strip<false>, dim3((unsigned)((waves + DNS_WAVES - 1) / DNS_WAVES)), dim3(DNS_LANES * DNS_WAVES), 0,
-                           stream, accum, normal, depth, mix, out, out_host, sink, width, row0, y0, y1, w_eff, h_eff, n_strips, per_strip,
-                           inv_idx);
 #endif
     return hipGetLastError();
 }
