@@ -830,7 +830,7 @@ static int denoise_band(cpt_ctx* c, uint32_t cur_sample_idx, int y0, int y1, uin
     if (!c->d_dn_sink) HIP_TRY(c, hipMalloc((void**)&c->d_dn_sink, cpt::DN_SINK_SLOTS * sizeof(float4)));
     HIP_TRY(c, hipEventRecord(c->ev_dn0, s));
     HIP_TRY(c, cpt::launch_denoise_mix(c->d_accum, c->d_normal, c->d_depth, c->d_mix, c->d_bgra, host_alias, c->d_dn_sink, c->width,
-                                      c->height, row0, y0, y1, cur_sample_idx, s));
+                                      c->height, row0, c->n_rows, y0, y1, cur_sample_idx, s));
     HIP_TRY(c, hipEventRecord(c->ev_dn1, s));
     c->have_dn_timing = true;
     if (bgra_host && host_alias) {

@@ -143,11 +143,12 @@ hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned l
                                 hipStream_t stream);
 hipError_t launch_stitch_rows(const float4* src_acc, const float* src_nrm, const float* src_dep, const int32_t* dst_row,
                               int width, int n_rows, float4* acc, float* nrm, float* dep, hipStream_t stream);
-// out_host (nullable): the device alias of a pinned host frame, written beside `out`; sink: a
+// out_host (nullable): the device alias of a pinned host frame, written beside `out`; accum /
+// normal / depth hold the context's ctx_rows rows from row0; sink: a
 // device buffer of DN_SINK_SLOTS float4s the strip kernel's lanes without an output pixel store to
 constexpr int DN_SINK_SLOTS = 1024 * 64;
 hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
-                              uint8_t* out_host, float4* sink, int width, int height, int row0, int y0, int y1,
+                              uint8_t* out_host, float4* sink, int width, int height, int row0, int ctx_rows, int y0, int y1,
                               uint32_t cur_sample_idx, hipStream_t stream);
 
 }  // namespace cpt

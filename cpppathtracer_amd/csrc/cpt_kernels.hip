@@ -1227,7 +1227,7 @@ template <bool HOST>
 __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_denoise_rows(
     const float4* __restrict__ accum, const float* __restrict__ normal, const float* __restrict__ depth,
     float* __restrict__ mix, uint8_t* __restrict__ out, uint8_t* __restrict__ out_host, float4* __restrict__ sink,
-    int width, int row0, int y0, int y1, int w_eff, int h_eff, int n_strips, int per_strip, float inv_idx) {
+    int width, int row0, int ctx_rows, int y0, int y1, int w_eff, int h_eff, int n_strips, int per_strip, float inv_idx) {
     __shared__ double s_tab[DN_EXP_N];
     __shared__ float4 rgbv[DNR_PIX_ROWS][DNS_LANES];
     __shared__ float4 ndr[DNR_PIX_ROWS][DNS_LANES];
@@ -1252,7 +1252,11 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
         valid = L >= 0 && L < limit;
         const int yy = col < 0 ? Y - 1 : (col >= w_eff ? Y + 1 : Y);
         const int xx = L - yy * w_eff;
-        const size_t px = valid ? (size_t)(yy - row0) * width + xx : (size_t)0;
+        // the window reads up to a super-step past the rows it outputs; rows the context does not
+        // hold (a band's, cpt_denoise_mix_band) are never a tap or pair of an output pixel, so
+        // they read address 0 like the out-of-frame ones
+        const bool held = yy - row0 >= 0 && yy - row0 < ctx_rows;
+        const size_t px = valid && held ? (size_t)(yy - row0) * width + xx : (size_t)0;
         a = accum[px];
         n = make_float3(normal[3 * px], normal[3 * px + 1], normal[3 * px + 2]);
         d = depth[px];
@@ -1388,7 +1392,7 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
 }
 
 hipError_t launch_denoise_mix(const float4* accum, const float* normal, const float* depth, float* mix, uint8_t* out,
-                              uint8_t* out_host, float4* sink, int width, int height, int row0, int y0, int y1,
+                              uint8_t* out_host, float4* sink, int width, int height, int row0, int ctx_rows, int y0, int y1,
                               uint32_t cur_sample_idx, hipStream_t stream) {
     const int w_eff = 16 * (width / 16), h_eff = 16 * (height / 16);
     if (w_eff == 0 || h_eff == 0 || y1 <= y0) return hipSuccess;
@@ -1411,10 +1415,10 @@ hipError_t launch_denoise_mix(const float4* accum, const float* normal, const fl
         const unsigned blocks = (unsigned)(n_strips * per_strip);
         if (out_host)
             hipLaunchKernelGGL(k_denoise_rows<true>, dim3(blocks), dim3(DNS_LANES * DNR_WAVES), 0, stream, accum, normal, depth, mix,
-                               out, out_host, sink, width, row0, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
+                               out, out_host, sink, width, row0, ctx_rows, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
         else
             hipLaunchKernelGGL(k_denoise_rows<false>, dim3(blocks), dim3(DNS_LANES * DNR_WAVES), 0, stream, accum, normal, depth, mix,
-                               out, out_host, sink, width, row0, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
+                               out, out_host, sink, width, row0, ctx_rows, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
         return hipGetLastError();
     }
 #else
