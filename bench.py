@@ -437,6 +437,9 @@ def run(args):
                 "width": W, "height": H, "spp": spp, "max_depth": depth, "seed": cfg["seed"],
                 "rows_rendered": H, "path": args.path, "walk": args.walk, "schedule": schedule,
                 "tail_consolidation": bool(consolidating),
+                # strong (default since round 4): the config's own frame at every N; weak: pixels per
+                # GPU fixed.  N > 1 values of rounds 1-3 were weak-scaled
+                "scaling": args.scaling,
                 "parallelism": f"row-tiled x{world} (interleaved {tiling.BLOCK_ROWS}-row blocks){collective}",
             },
             "rng_init_ms": round(t_init * 1e3, 2),

@@ -73,6 +73,11 @@ namespace cpt {
 #define CPT_TAKE_FRESH 1
 #endif
 
+// The LDS kernels' cold walks out of line (cpt_path.hpp trace_cold).
+#ifndef CPT_COLD_NOINLINE
+#define CPT_COLD_NOINLINE 0
+#endif
+
 constexpr int SUSPEND_AT = CPT_SUSPEND_AT;
 constexpr int SUSPEND_MIN_DONE = CPT_SUSPEND_MIN_DONE;
 constexpr int SPEC_LEAF_ROUND = CPT_SPEC_LEAF_ROUND;

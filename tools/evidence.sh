@@ -16,5 +16,7 @@ exec_steps=(
     "profile:900:bash tools/profile.sh c4full_$tag --steps 1 --warmup 0 --no-cpu-baseline --no-hbm-probe --no-count --no-strong-check"
     "reh_c4:300:python tools/scaling_rehearsal.py --config c4"
     "reh_c5:300:python tools/scaling_rehearsal.py --config c5 --spp 4096 --ns 1,8"
+    "dispatch_c4:200:python bench.py --dispatch 30"
+    "profile_dn:400:bash tools/profile.sh dn_$tag --dispatch 10 --dispatch-contexts 1"
 )
 bash tools/gpu_check.sh "${exec_steps[@]}"
