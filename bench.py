@@ -535,7 +535,7 @@ def run(args):
 # ---------------------------------------------------------------------------------------
 # --dispatch K: the reference's own per-pass loop (PipelineLoop, path_tracer.cu:256-306)
 # ---------------------------------------------------------------------------------------
-DISPLAY_BYTES_PER_PIXEL = 60   # k_denoise_mix: accum 16 + normal 12 + depth 4 + mix 12 read + 12 written + BGRA 4
+DISPLAY_BYTES_PER_PIXEL = 60   # k_denoise_rows (k_denoise_mix under CPT_DN_TILE=1): accum 16 + normal 12 + depth 4 + mix 12 read + 12 written + BGRA 4
 
 
 def dispatch_bench(args):
@@ -610,7 +610,7 @@ def dispatch_bench(args):
         "display_host_frame_ms": round(float(np.median(disp)) - d_ms, 4),
         "copy_and_host_ms": round(float(np.median(wall)) - float(np.median(rend)) - float(np.median(disp)), 3),
         "display_roofline": {
-            "kernel": "k_denoise_mix", "bound": "hbm", "bytes_per_launch": display_bytes,
+            "kernel": "k_denoise_rows", "bound": "hbm", "bytes_per_launch": display_bytes,
             "achieved": round(display_bytes / (d_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(display_bytes / (d_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "byte_model": f"{DISPLAY_BYTES_PER_PIXEL} B x W'H' ({w_eff}x{h_eff}): accumulator 16 + normal 12 + "
