@@ -288,14 +288,29 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                         // relaxed load per draw, i.e. per ~64 takes at spp >= 64).
                         uint32_t seen = res_seen;
 #if CPT_TAKE_FRESH
-                        if (p.spp >= 64) {
+                        // (CPT_TAKE_FRESH 2: only while this wave's last draw left more than the tail:
+                        // the counter only grows, so a wave once in the tail stays there)
+                        if (p.spp >= 64 && (CPT_TAKE_FRESH == 1 || res_seen + n_static < n_work)) {
                             uint32_t cur = 0;
                             if (lane == leader) cur = __hip_atomic_load(p.work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             seen = __builtin_amdgcn_readfirstlane(__shfl(cur, leader)) + off;
                         }
 #endif
-                        const uint32_t bsz_k = CONS ? (uint32_t)CPT_TAKE_BATCH_CONS_SIZE : bsz;
-                        const uint32_t grab = (!CONS || CPT_TAKE_BATCH_CONS) && n_work - seen > n_static && bsz_k > want ? bsz_k : want;
+                        uint32_t bsz_k = CONS ? (uint32_t)CPT_TAKE_BATCH_CONS_SIZE : bsz;
+                        const uint32_t left_ids = n_work > seen ? n_work - seen : 0u;
+#if CPT_TAKE_TAPER
+                        // long chains: the range shrinks with what is left (guided scheduling), so
+                        // the ids waves hold unstarted never amount to more than 1/TAPER of a round
+                        // of the grid's lanes
+                        if (p.spp >= 64) {
+                            const uint64_t t = (uint64_t)bsz_k * left_ids / ((uint64_t)n_static * CPT_TAKE_TAPER);
+                            bsz_k = t < bsz_k ? (uint32_t)t : bsz_k;
+                        }
+                        const bool batch_ok = p.spp >= 64 || left_ids > n_static;
+#else
+                        const bool batch_ok = left_ids > n_static;
+#endif
+                        const uint32_t grab = (!CONS || CPT_TAKE_BATCH_CONS) && batch_ok && bsz_k > want ? bsz_k : want;
                         if (lane == leader) nb = atomicAdd(p.work, grab);
                         nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader)) + off;
                         ncnt = grab;

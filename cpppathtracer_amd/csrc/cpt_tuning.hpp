@@ -66,11 +66,22 @@ namespace cpt {
 #ifndef CPT_TAKE_BATCH_CONS_SIZE
 #define CPT_TAKE_BATCH_CONS_SIZE 64
 #endif
-// Long chains: the leader reads the pixel counter before sizing a draw, so the tail rule (draw
-// only what is needed once less than one id per lane of the grid is left) sees the counter's
-// current value rather than the wave's last draw (advisor r04; A/B in DESIGN.md).
+// Long chains: the leader reads the pixel counter before sizing a draw, so the range size sees
+// the counter's current value rather than the wave's last draw (advisor r04).  2: only until
+// the wave's last draw left less than one id per lane of the grid (the tail, where draws are
+// frequent and nearly exact anyway); 1: on every draw.
 #ifndef CPT_TAKE_FRESH
-#define CPT_TAKE_FRESH 1
+#define CPT_TAKE_FRESH 2
+#endif
+// Long chains: the range a wave draws shrinks as 64 x left / (TAPER x grid lanes) (guided
+// scheduling), so the ids waves hold unstarted stay below 1/TAPER of a lane-round.  0: full
+// ranges until one id per lane is left, then exact draws — then up to a whole lane-round of ids
+// sits in waves' ranges when the tail starts, a chain-time lost at frames of few pixels per lane.
+// Round 5 (profiles/r05/ab_take_*.log), C2 (3.5 pixels per lane) / C4 (7.9): taper 0 with
+// fresh 1 24.4k / 1982; fresh 2 28.8k / 1963; taper 2 29.5k / 1965; taper 4 30.1k / 1982;
+// taper 8 30.4k / 1952; one atomic per take (CPT_TAKE_BATCH 0) 30.7k / 1954 Mpaths/s.
+#ifndef CPT_TAKE_TAPER
+#define CPT_TAKE_TAPER 4
 #endif
 
 // The LDS kernels' cold walks out of line (cpt_path.hpp trace_cold).
