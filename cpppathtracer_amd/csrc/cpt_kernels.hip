@@ -963,11 +963,27 @@ __device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b, 
 #ifndef CPT_DN_TILE          // 1: the round-4 tile kernel above (A/B); 0: k_denoise_rows (the default)
 #define CPT_DN_TILE 0
 #endif
-#ifndef CPT_DNR_BLOCKS_PER_CU  // k_denoise_rows' blocks per CU (43 KB of LDS each; three waves per SIMD)
-#define CPT_DNR_BLOCKS_PER_CU 3
+#ifndef CPT_DNR_BLOCKS_PER_CU  // k_denoise_rows' blocks per CU (8-wave blocks: 70 KB of LDS each; four waves per SIMD)
+#define CPT_DNR_BLOCKS_PER_CU 2
 #endif
+#ifndef CPT_DN_NOBRANCH        // 1: out-of-frame pairs weigh 0 in the weight ring, taps without a branch
+#define CPT_DN_NOBRANCH 1
+#endif
+#ifndef CPT_DN_SPLIT           // 1: all 36 squared differences before the weights (fewer live VGPRs)
+#define CPT_DN_SPLIT 0
+#endif
+#ifndef CPT_DN_TAPFENCE        // 1: a scheduling barrier between tap rows
+#define CPT_DN_TAPFENCE 0
+#endif
+#ifndef CPT_DN_LATELOAD        // where k_denoise_rows issues its global loads (see the loop)
+#define CPT_DN_LATELOAD 2
+#endif
+#ifndef CPT_DN_PACK            // 1: the taps' x/y products and sums as packed f32 pairs
+#define CPT_DN_PACK 0
+#endif
+typedef float dn_f2 __attribute__((ext_vector_type(2)));
 #ifndef CPT_DN_BATCH           // pair weights evaluated together (a divisor of 12)
-#define CPT_DN_BATCH 6
+#define CPT_DN_BATCH 4
 #endif
 constexpr int DN_TX = 64, DN_TY = CPT_DN_TY, DN_THREADS = DN_TX * DN_TY;
 constexpr int DN_BX = DN_TX + 4, DN_BY = DN_TY + 4;   // staged box (2-pixel halo each side)
@@ -1184,19 +1200,24 @@ __device__ __forceinline__ void dn_weights(const float d2[N], float w[N], const 
     }
 }
 
+// The three squared differences of one pair (path_tracer.cu:221-231): colour, normal (clamped at
+// 0: (float)max((double)dn, 0.0), the reference's clamp in double), depth.
+__device__ __forceinline__ void dn_pair_dist(const DnsPix& a, const DnsPix& b, float& c2, float& n2, float& p2) {
+    v3 t = mk(a.rgbv.x, a.rgbv.y, a.rgbv.z) - mk(b.rgbv.x, b.rgbv.y, b.rgbv.z);
+    c2 = dot(t, t);
+    t = mk(a.nd.x, a.nd.y, a.nd.z) - mk(b.nd.x, b.nd.y, b.nd.z);
+    const float dn = dot(t, t);
+    n2 = dn > 0.0f ? dn : 0.0f;
+    p2 = (a.nd.w - b.nd.w) * (a.nd.w - b.nd.w);
+}
+
+// c_w * n_w * p_w (left to right) of N pairs from their squared differences.
 template <int N>
-__device__ __forceinline__ void dn_pair_weights(const DnsPix a[N], const DnsPix& b, float out[N],
+__device__ __forceinline__ void dn_dist_weights(const float c2[N], const float n2[N], const float p2[N], float out[N],
                                                 const double* __restrict__ tab) {
-    float c2[N], n2[N], p2[N];
     bool any_n = false, any_p = false;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        v3 t = mk(a[i].rgbv.x, a[i].rgbv.y, a[i].rgbv.z) - mk(b.rgbv.x, b.rgbv.y, b.rgbv.z);
-        c2[i] = dot(t, t);
-        t = mk(a[i].nd.x, a[i].nd.y, a[i].nd.z) - mk(b.nd.x, b.nd.y, b.nd.z);
-        const float dn = dot(t, t);
-        n2[i] = dn > 0.0f ? dn : 0.0f;   // (float)max((double)dn, 0.0): the reference's clamp in double
-        p2[i] = (a[i].nd.w - b.nd.w) * (a[i].nd.w - b.nd.w);
         any_n |= n2[i] != 0.0f;
         any_p |= p2[i] != 0.0f;
     }
@@ -1212,27 +1233,39 @@ __device__ __forceinline__ void dn_pair_weights(const DnsPix a[N], const DnsPix&
     for (int i = 0; i < N; ++i) out[i] = cw[i] * nw[i] * pw[i];
 }
 
-// The block's four waves share the window: per super-step they take the next four rows, wave w
-// row R = B + w:
-//   1. each wave writes its row into the block's pixel ring (12 rows: the four new ones never alias
-//      the eight the other waves may still be reading for their taps) and prefetches row R + 4;
+template <int N>
+__device__ __forceinline__ void dn_pair_weights(const DnsPix a[N], const DnsPix& b, float out[N],
+                                                const double* __restrict__ tab) {
+    float c2[N], n2[N], p2[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) dn_pair_dist(a[i], b, c2[i], n2[i], p2[i]);
+    dn_dist_weights<N>(c2, n2, p2, out, tab);
+}
+
+// The block's n waves (CPT_DNR_WAVES, 8) share the window: per super-step they take the next n
+// rows, wave w row R = B + w:
+//   1. each wave writes its row into the block's pixel ring (2n + 4 rows: the n new ones never
+//      alias the n + 4 the other waves may still be reading for their taps);
 //   barrier;
-//   2. each wave computes its row's 12 pair weights into the block's weight ring (6 rows);
+//   2. each wave computes its row's 12 pair weights into the block's weight ring (n + 2 rows),
+//      then issues the loads of row R + n (the prefetch) and of its output row's mix;
 //   barrier;
 //   3. each wave finalizes output row O = R - 2 from the weights of rows O .. O + 2 and the pixel
 //      rows O - 2 .. O + 2, in the reference's tap order, and stores it.
-// Shared rings need 11 KB of LDS per wave, against 19.5 KB for one wave walking a strip alone (the
-// round-5 intermediate, k_denoise_strip: 0.127 ms at C4): three waves per SIMD (the VGPR limit,
-// 150) instead of two, 0.106 ms.  Loads: every load of a step is issued, unconditionally
-// (out-of-frame lanes read a valid address and discard it), before the step's stores, and the
-// stores sit in a branch-free tail (lanes without an output pixel store to `sink`), so the next
-// row's wait does not drain a branch's worth of uncertainty.  Eight-wave blocks at four waves per
-// SIMD spill 22 VGPRs and ran 0.117-0.124 ms.
+// Occupancy is the lever this kernel answered to (round 5, profiles/r05/ab_display_*.log, C4
+// device frame): one wave per strip with its own 19.5 KB ring (k_denoise_strip, retired) 0.127 ms;
+// 4-wave blocks sharing the rings, 3 waves per SIMD (150 VGPRs) 0.106-0.109; out-of-frame pairs
+// stored as weight 0 so the taps need no branch (138 VGPRs) 0.097; 8-wave blocks at 4 waves per
+// SIMD, batches of 4 pair weights and the loads issued after the pair weights (124 VGPRs, no
+// spill) 0.090-0.092 (with the loads ahead of the pairs: 14 VGPRs spilled, 0.093-0.099).
+// Loads are issued unconditionally (out-of-frame lanes read a valid address and discard it)
+// and the stores sit in a branch-free tail (lanes without an output pixel store to `sink`), so
+// the next row's wait does not drain a branch's worth of stores.
 #ifndef CPT_DNR_WAVES
-#define CPT_DNR_WAVES 4
+#define CPT_DNR_WAVES 8
 #endif
 #ifndef CPT_DNR_MINWAVES   // __launch_bounds__ waves per SIMD (3: <= 168 VGPRs; 4: <= 128)
-#define CPT_DNR_MINWAVES 3
+#define CPT_DNR_MINWAVES 4
 #endif
 // pixel ring: the n new rows + the 2n + 4 - n rows a slower wave may still read for its taps;
 // weight ring: the n + 2 rows the taps of one super-step read
@@ -1303,15 +1336,19 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
         const int R = B + wv;           // this wave's new row
         const int O = R - 2;            // the output row it finalizes
         float3 mix_cur;
-        {
+        auto load_mix = [&]() {
             const int orow = min(max(O, ra), rb - 1);
             const int ocol = min(max(col, 0), w_eff - 1);
             const size_t b = (size_t)(orow - y0) * width + ocol;
             mix_cur = make_float3(mix[3 * b], mix[3 * b + 1], mix[3 * b + 2]);
-        }
+        };
+        // CPT_DN_LATELOAD: 0 -- the output row's mix and the row a super-step ahead are loaded
+        // before the pair weights; 1 -- the mix after them; 2 -- both after them (fewer
+        // registers live through the pair weights, less time for the loads to land)
+        if (CPT_DN_LATELOAD < 1) load_mix();
         put(R, na, nn, nd, nvalid);
         const DnsPix me = ring(R, j);   // (this lane's own write: ordered)
-        load(R + DNR_WAVES, na, nn, nd, nvalid);
+        if (CPT_DN_LATELOAD < 2) load(R + DNR_WAVES, na, nn, nd, nvalid);
         __syncthreads();
         // ---- the 12 pair weights whose later pixel is (R, j) ---------------------------------------
         {
@@ -1321,17 +1358,47 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
             auto partner = [&](int k) {
                 return k < 2 ? ring(R, cl(j + k + 1)) : (k < 7 ? ring(R - 1, cl(j + k - 4)) : ring(R - 2, cl(j + k - 9)));
             };
+#if CPT_DN_SPLIT
+            // the 36 squared differences first (one partner's pixel live at a time), then the
+            // weights in batches of CPT_DN_BATCH
+            float c2[12], n2[12], p2[12];
+            uint32_t off_frame = 0;
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+                const DnsPix a = partner(k);
+                dn_pair_dist(a, me, c2[k], n2[k], p2[k]);
+                off_frame |= a.rgbv.w == 0.f ? 1u << k : 0u;
+            }
+            off_frame = me.rgbv.w == 0.f ? 0xfffu : off_frame;
+#pragma unroll
+            for (int k0 = 0; k0 < 12; k0 += CPT_DN_BATCH)
+                dn_dist_weights<CPT_DN_BATCH>(c2 + k0, n2 + k0, p2 + k0, w12 + k0, s_tab);
+#if CPT_DN_NOBRANCH
+#pragma unroll
+            for (int k = 0; k < 12; ++k) w12[k] = (off_frame >> k) & 1u ? 0.f : w12[k];
+#endif
+#else
 #pragma unroll
             for (int k0 = 0; k0 < 12; k0 += CPT_DN_BATCH) {
                 DnsPix a[CPT_DN_BATCH];
 #pragma unroll
                 for (int i = 0; i < CPT_DN_BATCH; ++i) a[i] = partner(k0 + i);
                 dn_pair_weights<CPT_DN_BATCH>(a, me, w12 + k0, s_tab);
+#if CPT_DN_NOBRANCH
+                // a pair with an out-of-frame pixel weighs +0 (the reference's c_w = n_w = p_w = 0),
+                // so the taps need no branch: such a pixel's ring colour is +0 as well
+#pragma unroll
+                for (int i = 0; i < CPT_DN_BATCH; ++i)
+                    w12[k0 + i] = a[i].rgbv.w != 0.f && me.rgbv.w != 0.f ? w12[k0 + i] : 0.f;
+#endif
             }
+#endif
             const int ws = (R + 4 * DNR_W_ROWS) % DNR_W_ROWS;
 #pragma unroll
             for (int k = 0; k < 12; ++k) W[ws][k][j] = w12[k];
         }
+        if (CPT_DN_LATELOAD >= 2) load(R + DNR_WAVES, na, nn, nd, nvalid);
+        if (CPT_DN_LATELOAD >= 1) load_mix();
         __syncthreads();
         // ---- output row O (wave-uniform condition; every lane computes, out_lane stores) --------
         v3 st_m = mk1(0.f);
@@ -1352,6 +1419,9 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
                 w_self = ws1[0];
             }
             v3 sum = mk1(0.f);
+#if CPT_DN_PACK
+            dn_f2 sum_xy = {0.f, 0.f};
+#endif
             float cum_w = 0.0f;
 #pragma unroll
             for (int i = 0; i < 5; ++i) {
@@ -1361,7 +1431,9 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
                     const float4 q = rgbv[(O + v + 4 * DNR_PIX_ROWS) % DNR_PIX_ROWS][jc + u];
                     float weight;
                     v3 ctmp;
-                    if (q.w == 0.f) {
+                    // (CPT_DN_NOBRANCH: an out-of-frame q holds colour +0 and its pair weight +0,
+                    // which is what the branch would give)
+                    if (!CPT_DN_NOBRANCH && q.w == 0.f) {
                         weight = 0.f * 0.f * 0.f;
                         ctmp = mk1(0.f);
                     } else {
@@ -1376,10 +1448,28 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
                         else if (v < 0) weight = W[wO][v == -1 ? 2 + (u + 2) : 7 + (u + 2)][jc];
                         else weight = W[v == 1 ? wO1 : wO2][v == 1 ? 2 + (-u + 2) : 7 + (-u + 2)][jc + u];
                     }
+#if CPT_DN_PACK
+                    // the same IEEE products and sums, x and y as one packed pair (v_pk_mul_f32 /
+                    // v_pk_add_f32 round each half like the scalar instruction)
+                    const float wk = weight * kernel5[i][jj];
+                    sum_xy = sum_xy + (dn_f2){wk, wk} * (dn_f2){ctmp.x, ctmp.y};
+                    sum.z = sum.z + wk * ctmp.z;
+                    cum_w += wk;
+#else
                     sum = sum + (weight * kernel5[i][jj]) * ctmp;
                     cum_w += weight * kernel5[i][jj];
+#endif
                 }
+#if CPT_DN_TAPFENCE
+                // keep each tap row's LDS reads after the previous row's (registers: the 25 taps'
+                // reads hoisted together hold 100 VGPRs)
+                __builtin_amdgcn_sched_barrier(0);
+#endif
             }
+#if CPT_DN_PACK
+            sum.x = sum_xy.x;
+            sum.y = sum_xy.y;
+#endif
             const v3 dn = sum / cum_w;
             const v3 clp = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),
                               __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of the display kernel (k_denoise_mix) across libraries: the display parity tests, then
+# A/B of the display kernel (k_denoise_rows) across libraries: the display parity tests, then
 # the per-pass DispatchRay timing (display_ms) of each.   usage: tools/ab_display.sh lib.so ...
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for lib in cpppathtracer_amd/libcpt.so "$@"; do
