@@ -83,16 +83,19 @@ def test_fullsize_wavefront_equals_megakernel(gpu, sky):
     np.testing.assert_array_equal(wf_rng, mk_rng)
 
 
-@pytest.mark.parametrize("config,spp", [("c2", 8), ("c3", 8), ("c4", 8)])
+@pytest.mark.parametrize("config,spp", [("c2", 8), ("c3", 8), ("c4", 8), ("c2", 64), ("c4", 64)])
 def test_fullsize_configs_timed_kernel_rows_match_oracle(gpu, oracle_mod, sky, config, spp):
     """BASELINE.json's C2 / C3 / C4 at full size through the instantiation bench.py times
     (ordered walk, cost schedule, no counters), 8 passes: six evenly spaced rows and their
-    XORWOW end states equal the oracle's bit for bit."""
+    XORWOW end states equal the oracle's bit for bit.  At 64 passes the long-chain take applies
+    (ranges shrinking with the ids left, cpt_tuning.hpp CPT_TAKE_TAPER): every pixel of the frame
+    must then have been taken exactly once, so every pass count is spp."""
     cfg = scenes.CONFIGS[config]
     W, H, depth = cfg["width"], cfg["height"], cfg["depth"]
     objs = scenes.SCENES[cfg["scene"]]()
     cam = _frame(gpu, sky, objs, W, H)
     acc, rng_end = _render(gpu, cam, spp, depth, ordered=True, schedule="cost")
+    np.testing.assert_array_equal(acc[:, 3], np.full(W * H, spp, np.float32))
     rows = np.linspace(0, H - 1, 6).astype(np.int32)
     rng = oracle_mod.init_rng(1234, W, rows, threads=16)
     o_acc, _, _, _ = oracle_mod.render(objs, cam, sky, rows, spp, depth, rng, threads=16)
