@@ -1,7 +1,7 @@
 """Wave-time breakdown of the megakernel from a CPT_STAMPS diagnostic build (cpt_stamps.hpp;
 never the timed library).
 
-    python tools/stamps.py [config] [spp] [--rows=a:b] [--width=W]   (CPT_LIB_PATH = the stamped build)
+    python tools/stamps.py [config] [spp] [--rows=a:b] [--width=W] [--schedule=cost|tiles|previous]   (CPT_LIB_PATH = the stamped build)
 
 Build the diagnostic library with
     python -c "from cpppathtracer_amd import build as b; b.build(out='build/diag/stamps.so', defines={'CPT_STAMPS': 1})"
@@ -23,7 +23,10 @@ cfg = scenes.CONFIGS[args[0] if args else "c4"]
 spp = int(args[1]) if len(args) > 1 else 8
 rows = None
 width = cfg["width"]
+schedule = "cost"
 for a in sys.argv[1:]:
+    if a.startswith("--schedule="):
+        schedule = a[11:]
     if a.startswith("--width="):
         width = int(a[8:])
     if a.startswith("--rows="):
@@ -38,7 +41,11 @@ cam = camera_get_copy(scenes.camera_for(width, cfg["height"]))
 r.render(cam, 1, cfg["depth"], sync=True, ordered=True)   # warm-up
 r.init_rng(1234)
 r.reset_stats()
-r.render(cam, spp, cfg["depth"], stats=True, sync=True, ordered=True, schedule="cost")
+if schedule == "previous":   # the DispatchRay loop's order: from a previous render's draws
+    r.render(cam, spp, cfg["depth"], sync=True, ordered=True, schedule="previous")
+    r.init_rng(1234)
+    r.reset_stats()
+r.render(cam, spp, cfg["depth"], stats=True, sync=True, ordered=True, schedule=schedule)
 c = r.diag_counters()
 st = dict(zip(["segments", "nodes", "prims", "hits", "misses"], r.raw_counters()[:5]))
 tot = sum(c[:8]) + c[11] + c[12]
