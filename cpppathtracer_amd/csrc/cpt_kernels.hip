@@ -832,14 +832,16 @@ __device__ __noinline__ float dn_weight_slow(float dist2) { return dn_weight_slo
 // The weight's short form (round 5): the same float, from a double approximation E' of
 // exp(-dist2/pi) that is within 2^-46.3 (relative) of the oracle's double E, rounded to float
 // only where that cannot matter:
-//  * E' = 2^-(n>>5) * T[n & 31] * P(r):  z = dist2 * 32/(pi ln2) (KN_HI + KN_LO), n = round(z)
-//    by the 1.5*2^52 shifter (n is t's low word), r = z - n in [-1/2, 1/2] (one fma against the
-//    exact product dist2 * KN_HI, then the low part), T[j] = 2^(-j/32) correctly rounded from the
-//    LDS table (cpt_dn_exp.hpp: 256 B, one bank pair per entry, so a wave's table read never
-//    conflicts), P = the degree-5 Taylor polynomial of 2^(-r/32) (truncation < 2^-48.7), and
-//    the 2^-(n>>5) applied to T's exponent field (T >= 1/2 and n>>5 <= 151: stays normal).  E'
-//    is within ~2^-48.5 of exp(-dist2/pi); the oracle's E = dm_exp(RN(-dist2/pi)) is within 2^-47
-//    (the quotient's rounding, |x| < 105.05) + 2^-52 of it.
+//  * E' = 2^-(n>>S) * T[n & (N-1)] * P(r) (cpt_dn_exp.hpp: N = 2^S table entries, P of degree
+//    DN_POLY_DEG):  z = dist2 * N/(pi ln2) (KN_HI + KN_LO), n = round(z) by the 1.5*2^52
+//    shifter (n is t's low word), r = z - n in [-1/2, 1/2] (one fma against the exact product
+//    dist2 * KN_HI, then the low part), T[j] = 2^(-j/N) correctly rounded from the LDS table,
+//    P = the Taylor polynomial of 2^(-r/N), and 2^-(n>>S) applied to T's exponent field
+//    (T >= 1/2 and n>>S <= 151: stays normal).  N = 1024, degree 3 (8 KB; truncation
+//    < 2^-50.7); round 5's first table was N = 32, degree 5 (256 B, conflict-free in LDS,
+//    truncation < 2^-48.7).  E' is within ~2^-48.5 of exp(-dist2/pi); the oracle's
+//    E = dm_exp(RN(-dist2/pi)) is within 2^-47 (the quotient's rounding, |x| < 105.05) + 2^-52
+//    of it.
 //  * Guard (dn_near_midpoint): if no float rounding boundary lies within 2^-44 E' of E' (its
 //    bits below float precision are not within 2^9 of the half-way pattern), every double in
 //    between rounds alike, E included (rounding is monotone), so (float)E' is the oracle's float.
@@ -858,8 +860,8 @@ __device__ __forceinline__ double dn_exp_short(float dist2, const double* __rest
     const uint32_t n = (uint32_t)__double2loint(t);
     double r = __builtin_fma(a, DN_KN_HI, -nd);
     r = __builtin_fma(a, DN_KN_LO, r);
-    double p = __builtin_fma(r, DN_C5, DN_C4);
-    p = __builtin_fma(r, p, DN_C3);
+    double p = DN_POLY_DEG >= 4 ? (DN_POLY_DEG >= 5 ? __builtin_fma(r, DN_C5, DN_C4) : DN_C4) : DN_C3;
+    if (DN_POLY_DEG >= 4) p = __builtin_fma(r, p, DN_C3);
     p = __builtin_fma(r, p, DN_C2);
     p = __builtin_fma(r, p, DN_C1);
     p = __builtin_fma(r, p, 1.0);
@@ -1002,7 +1004,7 @@ __global__ void __launch_bounds__(DN_THREADS, CPT_DN_MINWAVES) k_denoise_mix(con
                                                            float inv_idx) {
     __shared__ DnPix s_pix[DN_BY * DN_BX];
     __shared__ float s_wb[DN_THREADS * 12];   // backward weight k of tile pixel (ty, tx): w(p - d_k, p)
-    __shared__ double s_tab[DN_EXP_N];        // dn_weight's 2^(-j/32) table
+    __shared__ double s_tab[DN_EXP_N];        // dn_weight's 2^(-j/N) table
     // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs (each with its own
     // L2; MI355X_MICROARCH.md §Workgroup dispatch), so block b runs on the XCD of b mod 8.  Each
     // XCD takes one contiguous run of tiles in column-major order, so consecutive tiles on an

@@ -132,8 +132,8 @@ static float short_w(float d2, int t) {   /* cpt_kernels.hip dn_exp_short + dn_w
     const uint32_t n = (uint32_t)tb;
     double r = fma(a, cpt::DN_KN_HI, -nd);
     r = fma(a, cpt::DN_KN_LO, r);
-    double p = fma(r, cpt::DN_C5, cpt::DN_C4);
-    p = fma(r, p, cpt::DN_C3);
+    double p = cpt::DN_POLY_DEG >= 4 ? (cpt::DN_POLY_DEG >= 5 ? fma(r, cpt::DN_C5, cpt::DN_C4) : cpt::DN_C4) : cpt::DN_C3;
+    if (cpt::DN_POLY_DEG >= 4) p = fma(r, p, cpt::DN_C3);
     p = fma(r, p, cpt::DN_C2);
     p = fma(r, p, cpt::DN_C1);
     p = fma(r, p, 1.0);

@@ -1,11 +1,13 @@
-"""k_denoise_mix (Denoising + Mix, path_tracer.cu:177-254) on synthetic buffers written through
+"""The display kernel (k_denoise_rows; Denoising + Mix, path_tracer.cu:177-254) on synthetic buffers written through
 the checkpoint entry points (cpt_write_accum / cpt_write_aux), against the oracle's restatement
 on the same arrays, byte for byte.  The inputs reach every branch of the kernel's weight code:
 equal neighbours (exact zero differences: the skipped factors), colour differences up to 1e3
 (weights that round to 0, the >= 330 shortcut), depth differences (the depth factor the
 rendered frames never exercise: a18 makes depth the constant 1e30), infinite depths (inf - inf
 in the pair and the centre weight), accumulators with pass count 0, and frame sizes whose 16-aligned
-launch is narrower than the frame and than one 64-pixel tile.  Also: a render resumed from a
+launch is narrower than the frame and than one 64-pixel tile, one 60-column strip whose row runs
+are a single row each (64 x 200: more workgroups than rows per strip), a 16-pixel-wide column, and
+a 1000 x 16 frame (one super-step of rows).  Also: a render resumed from a
 checkpoint equals the uninterrupted render."""
 import numpy as np
 import pytest
@@ -36,7 +38,7 @@ def _buffers(W, H, seed):
     return acc, nrm, dep
 
 
-@pytest.mark.parametrize("W,H", [(200, 70), (1920 // 4, 36), (50, 40), (128, 16)])
+@pytest.mark.parametrize("W,H", [(200, 70), (1920 // 4, 36), (50, 40), (128, 16), (64, 200), (16, 300), (1000, 16), (333, 123)])
 def test_denoise_edges_match_oracle(gpu, oracle_mod, W, H):
     gpu.set_frame(W, H)
     for frame, seed in enumerate((1, 2, 3)):
