@@ -971,12 +971,6 @@ __device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b, 
 #ifndef CPT_DN_NOBRANCH        // 1: out-of-frame pairs weigh 0 in the weight ring, taps without a branch
 #define CPT_DN_NOBRANCH 1
 #endif
-#ifndef CPT_DN_SPLIT           // 1: all 36 squared differences before the weights (fewer live VGPRs)
-#define CPT_DN_SPLIT 0
-#endif
-#ifndef CPT_DN_TAPFENCE        // 1: a scheduling barrier between tap rows
-#define CPT_DN_TAPFENCE 0
-#endif
 #ifndef CPT_DN_LATELOAD        // where k_denoise_rows issues its global loads (see the loop)
 #define CPT_DN_LATELOAD 2
 #endif
@@ -1360,26 +1354,6 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
             auto partner = [&](int k) {
                 return k < 2 ? ring(R, cl(j + k + 1)) : (k < 7 ? ring(R - 1, cl(j + k - 4)) : ring(R - 2, cl(j + k - 9)));
             };
-#if CPT_DN_SPLIT
-            // the 36 squared differences first (one partner's pixel live at a time), then the
-            // weights in batches of CPT_DN_BATCH
-            float c2[12], n2[12], p2[12];
-            uint32_t off_frame = 0;
-#pragma unroll
-            for (int k = 0; k < 12; ++k) {
-                const DnsPix a = partner(k);
-                dn_pair_dist(a, me, c2[k], n2[k], p2[k]);
-                off_frame |= a.rgbv.w == 0.f ? 1u << k : 0u;
-            }
-            off_frame = me.rgbv.w == 0.f ? 0xfffu : off_frame;
-#pragma unroll
-            for (int k0 = 0; k0 < 12; k0 += CPT_DN_BATCH)
-                dn_dist_weights<CPT_DN_BATCH>(c2 + k0, n2 + k0, p2 + k0, w12 + k0, s_tab);
-#if CPT_DN_NOBRANCH
-#pragma unroll
-            for (int k = 0; k < 12; ++k) w12[k] = (off_frame >> k) & 1u ? 0.f : w12[k];
-#endif
-#else
 #pragma unroll
             for (int k0 = 0; k0 < 12; k0 += CPT_DN_BATCH) {
                 DnsPix a[CPT_DN_BATCH];
@@ -1394,7 +1368,6 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
                     w12[k0 + i] = a[i].rgbv.w != 0.f && me.rgbv.w != 0.f ? w12[k0 + i] : 0.f;
 #endif
             }
-#endif
             const int ws = (R + 4 * DNR_W_ROWS) % DNR_W_ROWS;
 #pragma unroll
             for (int k = 0; k < 12; ++k) W[ws][k][j] = w12[k];
@@ -1462,11 +1435,6 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
                     cum_w += weight * kernel5[i][jj];
 #endif
                 }
-#if CPT_DN_TAPFENCE
-                // keep each tap row's LDS reads after the previous row's (registers: the 25 taps'
-                // reads hoisted together hold 100 VGPRs)
-                __builtin_amdgcn_sched_barrier(0);
-#endif
             }
 #if CPT_DN_PACK
             sum.x = sum_xy.x;
