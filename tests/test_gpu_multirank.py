@@ -70,6 +70,11 @@ def test_ranks_stitch_equals_monolithic_and_oracle(oracle_mod, sky, W, H, SPP, w
         r.init_rng(scenes.DEFAULT_SEED)
         r.render(cam, SPP, DEPTH, ordered=True, schedule="cost", sync=True)
         mono = r.read_accum()
+    bad = np.any(fb.view(np.uint32) != mono.view(np.uint32), axis=1)
+    if bad.any():   # which side is wrong: rows, pass counts, and the stitched frame vs the oracle
+        ys = np.unique(np.nonzero(bad)[0] // W)
+        print(f"{bad.sum()} pixels differ in {ys.size} rows (first {ys[:16].tolist()}); pass counts "
+              f"stitched {np.unique(fb[bad, 3])[:8].tolist()} monolithic {np.unique(mono[bad, 3])[:8].tolist()}")
     np.testing.assert_array_equal(fb.view(np.uint32), mono.view(np.uint32))
     rows = np.arange(H, dtype=np.int32) if oracle_rows is None else np.array(oracle_rows, dtype=np.int32)
     orng = oracle_mod.init_rng(scenes.DEFAULT_SEED, W, rows, threads=8)
