@@ -64,9 +64,10 @@ def parse_args(argv=None):
                          "(CPT_TRAVERSAL_ORDERED, same closest hits; DESIGN.md §Ordered walk)")
     ap.add_argument("--consolidate", default="auto", choices=["auto", "on", "off"],
                     help="megakernel tail consolidation (auto: on for ranks of <= 4 pixels per lane, spp >= 512)")
-    ap.add_argument("--schedule", default="cost", choices=["cost", "tiles"],
+    ap.add_argument("--schedule", default="auto", choices=["auto", "cost", "tiles"],
                     help="megakernel pixel dequeue order: 8x8 tiles heaviest first from a pilot pass "
-                         "(CPT_SCHEDULE_COST), or tiles in row-major order")
+                         "(CPT_SCHEDULE_COST), or tiles in row-major order; auto: cost from 64 passes up "
+                         "(the pilot is one pass: a quarter of C1's 4-pass frame, C1 1043 vs 1556 Mpaths/s)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong (default): the config's image (C4: 1920x1080, the metric's resolution) at every N; "
                          "weak: pixels per GPU fixed (image grows by sqrt(N))")
@@ -282,6 +283,8 @@ def run(args):
     kernel_events = []
     ordered = args.walk == "ordered"
     schedule = args.schedule if args.path == "megakernel" else "tiles"
+    if schedule == "auto":
+        schedule = "cost" if spp >= 64 else "tiles"
     consolidate = {"auto": None, "on": True, "off": False}[args.consolidate]
     # the library's rule (cpt_capi.cpp): the LDS-walk megakernel consolidates its tail when the
     # rank holds at most 4 pixels per lane of the persistent grid (1024 lanes per CU) and the
