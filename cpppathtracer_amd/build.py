@@ -51,6 +51,11 @@ HIPCC_FLAGS = [
     # register pairs; at the 4-wave (128-VGPR) budget that spilled 9 registers to scratch
     # (C4: 1490 vs 1392 Mpaths/s without it; each lane's arithmetic is unchanged)
     "-fno-slp-vectorize",
+    # the machine scheduler tries several schedules per region and keeps the best one that holds
+    # the occupancy target (round 5, profiles/r05/ab_sched_strategy_*.log: C4 +0.3 to +3.6% in six
+    # interleaved pairs on two boxes, 1990 vs 1965 Mpaths/s on average; C2 / C3 / the display kernel unchanged;
+    # iterative-ilp: C4 +2%, C2 / C3 -2%; max-ilp / max-memory-clause / iterative-minreg: no gain)
+    "-mllvm", "-amdgpu-sched-strategy=iterative-maxocc",
 ] + os.environ.get("CPT_EXTRA_HIPCC_FLAGS", "").split()
 
 
@@ -69,7 +74,7 @@ def needs_build() -> bool:
     if not os.path.exists(LIB_PATH):
         return True
     t = os.path.getmtime(LIB_PATH)
-    deps = _extra_sources() + [h for h in HEADERS if os.path.exists(h)]
+    deps = _extra_sources() + [h for h in HEADERS if os.path.exists(h)] + [os.path.abspath(__file__)]   # (the flags)
     deps += [os.path.join(REPO_DIR, "include", "cpppathtracer", f)
              for f in os.listdir(os.path.join(REPO_DIR, "include", "cpppathtracer"))] if os.path.isdir(
         os.path.join(REPO_DIR, "include", "cpppathtracer")) else []
