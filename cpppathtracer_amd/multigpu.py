@@ -24,10 +24,19 @@ class TileGather:
         self.send = torch.zeros((self.max_rows * width, 4), dtype=torch.float32, device=device)
         self.gathered = torch.zeros((world * self.max_rows * width, 4), dtype=torch.float32, device=device)
         self.stitch_idx = torch.from_numpy(tiling.stitch_index(height, width, world)).to(device)
+        self.device = torch.device(device)
+        # the zero fills above run on torch's stream; the renderer's copy into `send` runs on the
+        # context's own stream, which nothing orders after them: finish them here
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
 
     def __call__(self, renderer):
         """The full (height, width, 4) fp32 framebuffer (rgb sums + pass count) after this
         rank's render: device copy of the local tile, all-gather, row stitch."""
+        # torch's stream may still read `send` (the previous frame's collective) when the context
+        # runs on a stream of its own: let it finish before the context overwrites the buffer
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
         renderer.copy_accum_device(self.send.data_ptr(), self.rows.size * self.width * 16)
         # the copy runs on the context's stream: wait for it before torch's stream reads `send`
         # (a no-op wait when the context launches on torch's stream, as bench.py sets up), and
