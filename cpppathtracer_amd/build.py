@@ -54,7 +54,9 @@ HIPCC_FLAGS = [
     # the machine scheduler tries several schedules per region and keeps the best one that holds
     # the occupancy target (round 5, profiles/r05/ab_sched_strategy_*.log: C4 +0.3 to +3.6% in six
     # interleaved pairs on two boxes, 1990 vs 1965 Mpaths/s on average; C2 / C3 / the display kernel unchanged;
-    # iterative-ilp: C4 +2%, C2 / C3 -2%; max-ilp / max-memory-clause / iterative-minreg: no gain)
+    # iterative-ilp: C4 +2%, C2 / C3 -2%; max-ilp / max-memory-clause / iterative-minreg: no gain).
+    # It spills a few VGPRs where the default did not (timed megakernel 8 B, k_denoise_rows 20 B),
+    # with no measurable cost (profiles/r05/ab_display_sched.log).
     "-mllvm", "-amdgpu-sched-strategy=iterative-maxocc",
 ] + os.environ.get("CPT_EXTRA_HIPCC_FLAGS", "").split()
 
