@@ -19,6 +19,14 @@
 
 #include "cpt_context.hpp"
 
+// CPT_SCHEDULE_PREVIOUS: renders between rebuilds of the heaviest-first tile order.  Round 5,
+// C4 DispatchRay loop, three interleaved rounds (profiles/r05/ab_dispatch_order_every.log): every
+// render 1.71-1.72 ms per pass, every 4th 1.66-1.68, every 8th 1.65-1.66; the 1-spp render itself
+// is unchanged (1.42-1.43), so the staler order costs nothing measurable.
+#ifndef CPT_PREV_ORDER_EVERY
+#define CPT_PREV_ORDER_EVERY 8
+#endif
+
 static_assert(sizeof(cpt_material) == 40, "cpt_material must match Material (40 B)");
 static_assert(sizeof(cpt_object) == 72, "cpt_object must match Object (72 B)");
 static_assert(sizeof(cpt_camera) == 136, "cpt_camera must match MotionalCamera (136 B)");
@@ -423,9 +431,11 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
             const size_t npix = (size_t)c->n_rows * c->width;
             if (c->prev_order_valid) p.tile_order = c->d_prev_order;
             if (!c->d_prev_d) HIP_TRY(c, hipMalloc((void**)&c->d_prev_d, npix * sizeof(uint32_t)));
-            if (!c->prev_d_valid)
+            if (!c->prev_d_valid) {
                 HIP_TRY(c, hipMemcpyAsync(c->d_prev_d, c->d_rng + 5 * npix, npix * sizeof(uint32_t),
                                           hipMemcpyDeviceToDevice, s));
+                c->prev_d_valid = true;   // the draws are counted from here
+            }
             prev_schedule = true;
         }
         if ((flags & CPT_SCHEDULE_COST) && spp > 0 && c->n_rows > 0) {
@@ -467,9 +477,11 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
         HIP_TRY(c, hipEventRecord(c->ev_main, s));
         HIP_TRY(c, cpt::launch_megakernel(p, (flags & CPT_RENDER_STATS) != 0, aux, s));
         HIP_TRY(c, hipEventRecord(c->ev_stop, s));
-        if (prev_schedule) {
+        if (prev_schedule && (!c->prev_order_valid || ++c->prev_since_order >= CPT_PREV_ORDER_EVERY)) {
             // the next render's order from this one's draws (after the timed events: the render's
-            // own time is the kernel's; the stream runs this before the caller's next work)
+            // own time is the kernel's; the stream runs this before the caller's next work).
+            // Refreshed every CPT_PREV_ORDER_EVERY renders: the draws then span those renders (the
+            // RNG's d word counts them all), and the order, a heuristic, costs ~65 us to rebuild
             const size_t n_tiles = (size_t)((c->width + 7) / 8) * ((c->n_rows + 7) / 8);
             const size_t bytes = cpt::tile_schedule_scratch_bytes(c->width, c->n_rows);
             if (c->cap_sched < bytes) {
@@ -483,6 +495,7 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
             HIP_TRY(c, cpt::launch_tile_order_from_draws(p, c->d_prev_d, c->d_sched, c->cap_sched, c->d_prev_order, s));
             c->prev_d_valid = true;
             c->prev_order_valid = true;
+            c->prev_since_order = 0;
         }
     }
     if (flags & CPT_PATH_WAVEFRONT) HIP_TRY(c, hipEventRecord(c->ev_stop, s));

@@ -101,6 +101,7 @@ struct cpt_ctx {
     uint32_t* d_prev_d = nullptr;
     uint32_t* d_prev_order = nullptr;
     bool prev_d_valid = false, prev_order_valid = false;
+    int prev_since_order = 0;   // renders since the CPT_SCHEDULE_PREVIOUS order was rebuilt
     uint4* d_resume = nullptr;          // tail consolidation: handed-over chains (5 x uint4 each)
     size_t cap_resume = 0;
     cpt::WfState wf{};           // wavefront path state (allocated on first use)
