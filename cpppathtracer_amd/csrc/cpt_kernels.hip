@@ -182,7 +182,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     for (;;) {
         stamps::lap(5);
         stamps::count(8);
-        if (cons && !retiring && level > 0 && exhausted && vq[3] == 0u && vq[2] <= level * 256u) retiring = true;
+        if (cons && !retiring && level > 0 && exhausted && vq[3] == 0u && vq[2] <= level * (uint32_t)CPT_CONS_RETIRE_PER_LEVEL) retiring = true;
         bool begin = false;   // a lane took a chain: start its next pass
         // ---- take handed-over chains into idle lanes (consolidation) ---------------------
         if (cons && !retiring && exhausted) {

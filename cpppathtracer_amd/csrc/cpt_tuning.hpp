@@ -85,6 +85,15 @@ namespace cpt {
 #define CPT_TAKE_TAPER 4
 #endif
 
+// Tail consolidation: a level-L wave (L = 1..3) retires, handing its chains to the keepers, once
+// the workgroup's live chains are at most L x this (each retiring wave hands over <= 64 chains, so
+// the slab's 3 x 256 slots hold every hand-over whatever the value).  Round 5 rehearsal, C5 N = 8
+// slowest rank (profiles/r05/reh_cons_retire_threshold.log): 128 / 192 / 384 2574-2582 ms against
+// 2521 / 2551 at 256; 384 also costs C4 N = 8 (380 vs 322 ms).
+#ifndef CPT_CONS_RETIRE_PER_LEVEL
+#define CPT_CONS_RETIRE_PER_LEVEL 256
+#endif
+
 // The LDS kernels' cold walks out of line (cpt_path.hpp trace_cold).
 #ifndef CPT_COLD_NOINLINE
 #define CPT_COLD_NOINLINE 0
