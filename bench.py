@@ -338,10 +338,10 @@ def run(args):
         walk_counts = st
         if ordered:
             fb_ref = torch.empty((npix_local, 4), dtype=torch.float32, device=dev)
-            r.copy_accum_device(fb_ref.data_ptr(), npix_local * 16)
+            r.copy_accum_device(fb_ref.data_ptr(), npix_local * 16, torch.cuda.current_stream().cuda_stream)
             walk_counts = count_pass(True)
             fb_ord = torch.empty_like(fb_ref)
-            r.copy_accum_device(fb_ord.data_ptr(), npix_local * 16)
+            r.copy_accum_device(fb_ord.data_ptr(), npix_local * 16, torch.cuda.current_stream().cuda_stream)
             torch.cuda.synchronize()
             nd = (fb_ref.view(torch.int32) != fb_ord.view(torch.int32)).any(dim=1).sum().to(torch.float64)
             if use_pg:

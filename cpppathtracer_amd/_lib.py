@@ -46,7 +46,7 @@ PROTOTYPES = {
     "cpt_read_aux": (_I, [_P, _P, _P]),
     "cpt_write_accum": (_I, [_P, _P]),
     "cpt_write_aux": (_I, [_P, _P, _P]),
-    "cpt_copy_accum_device": (_I, [_P, _P, _SZ]),
+    "cpt_copy_accum_device": (_I, [_P, _P, _SZ, _P]),
     "cpt_gather_rows": (_I, [_P, _P]),
     "cpt_last_gather_mode": (_I, [_P, _P, _P]),
     "cpt_set_debug_gather": (_I, [_P, _I]),
@@ -64,10 +64,11 @@ PROTOTYPES = {
     "cpt_host_register": (_I, [_P, _SZ]),
     "cpt_host_unregister": (_I, [_P]),
     "cpt_denoise_mix_band": (_I, [_P, _U32, _I, _I, _P]),
-    "cpt_copy_bgra_device": (_I, [_P, _P, _SZ]),
+    "cpt_copy_bgra_device": (_I, [_P, _P, _SZ, _P]),
     "cpt_last_display_ms": (_I, [_P, _P]),
     "cpt_reset_display": (_I, [_P]),
-    "cpt_read_mix": (_I, [_P, _P]),
+    "cpt_display_band": (_I, [_P, _P, _P]),
+    "cpt_read_mix": (_I, [_P, _P, _SZ]),
     "cpt_math_batch": (_I, [_P, _I, _P, _P, _P, _SZ]),
     "cpt_selftest_qdiv": (_I, [_P, _I, _U64, _U64, _P, _I]),
     "cpt_set_debug_consolidation": (_I, [_P, _U32, _I, _I]),

@@ -160,6 +160,8 @@ int cpt_create(int device, cpt_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&c->ev_dn1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_gathered, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_caller, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_copied, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 128 * sizeof(unsigned long long));   // [64..128) execdiag
     if (e == hipSuccess) e = hipMalloc((void**)&c->d_work, 64);   // [0] dequeue counter, [4] error word
     if (e == hipSuccess) e = hipMemset(c->d_work, 0, 64);
@@ -203,6 +205,8 @@ int cpt_destroy(cpt_ctx* c) {
     if (c->ev_dn1) (void)hipEventDestroy(c->ev_dn1);
     if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
     if (c->ev_gathered) (void)hipEventDestroy(c->ev_gathered);
+    if (c->ev_caller) (void)hipEventDestroy(c->ev_caller);
+    if (c->ev_copied) (void)hipEventDestroy(c->ev_copied);
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
@@ -711,13 +715,30 @@ int cpt_write_aux(cpt_ctx* c, const float* normal3, const float* depth) {
     return CPT_OK;
 }
 
-int cpt_copy_accum_device(cpt_ctx* c, void* dst, size_t bytes) {
+// A device-to-device copy from one of the context's buffers, ordered against the caller's stream
+// without a host wait: the context's stream waits for the work queued on `caller` so far (a fill
+// of dst, a collective still reading it), copies, and `caller` waits for the copy (the collective
+// queued next reads the copied bytes).  Nothing to order when caller is the context's stream.
+static int copy_ordered(cpt_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t caller) {
+    HIP_TRY(c, hipSetDevice(c->device));
+    const bool other = caller != c->stream();
+    if (other) {
+        HIP_TRY(c, hipEventRecord(c->ev_caller, caller));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream(), c->ev_caller, 0));
+    }
+    if (bytes) HIP_TRY(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream()));
+    if (other) {
+        HIP_TRY(c, hipEventRecord(c->ev_copied, c->stream()));
+        HIP_TRY(c, hipStreamWaitEvent(caller, c->ev_copied, 0));
+    }
+    return CPT_OK;
+}
+
+int cpt_copy_accum_device(cpt_ctx* c, void* dst, size_t bytes, void* caller_stream) {
     if (!c || (!dst && bytes)) return CPT_ERR_INVALID_ARG;
     size_t have = (size_t)c->n_rows * c->width * sizeof(float4);
     if (bytes > have) return fail(c, CPT_ERR_INVALID_ARG, "cpt_copy_accum_device: %zu > %zu bytes", bytes, have);
-    HIP_TRY(c, hipSetDevice(c->device));
-    if (bytes) HIP_TRY(c, hipMemcpyAsync(dst, c->d_accum, bytes, hipMemcpyDeviceToDevice, c->stream()));
-    return CPT_OK;
+    return copy_ordered(c, dst, c->d_accum, bytes, (hipStream_t)caller_stream);
 }
 
 int cpt_get_stats(cpt_ctx* c, cpt_stats* out) {
@@ -900,20 +921,28 @@ int cpt_denoise_mix_band(cpt_ctx* c, uint32_t cur_sample_idx, int y0, int y1, ui
     return denoise_band(c, cur_sample_idx, y0, y1, bgra_host, 0);
 }
 
-int cpt_copy_bgra_device(cpt_ctx* c, void* device_dst, size_t bytes) {
+int cpt_copy_bgra_device(cpt_ctx* c, void* device_dst, size_t bytes, void* caller_stream) {
     if (!c || !device_dst) return CPT_ERR_INVALID_ARG;
     if (!c->d_bgra) return fail(c, CPT_ERR_STATE, "cpt_copy_bgra_device: no display frame yet");
     const size_t have = (size_t)(c->band_y1 - c->band_y0) * c->width * 4;
     if (bytes > have) return fail(c, CPT_ERR_INVALID_ARG, "cpt_copy_bgra_device: %zu bytes requested, band holds %zu", bytes, have);
-    HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, hipMemcpyAsync(device_dst, c->d_bgra, bytes, hipMemcpyDeviceToDevice, c->stream()));
+    return copy_ordered(c, device_dst, c->d_bgra, bytes, (hipStream_t)caller_stream);
+}
+
+int cpt_display_band(const cpt_ctx* c, int* y0, int* y1) {
+    if (!c || !y0 || !y1) return CPT_ERR_INVALID_ARG;
+    *y0 = c->d_mix ? c->band_y0 : 0;
+    *y1 = c->d_mix ? c->band_y1 : 0;
     return CPT_OK;
 }
 
-int cpt_read_mix(cpt_ctx* c, float* rgb) {
+int cpt_read_mix(cpt_ctx* c, float* rgb, size_t capacity) {
     if (!c || !rgb) return CPT_ERR_INVALID_ARG;
     if (!c->d_mix) return fail(c, CPT_ERR_STATE, "cpt_read_mix: no display frame yet");
     const size_t rows = (size_t)(c->band_y1 - c->band_y0);
+    if (capacity < rows * c->width * 3)
+        return fail(c, CPT_ERR_INVALID_ARG, "cpt_read_mix: %zu floats given, the band [%d, %d) holds %zu", capacity,
+                    c->band_y0, c->band_y1, rows * c->width * 3);
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipMemcpyAsync(rgb, c->d_mix, rows * c->width * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream()));
     return sync_checked(c);
@@ -989,7 +1018,7 @@ int cpt_measure_read_bandwidth(cpt_ctx* c, size_t bytes, int iters, float* gbps)
 }
 
 int cpt_selftest_qdiv(cpt_ctx* c, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len) {
-    if (!c || !out || out_len < 1 || which < 0 || which > 7) return CPT_ERR_INVALID_ARG;
+    if (!c || !out || out_len < 1 || which < 0 || which > 11) return CPT_ERR_INVALID_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     unsigned long long* d = nullptr;
     HIP_TRY(c, hipMalloc((void**)&d, out_len * sizeof(unsigned long long)));

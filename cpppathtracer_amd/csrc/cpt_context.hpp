@@ -28,7 +28,7 @@ struct cpt_ctx {
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     hipEvent_t ev_main = nullptr;   // after the cost schedule's pilot: the dominant kernel(s) only
     bool have_timing = false;
-    hipEvent_t ev_dn0 = nullptr, ev_dn1 = nullptr;   // around the last display kernel (k_denoise_mix)
+    hipEvent_t ev_dn0 = nullptr, ev_dn1 = nullptr;   // around the last display kernel (k_denoise_rows)
     bool have_dn_timing = false;
     std::string err;
 
@@ -129,6 +129,8 @@ struct cpt_ctx {
     uint64_t frame_gen = 0;           // process-unique id of the current frame layout (cpt_set_frame)
     hipEvent_t ev_ready = nullptr;    // a gather's source: its queued work
     hipEvent_t ev_gathered = nullptr; // a gather's destination: the stitch done
+    hipEvent_t ev_caller = nullptr;   // a device copy's caller stream: its queued work
+    hipEvent_t ev_copied = nullptr;   // a device copy: done on the context's stream
     // consolidation test hooks (cpt_set_debug_consolidation)
     uint32_t dbg = 0;
     bool force_staged_gather = false;   // gather test hook (cpt_set_debug_gather)

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "cpt_fm_tables.hpp"
+
 namespace cpt {
 
 // ------------------------------------------------------------------------------------
@@ -324,6 +326,123 @@ __device__ __forceinline__ float div255(uint32_t k) {
 }
 
 }  // namespace dm
+
+// ------------------------------------------------------------------------------------
+// Short forms of the BSDF lobe's transcendentals (round 6).  Each returns a double within
+// ~2^-49 (relative) of the exact function, and `ok`: whether that double rounds to the same
+// float as every double within 2^-43 of it -- then it rounds like the full dm:: sequence
+// (itself within ~2^-51 of the exact value), and the caller uses it; otherwise (about 1 in
+// 2^18 inputs, and every input outside the form's domain) the caller runs the dm:: sequence.
+// Tables and constants: cpt_fm_tables.hpp (tools/make_fastmath_tables.py).  Checked on the
+// device against the dm:: sequence for every float of the lobe's domain
+// (test_gpu_parity.py::test_lobe_*_exhaustive) and restated on the host against the oracle
+// (tests/test_fastmath.py).
+// ------------------------------------------------------------------------------------
+namespace fm {
+
+__device__ const double g_log_tab[2 * FM_LOG_N] = CPT_FM_LOG_TABLE_INIT;        // {c_i, -ln c_i}
+__device__ const double g_exp_tab[FM_EXP_N] = CPT_FM_EXP_TABLE_INIT;             // 2^(j/N)
+__device__ const double g_sc_tab[2 * (2 * FM_SC_N + 1)] = CPT_FM_SC_TABLE_INIT;  // {sin, cos}(k pi/32)
+
+// d rounds to float like every double within 2^-43 |d| of it, and 2^-126 <= |d| < 2: d's 29
+// bits below float precision (all in its low word) are not within 2^10 double ulps of the
+// half-way pattern 2^28 (2^10 ulps >= 2^-43 |d|).  NaN, inf, 0 and subnormal floats fail.
+__device__ __forceinline__ bool sure_f32(double d) {
+    const uint32_t lo = (uint32_t)__double2loint(d), hi = (uint32_t)__double2hiint(d) & 0x7fffffffu;
+    const int dm_ = (int)(lo & 0x1fffffffu) - (1 << 28);
+    return hi - 0x38100000u < 0x07f00000u && (dm_ >= 1024 || dm_ <= -1024);
+}
+
+// pow(x, y) for a float x in [2^-126, 1] and 0 < y <= 1 with |y ln x| <= 2 (else ok = false):
+// x = 2^e m, ln x = e ln2 - ln c_i + log1p(m c_i - 1) (i: m's top 7 fraction bits; the fma is
+// exact), then exp(t) = 2^(n/128) P(s) with n = round(t 128/ln2) (the 1.5 2^52 shifter: n is
+// the low word), s the remainder in units of ln2/128, 2^(n>>7) applied to T_j's exponent field.
+__device__ __forceinline__ double pow_unit(float x, double y, bool& ok) {
+    const uint32_t ux = __float_as_uint(x);
+    const int e = (int)(ux >> 23) - 127;
+    const uint32_t i = (ux >> 16) & (uint32_t)(FM_LOG_N - 1);
+    const double m = (double)__uint_as_float((ux & 0x007fffffu) | 0x3f800000u);
+    const double c = g_log_tab[2 * i], lnc = g_log_tab[2 * i + 1];
+    const double r = __builtin_fma(m, c, -1.0);
+    double q = __builtin_fma(r, dm::kc(FM_L6), dm::kc(FM_L5));
+    q = __builtin_fma(r, q, dm::kc(FM_L4));
+    q = __builtin_fma(r, q, dm::kc(FM_L3));
+    q = __builtin_fma(r, q, dm::kc(FM_L2));
+    const double lp = __builtin_fma(r * r, q, r);
+    const double t = y * __builtin_fma((double)e, dm::kc(FM_LN2), lnc + lp);
+    constexpr double SHIFT = 0x1.8p52;
+    const double tt = __builtin_fma(t, dm::kc(FM_KN_HI), SHIFT);
+    const double nd = tt - SHIFT;
+    const int n = __double2loint(tt);
+    double s = __builtin_fma(t, dm::kc(FM_KN_HI), -nd);
+    s = __builtin_fma(t, dm::kc(FM_KN_LO), s);
+    double p = __builtin_fma(s, dm::kc(FM_E4), dm::kc(FM_E3));
+    p = __builtin_fma(s, p, dm::kc(FM_E2));
+    p = __builtin_fma(s, p, dm::kc(FM_E1));
+    p = __builtin_fma(s, p, 1.0);
+    const double T = g_exp_tab[n & (FM_EXP_N - 1)];
+    const double Ts = __hiloint2double(__double2hiint(T) + (int)((uint32_t)(n >> 7) << 20), __double2loint(T));
+    const double d = Ts * p;
+    ok = ux - 0x00800000u <= 0x3f000000u && y > 0.0 && y <= 1.0 && t >= -2.0 && sure_f32(d);
+    return d;
+}
+
+// sin and cos of a float phi in [0, 2 pi] (else ok = false): k = round(phi 32/pi), r = phi -
+// k pi/32 (two-part constant: exact to ~2^-53 |r|), sin phi = S_k cos r + C_k sin r, cos phi =
+// C_k cos r - S_k sin r; the table's zeros and ones are exact, so each result near a zero of sin
+// or cos is the short series of r alone.
+__device__ __forceinline__ void sincos_2pi(float phi, double& s, double& c, bool& ok) {
+    const double x = (double)phi;
+    constexpr double SHIFT = 0x1.8p52;
+    const double tt = __builtin_fma(x, dm::kc(FM_SC_K), SHIFT);
+    const double kd = tt - SHIFT;
+    const uint32_t k = (uint32_t)__double2loint(tt);
+    double r = __builtin_fma(-kd, dm::kc(FM_SC_P1), x);
+    r = __builtin_fma(-kd, dm::kc(FM_SC_P2), r);
+    const double r2 = r * r;
+    double ps = __builtin_fma(r2, dm::kc(FM_S7), dm::kc(FM_S5));
+    ps = __builtin_fma(r2, ps, dm::kc(FM_S3));
+    const double sr = __builtin_fma(r * r2, ps, r);
+    double pc = __builtin_fma(r2, dm::kc(FM_C6), dm::kc(FM_C4));
+    pc = __builtin_fma(r2, pc, dm::kc(FM_C2));
+    const double cr = __builtin_fma(r2, pc, 1.0);
+    const uint32_t kk = k <= (uint32_t)(2 * FM_SC_N) ? k : 0u;
+    const double S = g_sc_tab[2 * kk], C = g_sc_tab[2 * kk + 1];
+    s = __builtin_fma(S, cr, C * sr);
+    c = __builtin_fma(C, cr, -(S * sr));
+    ok = phi >= 0.0f && phi <= 6.28318548f && sure_f32(s) && sure_f32(c);
+}
+
+}  // namespace fm
+
+// The lobe's z = (float)pow(x_1, inv_alpha) (material.cu:24,45,78,85,104): Diffuse's exponent 1/2
+// as sqrtf -- (float)dm::pow(x, 0.5) == sqrtf(x) for every float x in [2^-42, 1] (x_1 >= 2^-33),
+// checked on the host against the oracle and on the device (test_lobe_pow_exhaustive); the
+// other exponents through fm::pow_unit, the dm:: sequence where its guard fails.
+#ifndef CPT_FM_LOBE   // A/B: 0 = the full dm:: sequences in the lobe (round 5)
+#define CPT_FM_LOBE 1
+#endif
+__device__ __forceinline__ float lobe_pow(float x, double y) {
+    if (!CPT_FM_LOBE) return (float)dm::pow((double)x, y);
+    if (y == 0.5 && x >= 0x1p-42f) return sqrt_nn(x);
+    bool ok;
+    const double d = fm::pow_unit(x, y, ok);
+    float z = (float)d;
+    if (__builtin_expect(!ok, 0)) z = (float)dm::pow((double)x, y);
+    return z;
+}
+
+// sinf / cosf of the lobe's phi = (float)(2 pi x_2) in [0, 2 pi] (material.cu:26-27,47-48):
+// fm::sincos_2pi, dm::sincosf_ where its guard fails (test_lobe_sincos_exhaustive).
+__device__ __forceinline__ void lobe_sincos(float phi, float* s_out, float* c_out) {
+    if (!CPT_FM_LOBE) return dm::sincosf_(phi, s_out, c_out);
+    double s, c;
+    bool ok;
+    fm::sincos_2pi(phi, s, c, ok);
+    *s_out = (float)s;
+    *c_out = (float)c;
+    if (__builtin_expect(!ok, 0)) dm::sincosf_(phi, s_out, c_out);
+}
 
 // ------------------------------------------------------------------------------------
 // cuRAND XORWOW (curand_kernel.h restated).  State lives in registers

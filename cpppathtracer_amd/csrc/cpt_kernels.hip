@@ -785,11 +785,12 @@ __global__ void k_rng_pixels(const uint32_t* __restrict__ rowmats, const uint32_
 // offsets outside [0, W'*H') get zero weight (path_tracer.cu:205-216); reproduced here.
 // Weights min(exp(-d2/M_PI), 1.0) are double (path_tracer.cu:215-222).  Mix:
 // mix = lerp(mix, clamp(denoised, 0, 1), 1/cur_sample_idx); bytes 0..2 = 255.99*(b, g, r)
-// (path_tracer.cu:241-254); the alpha byte is not written.
+// (path_tracer.cu:241-254); the alpha byte, which the reference never writes (its frame copies
+// whatever the device buffer held, :251-253,303), is stored as 0 in one 32-bit store.
 // ======================================================================================
 // min(exp(-(dist2) / M_PI), 1.0) in double, stored to float (path_tracer.cu:224,228,231), for a
 // float dist2 -- the oracle's dm_exp(-(double)dist2 / REF_PI), branch-free.  The SLOW form (round 4),
-// now only the fallback of dn_weight below near a float rounding boundary:
+// now only the fallback of dn_weights below near a float rounding boundary:
 //  * dist2 in (0, 330): x = -dist2/pi in (-105.05, 0), the quotient from dm::div_pi's sequence
 //    (correctly rounded: it depends only on dist2's significand, and every significand is
 //    checked); then dm::exp's own steps -- k, the two-part reduction, the Horner polynomial --
@@ -882,268 +883,39 @@ __device__ __forceinline__ bool dn_near_midpoint(double e) {
     return !normal_f || (d < 512 && d > -512);
 }
 
-__device__ __forceinline__ float dn_weight(float dist2, const double* __restrict__ tab) {
-#ifdef CPT_DN_SLOW_ONLY   // A/B: the round-4 weight
-    return dn_weight_slow(dist2);
-#endif
-    const double e = dn_exp_short(dist2, tab);
-    float f = (float)e;
-    if (dn_near_midpoint(e) && !(dist2 >= 330.0f)) f = dn_weight_slow(dist2);   // near a midpoint, or NaN
-    f = dist2 >= 330.0f ? 0.0f : f;
-    return dist2 == 0.0f ? 1.0f : f;
-}
-
-// Exhaustive check of dn_weight against dn_weight_slow (cpt_selftest_qdiv which = 6: mismatches
-// over the float patterns [0, n); which = 7: how many of them take the fallback).
-__global__ void k_selftest_dn_weight(int which, uint64_t n, unsigned long long* out, int out_len) {
+// Exhaustive checks of the lobe's short transcendentals (cpt_device.hpp lobe_pow, lobe_sincos)
+// against the full dm:: sequences, over the float patterns [0, n) (cpt_selftest_qdiv):
+// which = 8: lobe_pow(x, y) vs (float)dm::pow(x, y), y = the double with the bits of `seed`;
+// 9: how many x take pow's fallback; 10: lobe_sincos(phi) vs dm::sincosf_(phi), both results;
+// 11: how many phi take sincos' fallback.  out[0] = count, out[1..] = some of the floats' bits.
+__global__ void k_selftest_fm(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const double y = __longlong_as_double((long long)seed);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const float d = __uint_as_float((uint32_t)i);
+        const float x = __uint_as_float((uint32_t)i);
         bool flag;
-        if (which == 6) {
-            const float w = dn_weight(d, g_dn_exp_table), w_ref = dn_weight_slow(d);
-            flag = __float_as_uint(w) != __float_as_uint(w_ref);
+        if (which == 8) {
+            flag = __float_as_uint(lobe_pow(x, y)) != __float_as_uint((float)dm::pow((double)x, y));
+        } else if (which == 9) {
+            bool ok;
+            (void)fm::pow_unit(x, y, ok);
+            flag = !ok && !(y == 0.5 && x >= 0x1p-42f);
+        } else if (which == 10) {
+            float s, c, s_ref, c_ref;
+            lobe_sincos(x, &s, &c);
+            dm::sincosf_(x, &s_ref, &c_ref);
+            flag = __float_as_uint(s) != __float_as_uint(s_ref) || __float_as_uint(c) != __float_as_uint(c_ref);
         } else {
-            const double e = dn_exp_short(d, g_dn_exp_table);
-            flag = dn_near_midpoint(e) && !(d >= 330.0f);
+            double s, c;
+            bool ok;
+            fm::sincos_2pi(x, s, c, ok);
+            flag = !ok;
         }
         if (flag) {
             unsigned long long k = atomicAdd(&out[0], 1ull);
-            if ((long long)k + 1 < out_len) out[k + 1] = ((unsigned long long)__float_as_uint(d) << 32);
+            if ((long long)k + 1 < out_len) out[k + 1] = ((unsigned long long)__float_as_uint(x) << 32);
         }
     }
-}
-
-// The 5x5 stencil's pair weight c_w * n_w * p_w between pixels a and b (path_tracer.cu:
-// 219-233).  Every factor is a function of the difference of the two pixels' values, squared:
-// a - b = -(b - a) exactly, so w(a, b) == w(b, a) bit for bit, and each unordered pair needs
-// evaluating once.  The depth factor is exactly 1 when the depths are equal (a18: depth is the
-// constant 1e30), so its exp only runs where it can differ.
-struct DnPix { float r, g, b, nx, ny, nz, d, pad; };
-
-// The pair weight c_w * n_w * p_w (left to right) from the two pixels' values: colour
-// difference squared, normal difference squared clamped at 0 in double, depth difference
-// squared (path_tracer.cu:219-233).  Inlined where the pairs are independent (the forward
-// pairs of a pixel, unrolled), so several exp sequences are in flight per lane.
-__device__ __forceinline__ float dn_pair_weight(const DnPix& a, const DnPix& b, const double* __restrict__ tab) {
-    v3 t = mk(a.r, a.g, a.b) - mk(b.r, b.g, b.b);
-    const float c_w = dn_weight(dot(t, t), tab);
-    t = mk(a.nx, a.ny, a.nz) - mk(b.nx, b.ny, b.nz);
-    const double dn = (double)dot(t, t);
-    const float dnf = (float)(dn > 0.0 ? dn : 0.0);
-    // equal normals (a flat surface: the floor's are exactly (0, +-1, 0)) give n_w = 1; the
-    // branch skips the sequence when no lane of the wave needs it
-    float n_w = 1.0f;
-    if (dnf != 0.0f) n_w = dn_weight(dnf, tab);
-    const float dd = (a.d - b.d) * (a.d - b.d);
-    // a18: the depths are the constant 1e30, so dd == 0 and p_w == 1 (dn_weight(0)) almost
-    // always; the branch skips the sequence when no lane of the wave needs it
-    float p_w = 1.0f;
-    if (dd != 0.0f) p_w = dn_weight(dd, tab);
-    return c_w * n_w * p_w;
-}
-
-// One band of output rows [y0, y1) of the W' x H' launch (W' = 16 floor(W/16), H' likewise).
-// accum/normal/depth hold the context's rows row0, row0 + 1, ... (row stride `width`): the
-// band plus a 3-row halo, enough for every neighbour the linear-offset stencil reaches (x +- 2
-// wraps into the adjacent row, so rows y - 3 .. y + 3).  mix and out hold the band's rows
-// only.  The full frame is the band [0, H') with row0 = 0.
-//
-// A block of DN_TX x DN_TY threads takes a tile of as many output pixels, one per thread.  The
-// stencil indexes neighbours by the LINEAR offset v*W' + u, so tile row r's neighbours are the
-// linear run r*W' + x0 - 2 .. r*W' + x0 + DN_TX + 1 (which wraps into the adjacent image row
-// exactly as the reference does); the block stages those runs for rows ty0 - 2 .. ty0 + DN_TY
-// + 1 in LDS once, as radiance (accumulator / pass count), normal and depth.  Pair weights are
-// evaluated once per unordered pair: each pixel evaluates its 12 forward neighbours (dy > 0, or
-// dy = 0 and dx > 0; unrolled, kept in registers) and hands each weight to the neighbour when
-// that one is in the tile; the pairs whose first pixel lies outside the tile (the halo band
-// above and beside it) are evaluated by the whole block from a flat list.  Each pixel then
-// sums its 25 taps in the reference's order.
-#ifndef CPT_DN_TY
-#define CPT_DN_TY 8
-#endif
-#ifndef CPT_DN_TILE          // 1: the round-4 tile kernel above (A/B); 0: k_denoise_rows (the default)
-#define CPT_DN_TILE 0
-#endif
-#ifndef CPT_DNR_BLOCKS_PER_CU  // k_denoise_rows' blocks per CU (8-wave blocks: 70 KB of LDS each; four waves per SIMD)
-#define CPT_DNR_BLOCKS_PER_CU 2
-#endif
-#ifndef CPT_DN_NOBRANCH        // 1: out-of-frame pairs weigh 0 in the weight ring, taps without a branch
-#define CPT_DN_NOBRANCH 1
-#endif
-#ifndef CPT_DN_LATELOAD        // where k_denoise_rows issues its global loads (see the loop)
-#define CPT_DN_LATELOAD 2
-#endif
-#ifndef CPT_DN_PACK            // 1: the taps' x/y products and sums as packed f32 pairs
-#define CPT_DN_PACK 0
-#endif
-typedef float dn_f2 __attribute__((ext_vector_type(2)));
-#ifndef CPT_DN_BATCH           // pair weights evaluated together (a divisor of 12)
-#define CPT_DN_BATCH 4
-#endif
-constexpr int DN_TX = 64, DN_TY = CPT_DN_TY, DN_THREADS = DN_TX * DN_TY;
-constexpr int DN_BX = DN_TX + 4, DN_BY = DN_TY + 4;   // staged box (2-pixel halo each side)
-// forward offsets (dx, dy), k = 0..11: dy = 0, dx = 1, 2; dy = 1, dx = -2..2; dy = 2, dx = -2..2
-__host__ __device__ constexpr int dn_fdx(int k) { return k < 2 ? k + 1 : ((k - 2) % 5) - 2; }
-__host__ __device__ constexpr int dn_fdy(int k) { return k < 2 ? 0 : (k < 7 ? 1 : 2); }
-
-#ifndef CPT_DN_MINWAVES
-#define CPT_DN_MINWAVES 1
-#endif
-__global__ void __launch_bounds__(DN_THREADS, CPT_DN_MINWAVES) k_denoise_mix(const float4* __restrict__ accum,
-                                                           const float* __restrict__ normal,
-                                                           const float* __restrict__ depth, float* __restrict__ mix,
-                                                           uint8_t* __restrict__ out, uint8_t* __restrict__ out_host,
-                                                           int width, int row0, int y0, int y1, int w_eff, int h_eff,
-                                                           float inv_idx) {
-    __shared__ DnPix s_pix[DN_BY * DN_BX];
-    __shared__ float s_wb[DN_THREADS * 12];   // backward weight k of tile pixel (ty, tx): w(p - d_k, p)
-    __shared__ double s_tab[DN_EXP_N];        // dn_weight's 2^(-j/N) table
-    // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs (each with its own
-    // L2; MI355X_MICROARCH.md §Workgroup dispatch), so block b runs on the XCD of b mod 8.  Each
-    // XCD takes one contiguous run of tiles in column-major order, so consecutive tiles on an
-    // XCD are vertical neighbours whose 2-row halos overlap in that XCD's L2.
-    const int tiles_x = (w_eff + DN_TX - 1) / DN_TX, tiles_y = (y1 - y0 + DN_TY - 1) / DN_TY;
-    const int n_tiles = tiles_x * tiles_y;
-    const int xcd = (int)(blockIdx.x & 7u), k_on = (int)(blockIdx.x >> 3);
-    const int per = n_tiles >> 3, extra = n_tiles & 7;
-    const int t = xcd * per + min(xcd, extra) + k_on;   // bijective over [0, n_tiles)
-    const int tile_x = t / tiles_y, tile_y = t - tile_x * tiles_y;
-    const int x0 = tile_x * DN_TX, ty0 = y0 + tile_y * DN_TY;
-    const int tw = min(DN_TX, w_eff - x0), th = min(DN_TY, y1 - ty0);   // the tile's extent
-    const int limit = w_eff * h_eff;
-    // ---- stage the box: linear pixels (ty0 - 2 + by) * W' + x0 - 2 + bx ----------------
-    for (int i = threadIdx.x; i < DN_EXP_N; i += DN_THREADS) s_tab[i] = g_dn_exp_table[i];
-#pragma unroll 1
-    for (int i = threadIdx.x; i < DN_BY * DN_BX; i += DN_THREADS) {
-        const int by = i / DN_BX, bx = i - by * DN_BX;
-        const int L = (ty0 - 2 + by) * w_eff + x0 - 2 + bx;
-        DnPix q;
-        if (L >= 0 && L < limit) {
-            const int yy = L / w_eff;
-            const int px = (yy - row0) * width + (L - yy * w_eff);
-            const float4 a = accum[px];
-            const v3 c = a.w != 0.f ? mk(a.x, a.y, a.z) / a.w : mk(a.x, a.y, a.z);
-            q.r = c.x; q.g = c.y; q.b = c.z;
-            q.nx = normal[3 * px]; q.ny = normal[3 * px + 1]; q.nz = normal[3 * px + 2];
-            q.d = depth[px];
-            q.pad = 1.f;   // in [0, W'H')
-        } else {   // outside [0, W'H'): weight 0 (never read as a value)
-            q.r = q.g = q.b = q.nx = q.ny = q.nz = q.d = 0.f;
-            q.pad = 0.f;
-        }
-        s_pix[i] = q;
-    }
-    __syncthreads();
-    auto box = [&](int tx, int ty) -> const DnPix& { return s_pix[(ty + 2) * DN_BX + tx + 2]; };
-    auto in_tile = [&](int tx, int ty) { return tx >= 0 && tx < tw && ty >= 0 && ty < th; };
-    const int ty = threadIdx.x / DN_TX, tx = threadIdx.x - ty * DN_TX;
-    const bool mine = in_tile(tx, ty);
-    const DnPix p = box(tx, ty);
-    // ---- this pixel's forward pairs (independent: unrolled) ------------------------------
-    float wf[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const int dx = dn_fdx(k), dy = dn_fdy(k);
-        const DnPix& q = box(tx + dx, ty + dy);
-        wf[k] = (mine && q.pad != 0.f) ? dn_pair_weight(p, q, s_tab) : 0.f;
-        if (mine && in_tile(tx + dx, ty + dy)) s_wb[((ty + dy) * DN_TX + tx + dx) * 12 + k] = wf[k];
-    }
-    // ---- pairs (s, t = s + d) with t in the tile and s outside it ------------------------
-    // For offset k the targets are the first dy rows of the tile (all columns), then in the
-    // other rows the |dx| columns at the side the offset reaches in from.
-    {
-        int total = 0;
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const int adx = dn_fdx(k) < 0 ? -dn_fdx(k) : dn_fdx(k), rows_top = min(dn_fdy(k), th);
-            total += rows_top * tw + (th - rows_top) * min(adx, tw);
-        }
-#pragma unroll 1
-        for (int e = threadIdx.x; e < total; e += DN_THREADS) {
-            int k = 0, r = e, dx = 0, dy = 0, adx = 0, rows_top = 0, cols = 0;
-            for (;; ++k) {
-                dx = dn_fdx(k);
-                dy = dn_fdy(k);
-                adx = dx < 0 ? -dx : dx;
-                rows_top = min(dy, th);
-                cols = min(adx, tw);
-                const int cnt = rows_top * tw + (th - rows_top) * cols;
-                if (r < cnt) break;
-                r -= cnt;
-            }
-            int sx, sy;
-            if (r < rows_top * tw) {
-                sy = r / tw;
-                sx = r - sy * tw;
-            } else {
-                r -= rows_top * tw;
-                sy = rows_top + r / cols;
-                const int c = r - (sy - rows_top) * cols;
-                sx = dx > 0 ? c : tw - adx + c;
-            }
-            const DnPix& t = box(sx, sy);
-            const DnPix& sp = box(sx - dx, sy - dy);
-            s_wb[(sy * DN_TX + sx) * 12 + k] = sp.pad != 0.f ? dn_pair_weight(sp, t, s_tab) : 0.f;
-        }
-    }
-    __syncthreads();
-    if (!mine) return;
-    // ---- the 25 taps in the reference's order (i = dx outer, j = dy inner) -----------------
-    constexpr float kernel5[5][5] = {{1.f, 4.f, 7.f, 4.f, 1.f},
-                                     {4.f, 16.f, 26.f, 16.f, 4.f},
-                                     {7.f, 26.f, 41.f, 26.f, 7.f},
-                                     {4.f, 16.f, 26.f, 16.f, 4.f},
-                                     {1.f, 4.f, 7.f, 4.f, 1.f}};
-    // the centre tap: w(p, p) = 1 for finite values (every squared difference is 0); the
-    // general expression otherwise (inf - inf, NaN)
-    const bool finite = __builtin_isfinite(p.r) && __builtin_isfinite(p.g) && __builtin_isfinite(p.b) &&
-                        __builtin_isfinite(p.nx) && __builtin_isfinite(p.ny) && __builtin_isfinite(p.nz) &&
-                        __builtin_isfinite(p.d);
-    float w_self = 1.0f;
-    if (!finite) w_self = dn_pair_weight(p, p, s_tab);
-    const float* wb = s_wb + threadIdx.x * 12;
-    v3 sum = mk1(0.f);
-    float cum_w = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-#pragma unroll
-        for (int jj = 0; jj < 5; ++jj) {
-            const int dx = i - 2, dy = jj - 2;
-            const DnPix& q = box(tx + dx, ty + dy);
-            float weight;
-            v3 ctmp;
-            if (q.pad == 0.f) {
-                weight = 0.f * 0.f * 0.f;
-                ctmp = mk1(0.f);
-            } else {
-                ctmp = mk(q.r, q.g, q.b);
-                if (dx == 0 && dy == 0) weight = w_self;
-                else if (dy > 0 || (dy == 0 && dx > 0)) weight = wf[dy == 0 ? dx - 1 : 2 + 5 * (dy - 1) + dx + 2];
-                else weight = wb[dy == 0 ? -dx - 1 : 2 + 5 * (-dy - 1) - dx + 2];
-            }
-            sum = sum + (weight * kernel5[i][jj]) * ctmp;
-            cum_w += weight * kernel5[i][jj];
-        }
-    }
-    const v3 dn = sum / cum_w;
-    const v3 cl = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),
-                     __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));
-    const int y = ty0 + ty, x = x0 + tx;
-    const size_t bself = (size_t)(y - y0) * width + x;   // this pixel in the band's mix / out
-    v3 m = mk(mix[3 * bself], mix[3 * bself + 1], mix[3 * bself + 2]);
-    m = m + inv_idx * (cl - m);      // lerp(a, b, t) = a + t*(b-a) (helper_math.h:1154-1157)
-    mix[3 * bself] = m.x;
-    mix[3 * bself + 1] = m.y;
-    mix[3 * bself + 2] = m.z;
-    // bytes 0..2 = 255.99 * (b, g, r); the alpha byte is never written by the reference and stays
-    // the buffer's zero here (one 32-bit store)
-    const uint32_t bgr = (uint32_t)(uint8_t)(255.99f * m.z) | ((uint32_t)(uint8_t)(255.99f * m.y) << 8) |
-                         ((uint32_t)(uint8_t)(255.99f * m.x) << 16);
-    reinterpret_cast<uint32_t*>(out)[bself] = bgr;
-    // the caller's pinned host frame (the callback's buffer), written over PCIe by the kernel
-    // itself instead of a copy after it
-    if (out_host) reinterpret_cast<uint32_t*>(out_host)[bself] = bgr;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1158,7 +930,7 @@ __global__ void __launch_bounds__(DN_THREADS, CPT_DN_MINWAVES) k_denoise_mix(con
 //    every unordered pair of the stencil exactly once -- into a ring of weights in LDS.
 //  * Row O = R - 2 is then complete: each output lane sums its 25 taps in the reference's order,
 //    reading the weights it needs from the ring (its own, or a neighbour's at lane j +- u).
-// The weights are evaluated in batches of CPT_DN_BATCH with one wave-wide fallback branch
+// The weights are evaluated in batches of DN_BATCH with one wave-wide fallback branch
 // (dn_weight's guard), so the batch's exp chains overlap.
 constexpr int DNS_LANES = 64, DNS_COLS = 60;
 struct DnsPix { float4 rgbv; float4 nd; };   // (r, g, b, valid), (nx, ny, nz, depth)
@@ -1238,7 +1010,31 @@ __device__ __forceinline__ void dn_pair_weights(const DnsPix a[N], const DnsPix&
     dn_dist_weights<N>(c2, n2, p2, out, tab);
 }
 
-// The block's n waves (CPT_DNR_WAVES, 8) share the window: per super-step they take the next n
+// Exhaustive check of the shipped weight (dn_weights: the short exp, the guard, the slow form's
+// fallback and the 0 / >= 330 shortcuts) against dn_weight_slow (cpt_selftest_qdiv which = 6:
+// mismatches over the float patterns [0, n); which = 7: how many of them take the fallback).
+__global__ void k_selftest_dn_weight(int which, uint64_t n, unsigned long long* out, int out_len) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float d = __uint_as_float((uint32_t)i);
+        bool flag;
+        if (which == 6) {
+            float w;
+            dn_weights<1>(&d, &w, g_dn_exp_table);
+            const float w_ref = dn_weight_slow(d);
+            flag = __float_as_uint(w) != __float_as_uint(w_ref);
+        } else {
+            const double e = dn_exp_short(d, g_dn_exp_table);
+            flag = dn_near_midpoint(e) && !(d >= 330.0f);
+        }
+        if (flag) {
+            unsigned long long k = atomicAdd(&out[0], 1ull);
+            if ((long long)k + 1 < out_len) out[k + 1] = ((unsigned long long)__float_as_uint(d) << 32);
+        }
+    }
+}
+
+// The block's n waves (DNR_WAVES, 8) share the window: per super-step they take the next n
 // rows, wave w row R = B + w:
 //   1. each wave writes its row into the block's pixel ring (2n + 4 rows: the n new ones never
 //      alias the n + 4 the other waves may still be reading for their taps);
@@ -1257,18 +1053,19 @@ __device__ __forceinline__ void dn_pair_weights(const DnsPix a[N], const DnsPix&
 // Loads are issued unconditionally (out-of-frame lanes read a valid address and discard it)
 // and the stores sit in a branch-free tail (lanes without an output pixel store to `sink`), so
 // the next row's wait does not drain a branch's worth of stores.
-#ifndef CPT_DNR_WAVES
-#define CPT_DNR_WAVES 8
-#endif
-#ifndef CPT_DNR_MINWAVES   // __launch_bounds__ waves per SIMD (3: <= 168 VGPRs; 4: <= 128)
-#define CPT_DNR_MINWAVES 4
-#endif
 // pixel ring: the n new rows + the 2n + 4 - n rows a slower wave may still read for its taps;
 // weight ring: the n + 2 rows the taps of one super-step read
-constexpr int DNR_WAVES = CPT_DNR_WAVES, DNR_PIX_ROWS = 2 * DNR_WAVES + 4, DNR_W_ROWS = DNR_WAVES + 2;
+constexpr int DNR_WAVES = 8, DNR_PIX_ROWS = 2 * DNR_WAVES + 4, DNR_W_ROWS = DNR_WAVES + 2;
+constexpr int DNR_MINWAVES = 4;        // __launch_bounds__ waves per SIMD (<= 128 VGPRs)
+constexpr int DNR_BLOCKS_PER_CU = 2;   // 8-wave blocks, 4 waves per SIMD
+constexpr int DN_BATCH = 4;            // pair weights evaluated together (a divisor of 12)
+// the static LDS of one block: the exp table, the two pixel rings, the weight ring (78 KB)
+constexpr size_t DNR_LDS_BYTES = DN_EXP_N * sizeof(double) + 2 * DNR_PIX_ROWS * DNS_LANES * sizeof(float4) +
+                                 DNR_W_ROWS * 12 * DNS_LANES * sizeof(float);
+static_assert(DNR_LDS_BYTES * DNR_BLOCKS_PER_CU <= 160 * 1024, "k_denoise_rows: blocks per CU exceed the CU's LDS");
 
 template <bool HOST>
-__global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_denoise_rows(
+__global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, DNR_MINWAVES) k_denoise_rows(
     const float4* __restrict__ accum, const float* __restrict__ normal, const float* __restrict__ depth,
     float* __restrict__ mix, uint8_t* __restrict__ out, uint8_t* __restrict__ out_host, float4* __restrict__ sink,
     int width, int row0, int ctx_rows, int y0, int y1, int w_eff, int h_eff, int n_strips, int per_strip, float inv_idx) {
@@ -1299,7 +1096,9 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
         // the window reads up to a super-step past the rows it outputs; rows the context does not
         // hold (a band's, cpt_denoise_mix_band) are never a tap or pair of an output pixel, so
         // they read address 0 like the out-of-frame ones
-        const bool held = yy - row0 >= 0 && yy - row0 < ctx_rows;
+        // (lanes past 2 W' of a narrow frame -- 16 or 32 columns -- wrap beyond the next row:
+        // never a tap either, and outside the row they must not address)
+        const bool held = yy - row0 >= 0 && yy - row0 < ctx_rows && xx >= 0 && xx < w_eff;
         const size_t px = valid && held ? (size_t)(yy - row0) * width + xx : (size_t)0;
         a = accum[px];
         n = make_float3(normal[3 * px], normal[3 * px + 1], normal[3 * px + 2]);
@@ -1338,42 +1137,37 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
             const size_t b = (size_t)(orow - y0) * width + ocol;
             mix_cur = make_float3(mix[3 * b], mix[3 * b + 1], mix[3 * b + 2]);
         };
-        // CPT_DN_LATELOAD: 0 -- the output row's mix and the row a super-step ahead are loaded
-        // before the pair weights; 1 -- the mix after them; 2 -- both after them (fewer
-        // registers live through the pair weights, less time for the loads to land)
-        if (CPT_DN_LATELOAD < 1) load_mix();
         put(R, na, nn, nd, nvalid);
         const DnsPix me = ring(R, j);   // (this lane's own write: ordered)
-        if (CPT_DN_LATELOAD < 2) load(R + DNR_WAVES, na, nn, nd, nvalid);
         __syncthreads();
         // ---- the 12 pair weights whose later pixel is (R, j) ---------------------------------------
         {
             float w12[12];
             // partner k of the 12 (k = 0, 1: (R, j + k + 1); 2..6: (R - 1, j + k - 4); 7..11:
-            // (R - 2, j + k - 9)), in batches of CPT_DN_BATCH pairs
+            // (R - 2, j + k - 9)), in batches of DN_BATCH pairs
             auto partner = [&](int k) {
                 return k < 2 ? ring(R, cl(j + k + 1)) : (k < 7 ? ring(R - 1, cl(j + k - 4)) : ring(R - 2, cl(j + k - 9)));
             };
 #pragma unroll
-            for (int k0 = 0; k0 < 12; k0 += CPT_DN_BATCH) {
-                DnsPix a[CPT_DN_BATCH];
+            for (int k0 = 0; k0 < 12; k0 += DN_BATCH) {
+                DnsPix a[DN_BATCH];
 #pragma unroll
-                for (int i = 0; i < CPT_DN_BATCH; ++i) a[i] = partner(k0 + i);
-                dn_pair_weights<CPT_DN_BATCH>(a, me, w12 + k0, s_tab);
-#if CPT_DN_NOBRANCH
+                for (int i = 0; i < DN_BATCH; ++i) a[i] = partner(k0 + i);
+                dn_pair_weights<DN_BATCH>(a, me, w12 + k0, s_tab);
                 // a pair with an out-of-frame pixel weighs +0 (the reference's c_w = n_w = p_w = 0),
                 // so the taps need no branch: such a pixel's ring colour is +0 as well
 #pragma unroll
-                for (int i = 0; i < CPT_DN_BATCH; ++i)
+                for (int i = 0; i < DN_BATCH; ++i)
                     w12[k0 + i] = a[i].rgbv.w != 0.f && me.rgbv.w != 0.f ? w12[k0 + i] : 0.f;
-#endif
             }
             const int ws = (R + 4 * DNR_W_ROWS) % DNR_W_ROWS;
 #pragma unroll
             for (int k = 0; k < 12; ++k) W[ws][k][j] = w12[k];
         }
-        if (CPT_DN_LATELOAD >= 2) load(R + DNR_WAVES, na, nn, nd, nvalid);
-        if (CPT_DN_LATELOAD >= 1) load_mix();
+        // the row a super-step ahead and the output row's mix, loaded after the pair weights (fewer
+        // registers live through them)
+        load(R + DNR_WAVES, na, nn, nd, nvalid);
+        load_mix();
         __syncthreads();
         // ---- output row O (wave-uniform condition; every lane computes, out_lane stores) --------
         v3 st_m = mk1(0.f);
@@ -1394,9 +1188,6 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
                 w_self = ws1[0];
             }
             v3 sum = mk1(0.f);
-#if CPT_DN_PACK
-            dn_f2 sum_xy = {0.f, 0.f};
-#endif
             float cum_w = 0.0f;
 #pragma unroll
             for (int i = 0; i < 5; ++i) {
@@ -1404,42 +1195,23 @@ __global__ void __launch_bounds__(DNS_LANES * DNR_WAVES, CPT_DNR_MINWAVES) k_den
                 for (int jj = 0; jj < 5; ++jj) {
                     const int u = i - 2, v = jj - 2;
                     const float4 q = rgbv[(O + v + 4 * DNR_PIX_ROWS) % DNR_PIX_ROWS][jc + u];
+                    // (an out-of-frame q holds colour +0 and its pair weight +0: the reference's
+                    // zero weight, without a branch)
+                    const v3 ctmp = mk(q.x, q.y, q.z);
+                    // where the pair (O, j) - (O + v, j + u) was stored: same row -- by the lane
+                    // of its left pixel, as that pixel's forward pair |u| - 1; other rows -- by
+                    // the lane of its lower pixel, at index 2 + dx + 2 (dy 1) or 7 + dx + 2
+                    // (dy 2), dx = upper column - lower column
                     float weight;
-                    v3 ctmp;
-                    // (CPT_DN_NOBRANCH: an out-of-frame q holds colour +0 and its pair weight +0,
-                    // which is what the branch would give)
-                    if (!CPT_DN_NOBRANCH && q.w == 0.f) {
-                        weight = 0.f * 0.f * 0.f;
-                        ctmp = mk1(0.f);
-                    } else {
-                        ctmp = mk(q.x, q.y, q.z);
-                        // where the pair (O, j) - (O + v, j + u) was stored: same row -- by the lane
-                        // of its left pixel, as that pixel's forward pair |u| - 1; other rows -- by
-                        // the lane of its lower pixel, at index 2 + dx + 2 (dy 1) or 7 + dx + 2
-                        // (dy 2), dx = upper column - lower column
-                        if (u == 0 && v == 0) weight = w_self;
-                        else if (v == 0 && u > 0) weight = W[wO][u - 1][jc];
-                        else if (v == 0) weight = W[wO][-u - 1][jc + u];
-                        else if (v < 0) weight = W[wO][v == -1 ? 2 + (u + 2) : 7 + (u + 2)][jc];
-                        else weight = W[v == 1 ? wO1 : wO2][v == 1 ? 2 + (-u + 2) : 7 + (-u + 2)][jc + u];
-                    }
-#if CPT_DN_PACK
-                    // the same IEEE products and sums, x and y as one packed pair (v_pk_mul_f32 /
-                    // v_pk_add_f32 round each half like the scalar instruction)
-                    const float wk = weight * kernel5[i][jj];
-                    sum_xy = sum_xy + (dn_f2){wk, wk} * (dn_f2){ctmp.x, ctmp.y};
-                    sum.z = sum.z + wk * ctmp.z;
-                    cum_w += wk;
-#else
+                    if (u == 0 && v == 0) weight = w_self;
+                    else if (v == 0 && u > 0) weight = W[wO][u - 1][jc];
+                    else if (v == 0) weight = W[wO][-u - 1][jc + u];
+                    else if (v < 0) weight = W[wO][v == -1 ? 2 + (u + 2) : 7 + (u + 2)][jc];
+                    else weight = W[v == 1 ? wO1 : wO2][v == 1 ? 2 + (-u + 2) : 7 + (-u + 2)][jc + u];
                     sum = sum + (weight * kernel5[i][jj]) * ctmp;
                     cum_w += weight * kernel5[i][jj];
-#endif
                 }
             }
-#if CPT_DN_PACK
-            sum.x = sum_xy.x;
-            sum.y = sum_xy.y;
-#endif
             const v3 dn = sum / cum_w;
             const v3 clp = mk(__builtin_fmaxf(0.f, __builtin_fminf(dn.x, 1.f)), __builtin_fmaxf(0.f, __builtin_fminf(dn.y, 1.f)),
                               __builtin_fmaxf(0.f, __builtin_fminf(dn.z, 1.f)));
@@ -1472,35 +1244,26 @@ hipError_t launch_denoise_mix(const float4* accum, const float* normal, const fl
     const int w_eff = 16 * (width / 16), h_eff = 16 * (height / 16);
     if (w_eff == 0 || h_eff == 0 || y1 <= y0) return hipSuccess;
     const float inv_idx = 1.f / float(cur_sample_idx);
-#if !CPT_DN_TILE
-    {
-        static int cus2[64] = {0};
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (dev < 0 || dev >= 64) dev = 0;
-        if (cus2[dev] == 0) {
-            int n = 0;
-            if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-            cus2[dev] = n;
-        }
-        const int n_strips = (w_eff + DNS_COLS - 1) / DNS_COLS;
-        const int rows = y1 - y0;
-        int per_strip = (cus2[dev] * CPT_DNR_BLOCKS_PER_CU + n_strips - 1) / n_strips;
-        per_strip = per_strip < 1 ? 1 : (per_strip > rows ? rows : per_strip);
-        const unsigned blocks = (unsigned)(n_strips * per_strip);
-        if (out_host)
-            hipLaunchKernelGGL(k_denoise_rows<true>, dim3(blocks), dim3(DNS_LANES * DNR_WAVES), 0, stream, accum, normal, depth, mix,
-                               out, out_host, sink, width, row0, ctx_rows, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
-        else
-            hipLaunchKernelGGL(k_denoise_rows<false>, dim3(blocks), dim3(DNS_LANES * DNR_WAVES), 0, stream, accum, normal, depth, mix,
-                               out, out_host, sink, width, row0, ctx_rows, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
-        return hipGetLastError();
+    static int cus2[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (cus2[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus2[dev] = n;
     }
-#else
-    const int n_tiles = ((w_eff + DN_TX - 1) / DN_TX) * ((y1 - y0 + DN_TY - 1) / DN_TY);
-    hipLaunchKernelGGL(k_denoise_mix, dim3((unsigned)n_tiles), dim3(DN_THREADS), 0, stream, accum, normal, depth, mix, out, out_host, width,
-                       row0, y0, y1, w_eff, h_eff, inv_idx);
-#endif
+    const int n_strips = (w_eff + DNS_COLS - 1) / DNS_COLS;
+    const int rows = y1 - y0;
+    int per_strip = (cus2[dev] * DNR_BLOCKS_PER_CU + n_strips - 1) / n_strips;
+    per_strip = per_strip < 1 ? 1 : (per_strip > rows ? rows : per_strip);
+    const unsigned blocks = (unsigned)(n_strips * per_strip);
+    if (out_host)
+        hipLaunchKernelGGL(k_denoise_rows<true>, dim3(blocks), dim3(DNS_LANES * DNR_WAVES), 0, stream, accum, normal, depth, mix,
+                           out, out_host, sink, width, row0, ctx_rows, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
+    else
+        hipLaunchKernelGGL(k_denoise_rows<false>, dim3(blocks), dim3(DNS_LANES * DNR_WAVES), 0, stream, accum, normal, depth, mix,
+                           out, out_host, sink, width, row0, ctx_rows, y0, y1, w_eff, h_eff, n_strips, per_strip, inv_idx);
     return hipGetLastError();
 }
 
@@ -1850,7 +1613,9 @@ hipError_t launch_stream_read(const float4* p, size_t n, float* out, int grid, h
 
 hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len,
                                 hipStream_t stream) {
-    if (which >= 6)
+    if (which >= 8)
+        hipLaunchKernelGGL(k_selftest_fm, dim3(8192), dim3(256), 0, stream, which, n, seed, out, out_len);
+    else if (which >= 6)
         hipLaunchKernelGGL(k_selftest_dn_weight, dim3(8192), dim3(256), 0, stream, which, n, out, out_len);
     else
         hipLaunchKernelGGL(k_selftest_qdiv, dim3(4096), dim3(256), 0, stream, which, n, seed, out, out_len);

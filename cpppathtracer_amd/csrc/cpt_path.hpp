@@ -999,13 +999,14 @@ __device__ __forceinline__ v3 to_world(v3 a, v3 N) {
     return (a.x * B + a.y * C) + a.z * N;
 }
 
-// z = pow(x1, inv_alpha) (double pow), r = sqrtf(1 - z^2), phi = (float)(2*M_PI*x2).
+// z = pow(x1, inv_alpha) (double pow), r = sqrtf(1 - z^2), phi = (float)(2*M_PI*x2); pow, sinf
+// and cosf through their short forms (cpt_device.hpp lobe_pow, lobe_sincos: the same floats).
 __device__ __forceinline__ v3 lobe(float x_1, float x_2, double inv_alpha) {
-    float z = (float)dm::pow((double)x_1, inv_alpha);
+    float z = lobe_pow(x_1, inv_alpha);
     float r = sqrt_nn(1.0f - z * z);
     float phi = (float)(2 * REF_PI * (double)x_2);
     float sp, cp;
-    dm::sincosf_(phi, &sp, &cp);
+    lobe_sincos(phi, &sp, &cp);
     return mk(r * cp, r * sp, z);
 }
 

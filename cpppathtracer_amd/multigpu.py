@@ -25,23 +25,18 @@ class TileGather:
         self.gathered = torch.zeros((world * self.max_rows * width, 4), dtype=torch.float32, device=device)
         self.stitch_idx = torch.from_numpy(tiling.stitch_index(height, width, world)).to(device)
         self.device = torch.device(device)
-        # the zero fills above run on torch's stream; the renderer's copy into `send` runs on the
-        # context's own stream, which nothing orders after them: finish them here
-        if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
 
     def __call__(self, renderer):
         """The full (height, width, 4) fp32 framebuffer (rgb sums + pass count) after this
-        rank's render: device copy of the local tile, all-gather, row stitch."""
-        # torch's stream may still read `send` (the previous frame's collective) when the context
-        # runs on a stream of its own: let it finish before the context overwrites the buffer
-        if self.device.type == "cuda":
-            torch.cuda.current_stream(self.device).synchronize()
-        renderer.copy_accum_device(self.send.data_ptr(), self.rows.size * self.width * 16)
-        # the copy runs on the context's stream: wait for it before torch's stream reads `send`
-        # (a no-op wait when the context launches on torch's stream, as bench.py sets up), and
-        # surface any device error of the render
-        renderer.synchronize()
+        rank's render: device copy of the local tile, all-gather, row stitch.
+
+        The copy is ordered against torch's current stream on the device, with no host wait
+        (cpt_copy_accum_device): it starts after the work queued there so far -- the zero fills
+        above, the previous frame's collective still reading `send` -- and the all-gather queued
+        next reads the copied tile.  Device errors of the render surface at the next
+        synchronising call (the renderer's, or torch.cuda.synchronize for the frame)."""
+        stream = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+        renderer.copy_accum_device(self.send.data_ptr(), self.rows.size * self.width * 16, stream)
         if self.world == 1 and not dist.is_initialized():
             return self.send.view(self.max_rows, self.width, 4)[: self.height]
         # with a process group the collective runs at any world size, 1 included (bench.py under

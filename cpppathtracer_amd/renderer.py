@@ -231,8 +231,12 @@ class Renderer:
         d = np.ascontiguousarray(depth, dtype=np.float32).reshape(self.npix)
         self._check(self._L.cpt_write_aux(self._ctx, _p(n), _p(d)))
 
-    def copy_accum_device(self, device_ptr, nbytes):
-        self._check(self._L.cpt_copy_accum_device(self._ctx, ctypes.c_void_p(device_ptr), nbytes))
+    def copy_accum_device(self, device_ptr, nbytes, stream):
+        """Device copy of the accumulator, ordered against the caller's HIP stream (a handle,
+        e.g. torch.cuda.current_stream().cuda_stream; 0 = the null stream) with no host wait:
+        it starts after the work queued there so far and that stream's next work sees it."""
+        self._check(self._L.cpt_copy_accum_device(self._ctx, ctypes.c_void_p(device_ptr), nbytes,
+                                                  ctypes.c_void_p(stream or None)))
 
     def gather_rows(self, src):
         """cpt_gather_rows: place the rows Renderer `src` rendered into this frame (row tiling)."""
@@ -307,7 +311,6 @@ class Renderer:
         frame on the device (no host write; returns None): the display kernel's device-only time."""
         if not host:
             self._check(self._L.cpt_denoise_mix(self._ctx, cur_sample_idx, None))
-            self._band_rows = None
             return None
         if out is None:
             out = np.zeros((self.height, self.width, 4), dtype=np.uint8)
@@ -322,14 +325,20 @@ class Renderer:
         if not out.flags["C_CONTIGUOUS"] or not out.flags["WRITEABLE"]:
             raise ValueError("denoise_mix: `out` must be C-contiguous and writeable")
         self._check(self._L.cpt_denoise_mix(self._ctx, cur_sample_idx, _p(out)))
-        self._band_rows = None
         return out
 
+    def display_band(self):
+        """The output rows (y0, y1) the display buffers hold (cpt_display_band)."""
+        y0, y1 = ctypes.c_int(0), ctypes.c_int(0)
+        self._check(self._L.cpt_display_band(self._ctx, ctypes.byref(y0), ctypes.byref(y1)))
+        return y0.value, y1.value
+
     def read_mix(self):
-        """The Mix running mean of the display band: [(y1 - y0) * width, 3] float32."""
-        rows = self._band_rows if getattr(self, "_band_rows", None) else 16 * (self.height // 16)
-        out = np.zeros((rows * self.width, 3), dtype=np.float32)
-        self._check(self._L.cpt_read_mix(self._ctx, _p(out)))
+        """The Mix running mean of the display band: [(y1 - y0) * width, 3] float32, sized from
+        the library's own band (a failed band switch cannot leave it stale)."""
+        y0, y1 = self.display_band()
+        out = np.zeros(((y1 - y0) * self.width, 3), dtype=np.float32)
+        self._check(self._L.cpt_read_mix(self._ctx, _p(out), out.size))
         return out
 
     def last_display_ms(self) -> float:
@@ -345,11 +354,13 @@ class Renderer:
         out = np.zeros((y1 - y0, self.width, 4), dtype=np.uint8) if host else None
         self._check(self._L.cpt_denoise_mix_band(self._ctx, cur_sample_idx, int(y0), int(y1),
                                                  _p(out) if host else None))
-        self._band_rows = int(y1 - y0)
         return out
 
-    def copy_bgra_device(self, device_ptr, nbytes):
-        self._check(self._L.cpt_copy_bgra_device(self._ctx, ctypes.c_void_p(device_ptr), nbytes))
+    def copy_bgra_device(self, device_ptr, nbytes, stream):
+        """Device copy of the display band's BGRA8 rows, ordered against `stream` as
+        copy_accum_device."""
+        self._check(self._L.cpt_copy_bgra_device(self._ctx, ctypes.c_void_p(device_ptr), nbytes,
+                                                 ctypes.c_void_p(stream or None)))
 
     def reset_display(self):
         self._check(self._L.cpt_reset_display(self._ctx))

@@ -265,8 +265,14 @@ int cpt_read_aux(cpt_ctx* ctx, float* normal3, float* depth); /* either may be N
  * With cpt_write_rng, a render (and the display path) resumes bit for bit. */
 int cpt_write_accum(cpt_ctx* ctx, const float* rgba);
 int cpt_write_aux(cpt_ctx* ctx, const float* normal3, const float* depth);
-/* Device-to-device copy of the accumulator (e.g. into an RCCL send buffer). */
-int cpt_copy_accum_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
+/* Device-to-device copy of the accumulator (e.g. into an RCCL send buffer), ordered against the
+ * caller's HIP stream `caller_stream` (NULL: the null stream) without blocking the host: the
+ * context's stream first waits for the work queued on caller_stream so far (a fill of dst, a
+ * collective still reading it), then copies, and caller_stream waits for the copy (work queued on
+ * it next, e.g. the all-gather, reads the copied bytes).  When caller_stream is the context's own
+ * launch stream (cpt_set_stream) the copy is simply queued there.  Device errors of the render
+ * surface at the next synchronising call. */
+int cpt_copy_accum_device(cpt_ctx* ctx, void* device_dst, size_t bytes, void* caller_stream);
 /* Row-tile gather (multi-GPU row tiling; the single-GPU reference writes the
  * whole frame from SamplePixel, path_tracer.cu:172-174): places the rows `src` rendered -- its
  * accumulator, and its first-hit normals and depths when it rendered with CPT_RENDER_AUX --
@@ -335,11 +341,17 @@ int cpt_host_unregister(void* ptr);
  * BGRA8 output hold the band's rows only ((y1-y0) x W x 4 bytes to bgra_host, may be NULL); a
  * new band starts a fresh (zeroed) mean.  Byte-identical to rows y0..y1-1 of cpt_denoise_mix. */
 int cpt_denoise_mix_band(cpt_ctx* ctx, uint32_t cur_sample_idx, int y0, int y1, uint8_t* bgra_host);
-/* Device-to-device copy of the current display band's BGRA8 rows (for an RCCL gather). */
-int cpt_copy_bgra_device(cpt_ctx* ctx, void* device_dst, size_t bytes);
+/* Device-to-device copy of the current display band's BGRA8 rows (for an RCCL gather), ordered
+ * against caller_stream as cpt_copy_accum_device. */
+int cpt_copy_bgra_device(cpt_ctx* ctx, void* device_dst, size_t bytes, void* caller_stream);
+/* The output rows [y0, y1) the display buffers currently hold (cpt_denoise_mix: the whole
+ * 16-aligned launch; cpt_denoise_mix_band: the band); 0, 0 before the first display pass. */
+int cpt_display_band(const cpt_ctx* ctx, int* y0, int* y1);
 /* The Mix running mean of the current display band ([(y1-y0)*W][3] floats: rows y0..y1-1; the
- * whole 16-aligned launch's rows for cpt_denoise_mix), read back for checking and checkpoints. */
-int cpt_read_mix(cpt_ctx* ctx, float* rgb);
+ * whole 16-aligned launch's rows for cpt_denoise_mix), read back for checking and checkpoints.
+ * `capacity` is rgb's size in floats: CPT_ERR_INVALID_ARG (nothing written) when it is smaller
+ * than the band (size it from cpt_display_band). */
+int cpt_read_mix(cpt_ctx* ctx, float* rgb, size_t capacity);
 /* Device time of the last display kernel (Denoising + Mix, the reference's per-pass log of
  * path_tracer.cu:261,300 split by kernel), from HIP events on the context's stream; waits
  * for it. */
@@ -371,6 +383,11 @@ int cpt_math_batch(cpt_ctx* ctx, int op, const float* a, const float* b, float* 
  * which = 6: the display weight dn_weight (short exp + rounding guard) against its slow form
  * dn_weight_slow for the float bit patterns [0, n) (n = 2^31: every non-negative float, inf and
  * NaN); which = 7: counts the patterns whose guard sends them to the slow form (not an error).
+ * which = 8: the BSDF lobe's short pow (lobe_pow) against (float)pow(x, y) of the full double
+ * sequence for the float bit patterns x in [0, n), y = the double whose bits are `seed`;
+ * which = 9: counts the x whose guard sends them to the full pow; which = 10: the lobe's short
+ * sinf/cosf (lobe_sincos) against the full sequence for the float patterns [0, n); which = 11:
+ * counts the guard's fallbacks there.
  * out[0] receives the mismatch count (0 expected), out[1..out_len) up to out_len-1 failing
  * pairs as (a bits << 32 | d bits). */
 int cpt_selftest_qdiv(cpt_ctx* ctx, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len);

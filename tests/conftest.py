@@ -39,3 +39,12 @@ def gpu():
 
 def frame_rows(h, rows=None):
     return np.arange(h, dtype=np.int32) if rows is None else np.asarray(rows, dtype=np.int32)
+
+
+def lobe_exponents(oracle_mod, scene):
+    """The inv_alpha of every non-Diffuse material of a scene: 1.0 / (double)powf(1000, smoothness)
+    (material.cu:43-45, cpt_kernels.hip k_prepare_materials; Diffuse's exponent is 1/2)."""
+    from cpppathtracer_amd import scenes, types
+    objs = scenes.SCENES[scene]()
+    sm = sorted({float(o["material"]["smoothness"]) for o in objs if int(o["material"]["type"]) != types.DIFFUSE})
+    return [1.0 / float(oracle_mod.lib().or_powf(np.float32(1000.0), np.float32(s))) for s in sm]

@@ -3,6 +3,7 @@
 Each simulated rank is its own context on cuda:0 rendering its band plus the 3-row halo; the
 stitched BGRA8 frame must equal the single-GPU display path byte for byte (the committed
 golden, and cpt_denoise_mix on the same frame)."""
+import ctypes
 import os
 
 import numpy as np
@@ -64,3 +65,40 @@ def test_gpu_band_needs_halo_rows(gpu, sky):
         gpu.denoise_mix_band(2, 16, 32)
     with pytest.raises(CptError):
         gpu.denoise_mix_band(2, 40, 64)   # past H'
+
+
+def test_gpu_banded_display_16_wide(gpu, sky):
+    """A 16-column frame through band contexts (round 6, advisor r05): k_denoise_rows' halo lanes
+    past 2 W' wrap beyond the next row; they must read nothing outside the context's rows (the
+    guard), and the stitched frame equals the full-frame display path byte for byte.  The Mix
+    mean read back is sized from the library's band (cpt_display_band) and checked against a
+    buffer too small for it (cpt_read_mix's capacity)."""
+    from cpppathtracer_amd import Renderer
+    from cpppathtracer_amd.renderer import CptError
+    W, H = 16, 100
+    objs = scenes.scene_s4()
+    cam = camera_get_copy(scenes.camera_for(W, H))
+    gpu.set_scene(objs)
+    gpu.set_env(sky)
+    gpu.set_frame(W, H)
+    gpu.init_rng(1234)
+    for idx in (2, 3):
+        gpu.render(cam, 1, 8, aux=True, sync=True)
+        full = gpu.denoise_mix(idx)
+    full_mix = gpu.read_mix()
+    assert gpu.display_band() == (0, 16 * (H // 16))
+    np.testing.assert_array_equal(_banded(sky, objs, W, H, 3, (2, 3)), full)
+    with Renderer(0) as r:
+        r.set_scene(objs)
+        r.set_env(sky)
+        from cpppathtracer_amd.display import BandedDisplay
+        d = BandedDisplay(r, W, H, 1234, 1, 3)
+        for idx in (2, 3):
+            d.dispatch(cam, idx, 8)
+        y0, y1 = r.display_band()
+        assert (y0, y1) == (d.y0, d.y1)
+        np.testing.assert_array_equal(r.read_mix().view(np.uint32),
+                                      full_mix[y0 * W: y1 * W].view(np.uint32))
+        small = np.zeros(((y1 - y0) * W - 1, 3), np.float32)
+        with pytest.raises(CptError):
+            r._check(r._L.cpt_read_mix(r._ctx, ctypes.c_void_p(small.ctypes.data), small.size))

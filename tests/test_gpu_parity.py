@@ -113,6 +113,39 @@ def test_dn_weight_exhaustive(gpu):
     assert fallbacks < 1e-5 * lim, fallbacks
 
 
+def test_lobe_pow_exhaustive(gpu, oracle_mod):
+    """The BSDF lobe's z = (float)pow(x_1, inv_alpha) through its short form (cpt_device.hpp
+    lobe_pow: sqrtf for Diffuse's 1/2, fm::pow_unit + rounding guard for the others) == the full
+    double sequence dm::pow, rounded to float, for every float x in [0, 1] at every exponent the
+    S4 and S1000 materials use, at 1/2, and at the edges of the short form's domain (round 6;
+    material.cu:24,43-45,78,85,104).  The full sequence equals the oracle's dm_pow
+    (test_binary_pow_bitexact); tests/test_fastmath.py restates the short form on the host."""
+    from conftest import lobe_exponents
+    n = int(np.float32(1.0).view(np.uint32)) + 1
+    ys = sorted(set(lobe_exponents(oracle_mod, "s4") + lobe_exponents(oracle_mod, "s1000")))
+    for y in ys + [0.5, 1.0, 0.999, 0.25, 2.0 ** -40, 1.5]:
+        seed = int(np.float64(y).view(np.uint64))
+        cnt, xs = gpu.selftest_qdiv(8, n, seed=seed)
+        assert cnt == 0, (y, [float(x) for x, _ in xs])
+    # the guard's fallbacks over the normal floats of (0, 1] at the materials' exponents
+    # (subnormal x always takes the full pow: the lobe's x_1 >= 2^-33 never is one)
+    for y in ys:
+        fell, _ = gpu.selftest_qdiv(9, n, seed=int(np.float64(y).view(np.uint64)))
+        assert fell - 0x00800000 < 1e-5 * n, (y, fell)
+
+
+def test_lobe_sincos_exhaustive(gpu):
+    """The lobe's sinf/cosf of phi = (float)(2 pi x_2) through the short table form + rounding
+    guard (cpt_device.hpp lobe_sincos) == the full dm::sincosf_ sequence, both results, for all
+    2^32 float patterns (outside [0, 2 pi] the guard always hands over), and how rarely the guard
+    fires on [0, 2 pi] (material.cu:26-27,47-48)."""
+    cnt, xs = gpu.selftest_qdiv(10, 1 << 32)
+    assert cnt == 0, [float(x) for x, _ in xs]
+    n = int(np.float32(2 * np.pi).view(np.uint32)) + 1
+    fell, _ = gpu.selftest_qdiv(11, n)
+    assert fell - 0x00800000 < 1e-5 * n, fell
+
+
 # ------------------------------------------------------------------------------- rng
 @pytest.mark.parametrize("w,rows", [(64, list(range(64))), (3840, [0, 1, 7, 1079, 2159]),
                                     (333, [5, 3, 200, 3])])

@@ -156,3 +156,33 @@ def test_gather_rows_peer_two_devices(sky):
     with Renderer(0) as frame:
         frame.set_frame(W, H)
         _gather_check(frame, tiles, mono, ["peer"] * world)
+
+
+def test_tilegather_copy_ordered_against_torch_stream(sky):
+    """cpt_copy_accum_device orders the tile copy against torch's stream with no host wait
+    (round 6; round 5 found one 8-rank stitched frame with pass counts of 0 where a late zero
+    fill of TileGather's send buffer on torch's stream landed after the copy on the context's own
+    stream).  Torch's stream is held busy by a long sleep right before each write of `send` it
+    queues -- the buffers' zero fill, then a NaN fill standing for a collective still using the
+    buffer -- while the context (on its own non-blocking stream) is idle: an unordered copy would
+    run first and be overwritten.  The frame must equal the render bit for bit both times."""
+    import torch
+    from cpppathtracer_amd import multigpu
+    W, H, spp, depth, seed = 96, 52, 2, 16, 41
+    dev = torch.device("cuda", 0)
+    cam = camera_get_copy(scenes.camera_for(W, H))
+    with Renderer(0) as r:   # its own stream: nothing orders it with torch's
+        r.set_scene(scenes.scene_s1000(n=200))
+        r.set_env(sky)
+        r.set_frame(W, H, tiling.partition_rows(H, 1, 0))
+        r.init_rng(seed)
+        r.render(cam, spp, depth, ordered=True, sync=True)
+        want = r.read_accum()
+        torch.cuda._sleep(300_000_000)                 # ~0.1 s of torch's stream
+        g = multigpu.TileGather(W, H, 1, 0, dev, backend="gloo")   # its zero fills: behind the sleep
+        got = g(r).reshape(H * W, 4).cpu().numpy()
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+        torch.cuda._sleep(300_000_000)
+        g.send.fill_(float("nan"))                     # a late writer of `send` on torch's stream
+        got = g(r).reshape(H * W, 4).cpu().numpy()
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
