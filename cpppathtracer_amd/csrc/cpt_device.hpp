@@ -413,17 +413,73 @@ __device__ __forceinline__ void sincos_2pi(float phi, double& s, double& c, bool
     ok = phi >= 0.0f && phi <= 6.28318548f && sure_f32(s) && sure_f32(c);
 }
 
+#ifndef CPT_FM   // A/B: bit 0 the lobe's short forms, bit 1 the sky fetch's (0 = round 5's full sequences)
+#define CPT_FM 3
+#endif
+__device__ const double g_at_tab[2 * (FM_AT_N + 1)] = CPT_FM_AT_TABLE_INIT;   // {atan(k/32), pi/2 - atan(k/32)}
+
+// atan(n / m) for n >= 0, m > 0 (else ok = false): with k = round(32 min(n/m, m/n)) from a float
+// estimate and c = k/32, atan(n/m) = A_k + atan((n - c m) / (m + c n)) when n <= m, and
+// B_k - atan((m - c n) / (n + c m)) when n > m (A_k = atan c, B_k = pi/2 - atan c); each
+// numerator and denominator is one fma (the numerator's cancellation is exact inside it), the
+// quotient a reciprocal (v_rcp_f64 + two Newton steps) times the numerator, |d| <= 2^-6, and
+// atan d to d^7.  No IEEE divide: the quotient n/m itself is never formed.
+__device__ __forceinline__ double atan_ratio(double n, double m, bool& ok) {
+    const bool big = n > m;
+    const float rf = (float)(big ? m : n) * __builtin_amdgcn_rcpf((float)(big ? n : m));
+    const float kf = __builtin_fminf(__builtin_rintf(32.0f * rf), 32.0f);
+    const double c = (double)kf * 0.03125;
+    const double num = big ? __builtin_fma(-c, n, m) : __builtin_fma(-c, m, n);
+    const double den = big ? __builtin_fma(c, m, n) : __builtin_fma(c, n, m);
+    double r = __builtin_amdgcn_rcp(den);
+    double e = __builtin_fma(-den, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-den, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double d = num * r;
+    const double d2 = d * d;
+    double p = __builtin_fma(d2, dm::kc(FM_A7), dm::kc(FM_A5));
+    p = __builtin_fma(d2, p, dm::kc(FM_A3));
+    const double at = __builtin_fma(d * d2, p, d);
+    const int k = (int)kf;   // 0..32 (a NaN estimate: the guard below fails)
+    const double T = g_at_tab[2 * (k >= 0 && k <= FM_AT_N ? k : 0) + (big ? 1 : 0)];
+    const double res = big ? T - at : T + at;
+    ok = n >= 0.0 && m > 0.0 && sure_f32(res);
+    return res;
+}
+
 }  // namespace fm
+
+// Miss's atanf(d.y / d.x) (path_tracer.cu:120): (float)dm::atan((double)x) through fm::atan_ratio
+// (|x| over 1), the full sequence where its guard fails (test_miss_atan_asin_exhaustive).
+__device__ __forceinline__ float miss_atanf(float x) {
+    if (!(CPT_FM & 2)) return dm::atanf_(x);
+    bool ok;
+    const double a = fm::atan_ratio(__builtin_fabs((double)x), 1.0, ok);
+    float f = (float)(x < 0.0f ? -a : a);
+    if (__builtin_expect(!ok, 0)) f = dm::atanf_(x);
+    return f;
+}
+
+// Miss's asinf(d.z) (path_tracer.cu:119): dm::asinf_ is (float)atan(z / sqrt((1 - z)(1 + z)));
+// fm::atan_ratio takes |z| over the same square root directly, so neither the quotient's divide
+// nor a second atan reduction runs; the full sequence where the guard fails (z = +-1, 0, NaN).
+__device__ __forceinline__ float miss_asinf(float z) {
+    if (!(CPT_FM & 2)) return dm::asinf_(z);
+    const double x = (double)z;
+    bool ok;
+    const double a = fm::atan_ratio(__builtin_fabs(x), __builtin_sqrt((1.0 - x) * (1.0 + x)), ok);
+    float f = (float)(z < 0.0f ? -a : a);
+    if (__builtin_expect(!ok, 0)) f = dm::asinf_(z);
+    return f;
+}
 
 // The lobe's z = (float)pow(x_1, inv_alpha) (material.cu:24,45,78,85,104): Diffuse's exponent 1/2
 // as sqrtf -- (float)dm::pow(x, 0.5) == sqrtf(x) for every float x in [2^-42, 1] (x_1 >= 2^-33),
 // checked on the host against the oracle and on the device (test_lobe_pow_exhaustive); the
 // other exponents through fm::pow_unit, the dm:: sequence where its guard fails.
-#ifndef CPT_FM_LOBE   // A/B: 0 = the full dm:: sequences in the lobe (round 5)
-#define CPT_FM_LOBE 1
-#endif
 __device__ __forceinline__ float lobe_pow(float x, double y) {
-    if (!CPT_FM_LOBE) return (float)dm::pow((double)x, y);
+    if (!(CPT_FM & 1)) return (float)dm::pow((double)x, y);
     if (y == 0.5 && x >= 0x1p-42f) return sqrt_nn(x);
     bool ok;
     const double d = fm::pow_unit(x, y, ok);
@@ -435,7 +491,7 @@ __device__ __forceinline__ float lobe_pow(float x, double y) {
 // sinf / cosf of the lobe's phi = (float)(2 pi x_2) in [0, 2 pi] (material.cu:26-27,47-48):
 // fm::sincos_2pi, dm::sincosf_ where its guard fails (test_lobe_sincos_exhaustive).
 __device__ __forceinline__ void lobe_sincos(float phi, float* s_out, float* c_out) {
-    if (!CPT_FM_LOBE) return dm::sincosf_(phi, s_out, c_out);
+    if (!(CPT_FM & 1)) return dm::sincosf_(phi, s_out, c_out);
     double s, c;
     bool ok;
     fm::sincos_2pi(phi, s, c, ok);

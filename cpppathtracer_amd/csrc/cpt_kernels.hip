@@ -887,7 +887,9 @@ __device__ __forceinline__ bool dn_near_midpoint(double e) {
 // against the full dm:: sequences, over the float patterns [0, n) (cpt_selftest_qdiv):
 // which = 8: lobe_pow(x, y) vs (float)dm::pow(x, y), y = the double with the bits of `seed`;
 // 9: how many x take pow's fallback; 10: lobe_sincos(phi) vs dm::sincosf_(phi), both results;
-// 11: how many phi take sincos' fallback.  out[0] = count, out[1..] = some of the floats' bits.
+// 11: how many phi take sincos' fallback; 12: miss_atanf / miss_asinf vs dm::atanf_ / dm::asinf_;
+// 13: how many x take either one's fallback (asinf: x in [-1, 1]).  out[0] = count, out[1..] =
+// some of the floats' bits.
 __global__ void k_selftest_fm(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const double y = __longlong_as_double((long long)seed);
@@ -900,6 +902,15 @@ __global__ void k_selftest_fm(int which, uint64_t n, uint64_t seed, unsigned lon
             bool ok;
             (void)fm::pow_unit(x, y, ok);
             flag = !ok && !(y == 0.5 && x >= 0x1p-42f);
+        } else if (which == 12) {
+            flag = __float_as_uint(miss_atanf(x)) != __float_as_uint(dm::atanf_(x)) ||
+                   __float_as_uint(miss_asinf(x)) != __float_as_uint(dm::asinf_(x));
+        } else if (which == 13) {
+            bool ok1, ok2;
+            (void)fm::atan_ratio(__builtin_fabs((double)x), 1.0, ok1);
+            const double xd = (double)x;
+            (void)fm::atan_ratio(__builtin_fabs(xd), __builtin_sqrt((1.0 - xd) * (1.0 + xd)), ok2);
+            flag = !ok1 || (!ok2 && x >= -1.0f && x <= 1.0f);
         } else if (which == 10) {
             float s, c, s_ref, c_ref;
             lobe_sincos(x, &s, &c);

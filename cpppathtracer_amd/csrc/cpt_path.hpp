@@ -1086,8 +1086,9 @@ __device__ inline void eval_material(const Mat& m, v3 normal, v3 in_dir, Xorwow&
 // Miss (path_tracer.cu:117-122)
 __device__ __forceinline__ v3 miss_radiance(const KParams& p, v3 dir) {
     v3 d = normalize_u(dir);
-    float v = (float)(dm::div_pi(dm::asinf_(d.z)) + 0.5);     // (double)asinf / REF_PI + 0.5
-    float u = (float)dm::div_pi(dm::atanf_(d.y / d.x) / 2);    // (double)(atanf / 2) / REF_PI
+    // asinf / atanf through their short forms (cpt_device.hpp miss_asinf, miss_atanf: the same floats)
+    float v = (float)(dm::div_pi(miss_asinf(d.z)) + 0.5);     // (double)asinf / REF_PI + 0.5
+    float u = (float)dm::div_pi(miss_atanf(d.y / d.x) / 2);    // (double)(atanf / 2) / REF_PI
     return tex2d(p, u, v);
 }
 

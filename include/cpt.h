@@ -387,7 +387,9 @@ int cpt_math_batch(cpt_ctx* ctx, int op, const float* a, const float* b, float* 
  * sequence for the float bit patterns x in [0, n), y = the double whose bits are `seed`;
  * which = 9: counts the x whose guard sends them to the full pow; which = 10: the lobe's short
  * sinf/cosf (lobe_sincos) against the full sequence for the float patterns [0, n); which = 11:
- * counts the guard's fallbacks there.
+ * counts the guard's fallbacks there; which = 12: the sky fetch's short atanf and asinf
+ * (miss_atanf, miss_asinf) against the full sequences for the float patterns [0, n); which = 13:
+ * counts the patterns where either guard falls back (asinf: on [-1, 1]).
  * out[0] receives the mismatch count (0 expected), out[1..out_len) up to out_len-1 failing
  * pairs as (a bits << 32 | d bits). */
 int cpt_selftest_qdiv(cpt_ctx* ctx, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len);

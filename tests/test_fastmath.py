@@ -9,7 +9,10 @@ material.cu:24-27,43-48,78-86,104-105's pow / cosf / sinf), float for float:
 * lobe_pow(x, y) == (float)pow(x, y) for every float x in [2^-33, 1] at one of S4's exponents,
   every 7th normal float at S4's others, and every 61st float of (0, 1] at the S1000 materials'
   and edge exponents of the short form's domain;
-* lobe_sincos(phi) == (sinf(phi), cosf(phi)) for every float phi in [0, 2 pi].
+* lobe_sincos(phi) == (sinf(phi), cosf(phi)) for every float phi in [0, 2 pi];
+* the sky fetch's miss_atanf / miss_asinf (fm::atan_ratio, path_tracer.cu:119-120) == atanf /
+  asinf on every 31st float / every 7th float in [-1, 1] (the host form uses IEEE quotients where the
+  device takes hardware reciprocal estimates; the device test checks the shipped code).
 
 Also reports how often the rounding guard sends an input to the full sequence.  The device
 code itself is checked against the device's full sequences for every float of the same domains
@@ -37,6 +40,8 @@ using namespace cpt;
 static double (*or_pow)(double, double);
 static float (*or_sinf)(float);
 static float (*or_cosf)(float);
+static float (*or_atanf)(float);
+static float (*or_asinf)(float);
 static const double LOG_TAB[2 * FM_LOG_N] = CPT_FM_LOG_TABLE_INIT;
 static const double EXP_TAB[FM_EXP_N] = CPT_FM_EXP_TABLE_INIT;
 static const double SC_TAB[2 * (2 * FM_SC_N + 1)] = CPT_FM_SC_TABLE_INIT;
@@ -100,6 +105,32 @@ static void sincos_2pi(float phi, double& s, double& c, bool& ok) {   /* fm::sin
     c = fma(C, cr, -(S * sr));
     ok = phi >= 0.0f && phi <= 6.28318548f && sure_f32(s) && sure_f32(c);
 }
+static const double AT_TAB[2 * (FM_AT_N + 1)] = CPT_FM_AT_TABLE_INIT;
+/* fm::atan_ratio, with the device's two hardware reciprocal estimates (v_rcp_f32 for k, v_rcp_f64
+   before the two Newton steps) replaced by IEEE quotients: k may differ where the float ratio
+   sits at a rounding tie and the double result in its last bits, so this restates the form and
+   its guard, and the device test compares the shipped code itself */
+static double atan_ratio(double n, double m, bool& ok) {
+    const bool big = n > m;
+    const float rf = (float)(big ? m : n) * (1.0f / (float)(big ? n : m));
+    const float kf = fminf(rintf(32.0f * rf), 32.0f);
+    const double c = (double)kf * 0.03125;
+    const double num = big ? fma(-c, n, m) : fma(-c, m, n);
+    const double den = big ? fma(c, m, n) : fma(c, n, m);
+    double r = 1.0 / den;
+    double e = fma(-den, r, 1.0);
+    r = fma(r, e, r);
+    const double d = num * r;
+    const double d2 = d * d;
+    double p = fma(d2, FM_A7, FM_A5);
+    p = fma(d2, p, FM_A3);
+    const double at = fma(d * d2, p, d);
+    const int k = (int)kf;
+    const double T = AT_TAB[2 * (k >= 0 && k <= FM_AT_N ? k : 0) + (big ? 1 : 0)];
+    const double res = big ? T - at : T + at;
+    ok = n >= 0.0 && m > 0.0 && sure_f32(res);
+    return res;
+}
 static float lobe_pow(float x, double y, bool& fell) {   /* lobe_pow */
     fell = false;
     if (y == 0.5 && x >= 0x1p-42f) return sqrtf(x);
@@ -126,7 +157,22 @@ static void* run(void* arg) {
             const float a = lobe_pow(x, g_y, fell), r = (float)or_pow((double)x, g_y);
             g_fell[t] += fell;
             if (fbits(a) != fbits(r)) { if (g_bad[t] < 3) printf("pow %a %a: %a vs %a\n", x, g_y, a, r); g_bad[t]++; }
-        } else {
+        } else if (g_mode == 3) {   /* miss_atanf */
+            bool ok;
+            const double a = atan_ratio(fabs((double)x), 1.0, ok);
+            float f = (float)(x < 0.0f ? -a : a);
+            const float r = or_atanf(x);
+            if (!ok) { f = r; g_fell[t]++; }
+            if (fbits(f) != fbits(r)) { if (g_bad[t] < 3) printf("atanf %a: %a vs %a\n", x, f, r); g_bad[t]++; }
+        } else if (g_mode == 4) {   /* miss_asinf */
+            const double xd = (double)x;
+            bool ok;
+            const double a = atan_ratio(fabs(xd), sqrt((1.0 - xd) * (1.0 + xd)), ok);
+            float f = (float)(x < 0.0f ? -a : a);
+            const float r = or_asinf(x);
+            if (!ok) { f = r; g_fell[t]++; }
+            if (fbits(f) != fbits(r)) { if (g_bad[t] < 3) printf("asinf %a: %a vs %a\n", x, f, r); g_bad[t]++; }
+        } else if (g_mode == 2) {
             double s, c;
             bool ok;
             sincos_2pi(x, s, c, ok);
@@ -148,6 +194,8 @@ int main(int argc, char** argv) {
     or_pow = (double (*)(double, double))dlsym(h, "or_pow");
     or_sinf = (float (*)(float))dlsym(h, "or_sinf");
     or_cosf = (float (*)(float))dlsym(h, "or_cosf");
+    or_atanf = (float (*)(float))dlsym(h, "or_atanf");
+    or_asinf = (float (*)(float))dlsym(h, "or_asinf");
     g_mode = atoi(argv[2]);
     g_lo = (uint32_t)strtoul(argv[3], 0, 0);
     g_hi = (uint32_t)strtoul(argv[4], 0, 0);
@@ -217,3 +265,18 @@ def test_lobe_sincos_exhaustive(fm_exe, oracle_mod):
     n, fell = _run(fm_exe, oracle_mod, 2, 0, X_2PI, 1)
     # 0 and the 2^23 - 1 subnormal phi (sin phi a subnormal float) always take the full sequence
     assert fell - X_MIN_NORMAL < 1e-5 * n
+
+
+@pytest.mark.parametrize("sign", [0, 0x80000000])
+def test_miss_atanf(fm_exe, oracle_mod, sign):
+    """Every 31st float of either sign (the device test takes all 2^32)."""
+    n, fell = _run(fm_exe, oracle_mod, 3, sign, sign + 0x7f800000, 31)
+    # 0 and the subnormals (atan x = x: a subnormal float) always take the full sequence
+    assert fell - X_MIN_NORMAL // 31 < 1e-5 * n
+
+
+def test_miss_asinf(fm_exe, oracle_mod):
+    """Every 7th float in [-1, 1] (the device test takes all 2^32)."""
+    for lo in (0, 0x80000000):
+        n, fell = _run(fm_exe, oracle_mod, 4, lo, lo + X_ONE, 7)
+        assert fell - X_MIN_NORMAL // 7 < 1e-5 * n

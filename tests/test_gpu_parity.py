@@ -146,6 +146,19 @@ def test_lobe_sincos_exhaustive(gpu):
     assert fell - 0x00800000 < 1e-5 * n, fell
 
 
+def test_miss_atan_asin_exhaustive(gpu):
+    """The sky fetch's atanf(d.y / d.x) and asinf(d.z) through fm::atan_ratio + rounding guard
+    (cpt_device.hpp miss_atanf, miss_asinf; round 6) == the full dm::atanf_ / dm::asinf_
+    sequences (themselves the oracle's: test_unary_math_bitexact) for all 2^32 float patterns,
+    and how rarely the guards fire (path_tracer.cu:119-120)."""
+    cnt, xs = gpu.selftest_qdiv(12, 1 << 32)
+    assert cnt == 0, [float(x) for x, _ in xs]
+    fell, _ = gpu.selftest_qdiv(13, 1 << 32)
+    # +-0 and the 2 (2^23 - 1) subnormals (atan x = x, asin x = x: subnormal floats), the
+    # infinities and NaNs (2^24 - 2 patterns) always take the full sequences
+    assert fell - 2 * 0x00800000 - (1 << 24) < 1e-5 * (1 << 32), fell
+
+
 # ------------------------------------------------------------------------------- rng
 @pytest.mark.parametrize("w,rows", [(64, list(range(64))), (3840, [0, 1, 7, 1079, 2159]),
                                     (333, [5, 3, 200, 3])])
