@@ -55,6 +55,7 @@ PROTOTYPES = {
     "cpt_get_raw_counters": (_I, [_P, _P]),
     "cpt_get_walk_info": (_I, [_P, _P]),
     "cpt_measure_read_bandwidth": (_I, [_P, _SZ, _I, _P]),
+    "cpt_measure_read_pattern": (_I, [_P, _I, _SZ, _I, _P]),
     "cpt_cap_disk_bound": (_I, [ctypes.c_float, _P]),
     "cpt_last_render_ms": (_I, [_P, _P]),
     "cpt_get_diag_counters": (_I, [_P, _P]),
@@ -68,6 +69,8 @@ PROTOTYPES = {
     "cpt_last_display_ms": (_I, [_P, _P]),
     "cpt_reset_display": (_I, [_P]),
     "cpt_display_band": (_I, [_P, _P, _P]),
+    "cpt_debug_timeline": (_I, [_P, _P, _I]),
+    "cpt_tile_costs": (_I, [_P, _P, _I, _I, ctypes.c_uint32, _P, _SZ]),
     "cpt_read_mix": (_I, [_P, _P, _SZ]),
     "cpt_math_batch": (_I, [_P, _I, _P, _P, _P, _SZ]),
     "cpt_selftest_qdiv": (_I, [_P, _I, _U64, _U64, _P, _I]),

@@ -335,23 +335,8 @@ int cpt_write_rng(cpt_ctx* c, const uint32_t* planar6) {
     return CPT_OK;
 }
 
-int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32_t flags) {
-    if (!c || !cam) return CPT_ERR_INVALID_ARG;
-    if (spp < 0 || max_depth < 0 || max_depth > (int)cpt::MAX_RECURSION_DEPTH_SET)
-        return fail(c, CPT_ERR_INVALID_ARG, "cpt_render: spp %d, max_depth %d (must be 0..32)", spp, max_depth);
-    if (!c->scene_set) return fail(c, CPT_ERR_STATE, "cpt_render: cpt_set_scene first");
-    if (!c->frame_set || !c->rng_set) return fail(c, CPT_ERR_STATE, "cpt_render: cpt_set_frame + cpt_init_rng first");
-    if (cam->width != c->width || cam->height != c->height)
-        return fail(c, CPT_ERR_INVALID_ARG, "cpt_render: camera %dx%d vs frame %dx%d", cam->width, cam->height, c->width, c->height);
-    HIP_TRY(c, hipSetDevice(c->device));
-    hipStream_t s = c->stream();
-    const bool aux = (flags & CPT_RENDER_AUX) != 0;
-    if (aux) {
-        size_t npix = (size_t)c->n_rows * c->width;
-        if (!c->d_normal && npix) HIP_TRY(c, hipMalloc((void**)&c->d_normal, npix * 3 * sizeof(float)));
-        if (!c->d_depth && npix) HIP_TRY(c, hipMalloc((void**)&c->d_depth, npix * sizeof(float)));
-    }
-    cpt::KParams p;
+// The megakernel's parameters for a render of the context's frame (cpt_render, cpt_tile_costs).
+static void fill_params(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32_t flags, cpt::KParams& p) {
     std::memset(&p, 0, sizeof(p));
     p.nodes = c->d_nodes;
     p.mats = c->d_mats;
@@ -401,6 +386,26 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     p.dbg = c->dbg;
     p.keeper_spin_log2 = c->keeper_spin_log2;
     p.publish_wait_log2 = c->publish_wait_log2;
+}
+
+int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32_t flags) {
+    if (!c || !cam) return CPT_ERR_INVALID_ARG;
+    if (spp < 0 || max_depth < 0 || max_depth > (int)cpt::MAX_RECURSION_DEPTH_SET)
+        return fail(c, CPT_ERR_INVALID_ARG, "cpt_render: spp %d, max_depth %d (must be 0..32)", spp, max_depth);
+    if (!c->scene_set) return fail(c, CPT_ERR_STATE, "cpt_render: cpt_set_scene first");
+    if (!c->frame_set || !c->rng_set) return fail(c, CPT_ERR_STATE, "cpt_render: cpt_set_frame + cpt_init_rng first");
+    if (cam->width != c->width || cam->height != c->height)
+        return fail(c, CPT_ERR_INVALID_ARG, "cpt_render: camera %dx%d vs frame %dx%d", cam->width, cam->height, c->width, c->height);
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream();
+    const bool aux = (flags & CPT_RENDER_AUX) != 0;
+    if (aux) {
+        size_t npix = (size_t)c->n_rows * c->width;
+        if (!c->d_normal && npix) HIP_TRY(c, hipMalloc((void**)&c->d_normal, npix * 3 * sizeof(float)));
+        if (!c->d_depth && npix) HIP_TRY(c, hipMalloc((void**)&c->d_depth, npix * sizeof(float)));
+    }
+    cpt::KParams p;
+    fill_params(c, cam, spp, max_depth, flags, p);
     const bool wavefront = (flags & CPT_PATH_WAVEFRONT) != 0;
     if (wavefront && !c->wf_ready && c->n_rows > 0) {
         const size_t npix = (size_t)c->n_rows * c->width;
@@ -506,6 +511,41 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
     c->have_timing = true;
     if (flags & CPT_RENDER_SYNC) return sync_checked(c);
     return CPT_OK;
+}
+
+// The cost schedule's pilot on its own (cost-balanced row partitions, tiling.py): `passes` passes
+// from the context's current RNG states, nothing written back, each 8x8 tile's work (segments +
+// node visits + primitive tests) into `out`.
+int cpt_tile_costs(cpt_ctx* c, const cpt_camera* cam, int passes, int max_depth, uint32_t flags, uint32_t* out,
+                   size_t n_out) {
+    if (!c || !cam || !out || passes < 1 || max_depth < 0 || max_depth > (int)cpt::MAX_RECURSION_DEPTH_SET)
+        return CPT_ERR_INVALID_ARG;
+    if (!c->scene_set) return fail(c, CPT_ERR_STATE, "cpt_tile_costs: cpt_set_scene first");
+    if (!c->frame_set || !c->rng_set) return fail(c, CPT_ERR_STATE, "cpt_tile_costs: cpt_set_frame + cpt_init_rng first");
+    if (cam->width != c->width || cam->height != c->height)
+        return fail(c, CPT_ERR_INVALID_ARG, "cpt_tile_costs: camera %dx%d vs frame %dx%d", cam->width, cam->height, c->width,
+                    c->height);
+    const size_t n_tiles = (size_t)((c->width + 7) / 8) * ((c->n_rows + 7) / 8);
+    if (n_out < n_tiles) return fail(c, CPT_ERR_INVALID_ARG, "cpt_tile_costs: %zu < %zu tiles", n_out, n_tiles);
+    if (n_tiles == 0) return CPT_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream();
+    cpt::KParams p;
+    fill_params(c, cam, passes, max_depth, flags & (CPT_TRAVERSAL_ORDERED | CPT_TRAVERSAL_PLAIN_LEAVES), p);
+    const size_t bytes = cpt::tile_schedule_scratch_bytes(c->width, c->n_rows);
+    if (c->cap_sched < bytes) {
+        (void)hipFree(c->d_sched);
+        c->d_sched = nullptr;
+        c->cap_sched = 0;
+        HIP_TRY(c, hipMalloc(&c->d_sched, bytes));
+        c->cap_sched = bytes;
+    }
+    int rc;
+    if ((rc = ensure(c, &c->d_tile_order, &c->cap_tile_order, n_tiles)) != CPT_OK) return rc;
+    HIP_TRY(c, cpt::launch_tile_schedule(p, passes, c->d_sched, c->cap_sched, c->d_tile_order, s));
+    // the unsorted costs are the scratch's first n_tiles words (the sort writes elsewhere)
+    HIP_TRY(c, hipMemcpyAsync(out, c->d_sched, n_tiles * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    return sync_checked(c);
 }
 
 // Row-tile gather: the rows `src` rendered, placed into `dst`'s frame at the
@@ -752,6 +792,15 @@ int cpt_get_stats(cpt_ctx* c, cpt_stats* out) {
     out->prim_tests = h[2];
     out->hits = h[3];
     out->misses = h[4];
+    return CPT_OK;
+}
+
+int cpt_debug_timeline(cpt_ctx* c, uint64_t* out, int n) {
+    if (!c || !out || n <= 0) return CPT_ERR_INVALID_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const hipError_t e = cpt::timeline_read(reinterpret_cast<unsigned long long*>(out), n, c->stream());
+    if (e == hipErrorNotSupported) return fail(c, CPT_ERR_STATE, "cpt_debug_timeline: not a CPT_TIMELINE build");
+    if (e != hipSuccess) return fail(c, CPT_ERR_HIP, "cpt_debug_timeline: %s", hipGetErrorString(e));
     return CPT_OK;
 }
 
@@ -1014,6 +1063,37 @@ int cpt_measure_read_bandwidth(cpt_ctx* c, size_t bytes, int iters, float* gbps)
     (void)hipFree(o);
     if (e != hipSuccess) return fail(c, CPT_ERR_HIP, "cpt_measure_read_bandwidth: %s", hipGetErrorString(e));
     *gbps = (float)((double)n * 16.0 * iters / (ms * 1e-3) / 1e9);
+    return CPT_OK;
+}
+
+int cpt_measure_read_pattern(cpt_ctx* c, int bytes_per_lane, size_t bytes, int iters, float* gbps) {
+    if (!c || !gbps || bytes < 64 || iters < 1 || (bytes_per_lane != 4 && bytes_per_lane != 12 && bytes_per_lane != 16))
+        return CPT_ERR_INVALID_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t n_lanes = bytes / (size_t)bytes_per_lane;
+    float* d = nullptr;
+    float* o = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int cus = 0;
+    hipError_t e = hipMalloc((void**)&d, n_lanes * bytes_per_lane);
+    if (e == hipSuccess) e = hipMalloc((void**)&o, sizeof(float));
+    if (e == hipSuccess) e = hipMemsetAsync(d, 0, n_lanes * bytes_per_lane, c->stream());
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    const int grid = 8 * std::max(cus, 1);
+    if (e == hipSuccess) e = hipEventRecord(e0, c->stream());
+    for (int i = 0; e == hipSuccess && i < iters; ++i) e = cpt::launch_read_pattern(bytes_per_lane, d, n_lanes, o, grid, c->stream());
+    if (e == hipSuccess) e = hipEventRecord(e1, c->stream());
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(d);
+    (void)hipFree(o);
+    if (e != hipSuccess) return fail(c, CPT_ERR_HIP, "cpt_measure_read_pattern: %s", hipGetErrorString(e));
+    *gbps = (float)((double)n_lanes * bytes_per_lane * iters / (ms * 1e-3) / 1e9);
     return CPT_OK;
 }
 

@@ -139,6 +139,8 @@ hipError_t launch_init_rng(const uint32_t* jumps, const uint32_t seed_state[6], 
                            int n_rows, uint32_t* scratch_w, uint32_t* scratch_mats, uint32_t* rng, hipStream_t stream);
 hipError_t launch_math_batch(int op, const float* a, const float* b, float* out, size_t n, hipStream_t stream);
 hipError_t launch_stream_read(const float4* p, size_t n, float* out, int grid, hipStream_t stream);
+hipError_t launch_read_pattern(int bpl, const float* p, size_t n_lanes, float* out, int grid, hipStream_t stream);
+hipError_t timeline_read(unsigned long long* out, int n, hipStream_t stream);
 hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len,
                                 hipStream_t stream);
 hipError_t launch_stitch_rows(const float4* src_acc, const float* src_nrm, const float* src_dep, const int32_t* dst_row,

@@ -90,6 +90,9 @@ __device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int&
 }
 
 // Scheduling constants (SUSPEND_AT, STATIC_FIRST, DEFER_MISS_ROUND, CPT_LDS_BLOCK): cpt_tuning.hpp.
+#ifndef CPT_TILE_KEY_MAX
+#define CPT_TILE_KEY_MAX 0
+#endif
 
 // LDST: the 4-wide walk tree's compact image (its first LDS_TREE_NODES nodes: the top of the
 // tree) is staged in LDS once per workgroup, and the walk reads those nodes there (a lane's
@@ -179,9 +182,12 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     bool counter_done = false;
     (void)res_id; (void)res_end; (void)res_seen; (void)counter_done;
     stamps::init();
+    timeline::State tl;
+    timeline::init(tl);
     for (;;) {
         stamps::lap(5);
         stamps::count(8);
+        timeline::round(tl, __ballot(busy), exhausted, level);
         if (cons && !retiring && level > 0 && exhausted && vq[3] == 0u && vq[2] <= level * (uint32_t)CPT_CONS_RETIRE_PER_LEVEL) retiring = true;
         bool begin = false;   // a lane took a chain: start its next pass
         // ---- take handed-over chains into idle lanes (consolidation) ---------------------
@@ -564,7 +570,11 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             const KParams& p = kernarg_params();   // cold fields (see the refill)
             if (PROBE) {
                 // ---- pilot: the pixel's work goes to its tile's cost ----------------------
+#if CPT_TILE_KEY_MAX   // A/B: a tile's key is its heaviest pixel's pilot work
+                atomicMax(&p.tile_cost[L.tile], cnt.segments + cnt.nodes + cnt.prims - work_at_take);
+#else
                 atomicAdd(&p.tile_cost[L.tile], cnt.segments + cnt.nodes + cnt.prims - work_at_take);
+#endif
             } else {
                 // ---- pixel finished: write back (path_tracer.cu:172-174) -----------------
                 execdiag::lanes(p.stats + 64, 11);
@@ -592,6 +602,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     }
     stamps::flush(p.stats + 16);
     pooldiag::flush(p.stats + 64);
+    timeline::flush(tl);
     if (STATS && !PROBE) {
         uint64_t a = wave_sum(cnt.segments), b = wave_sum(cnt.nodes), c = wave_sum(cnt.prims);
         uint64_t d = wave_sum(cnt.hits), e = wave_sum(cnt.misses);
@@ -1620,6 +1631,52 @@ __global__ void __launch_bounds__(256) k_stream_read(const float4* __restrict__ 
 hipError_t launch_stream_read(const float4* p, size_t n, float* out, int grid, hipStream_t stream) {
     hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, stream, p, n, out);
     return hipGetLastError();
+}
+
+// FETCH_SIZE calibration (cpt_measure_read_pattern): the same grid-stride read with BPL bytes per
+// lane in the display kernel's access shapes: 4 (one float per lane: depth), 12 (three
+// consecutive floats per lane at a 12-B stride: the first-hit normals), 16 (one float4: the
+// accumulator).  One kernel per shape, so a rocprofv3 --pmc FETCH_SIZE pass reports each alone.
+template <int BPL>
+__global__ void __launch_bounds__(256) k_read_pattern(const float* __restrict__ p, size_t n_lanes, float* out) {
+    float acc = 0.f;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_lanes; i += stride) {
+        if (BPL == 4) {
+            acc += p[i];
+        } else if (BPL == 12) {
+            acc += (p[3 * i] + p[3 * i + 1]) + p[3 * i + 2];
+        } else {
+            const float4 v = reinterpret_cast<const float4*>(p)[i];
+            acc += (v.x + v.y) + (v.z + v.w);
+        }
+    }
+    if (acc == 1.2345e-30f) out[0] = acc;
+}
+
+hipError_t launch_read_pattern(int bpl, const float* p, size_t n_lanes, float* out, int grid, hipStream_t stream) {
+    if (bpl == 4) hipLaunchKernelGGL(k_read_pattern<4>, dim3(grid), dim3(256), 0, stream, p, n_lanes, out);
+    else if (bpl == 12) hipLaunchKernelGGL(k_read_pattern<12>, dim3(grid), dim3(256), 0, stream, p, n_lanes, out);
+    else hipLaunchKernelGGL(k_read_pattern<16>, dim3(grid), dim3(256), 0, stream, p, n_lanes, out);
+    return hipGetLastError();
+}
+
+// DIAGNOSTIC (CPT_TIMELINE builds): copy the lane-occupancy timeline out (n words, at most
+// timeline::TL_WORDS) and clear it for the next render; other builds: hipErrorNotSupported.
+hipError_t timeline_read(unsigned long long* out, int n, hipStream_t stream) {
+#ifdef CPT_TIMELINE
+    if (n > timeline::TL_WORDS) n = timeline::TL_WORDS;
+    void* sym = nullptr;
+    hipError_t e = hipGetSymbolAddress(&sym, HIP_SYMBOL(timeline::g_tl));
+    if (e == hipSuccess) e = hipMemcpyAsync(out, sym, (size_t)n * 8, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(sym, 0, (size_t)timeline::TL_WORDS * 8, stream);
+    if (e == hipSuccess) e = hipMemsetAsync((unsigned long long*)sym + 4 * timeline::TL_BINS, 0xff, 8, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    return e;
+#else
+    (void)out; (void)n; (void)stream;
+    return hipErrorNotSupported;
+#endif
 }
 
 hipError_t launch_selftest_qdiv(int which, uint64_t n, uint64_t seed, unsigned long long* out, int out_len,

@@ -50,6 +50,60 @@ __device__ __forceinline__ void flush(unsigned long long*) {}
 #endif
 }  // namespace stamps
 
+// DIAGNOSTIC lane-occupancy timeline (CPT_TIMELINE builds only; never the timed library): at the
+// top of every round of the megakernel each wave adds, for the time since its previous round
+// (s_memrealtime, 100 MHz), busy lanes x dt and 64 x dt to the bin of the current time, and busy x
+// dt again to a second / third slot when the wave has seen the pixel queue run dry / is a level-0
+// (keeper) wave of the tail consolidation.  Bins of 2^TL_SHIFT ticks (1.31 ms) on a ring of
+// TL_BINS (5.4 s); meta[0] = the first time a wave saw the queue dry (atomicMin).
+// tools/timeline.py reads it through cpt_debug_timeline.
+namespace timeline {
+constexpr int TL_BINS = 4096, TL_SHIFT = 17, TL_WORDS = TL_BINS * 4 + 4;
+// a wave's accumulators for the bin it is in (flushed to the global bins when the bin changes)
+struct State {
+    unsigned long long last, acc[4];
+    uint32_t bin;
+};
+#ifdef CPT_TIMELINE
+static __device__ unsigned long long g_tl[TL_WORDS];
+__device__ __forceinline__ unsigned long long now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void init(State& st) {
+    st.last = now();
+    st.bin = (uint32_t)(st.last >> TL_SHIFT) & (uint32_t)(TL_BINS - 1);
+    st.acc[0] = st.acc[1] = st.acc[2] = st.acc[3] = 0;
+}
+__device__ __forceinline__ void flush(State& st) {
+    if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1)
+        for (int k = 0; k < 4; ++k)
+            if (st.acc[k]) atomicAdd(&g_tl[4 * st.bin + k], st.acc[k]);
+    st.acc[0] = st.acc[1] = st.acc[2] = st.acc[3] = 0;
+}
+__device__ __forceinline__ void round(State& st, uint64_t busy, bool exhausted, uint32_t level) {
+    const unsigned long long t = now(), dt = t - st.last;
+    st.last = t;
+    const uint32_t b = (uint32_t)(t >> TL_SHIFT) & (uint32_t)(TL_BINS - 1);
+    if (b != st.bin) {
+        flush(st);
+        st.bin = b;
+    }
+    const unsigned long long n = (unsigned long long)__popcll(busy);
+    st.acc[0] += n * dt;
+    st.acc[1] += 64ull * dt;
+    if (exhausted) {
+        if (st.acc[2] == 0 && (int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1)
+            atomicMin(&g_tl[4 * TL_BINS], t);
+        st.acc[2] += n * dt;
+    }
+    if (level == 0) st.acc[3] += n * dt;
+}
+#else
+__device__ __forceinline__ unsigned long long now() { return 0; }
+__device__ __forceinline__ void init(State&) {}
+__device__ __forceinline__ void flush(State&) {}
+__device__ __forceinline__ void round(State&, uint64_t, bool, uint32_t) {}
+#endif
+}  // namespace timeline
+
 // DIAGNOSTIC exec-mask census (CPT_EXECDIAG builds only; never the timed library): lanes(out, r)
 // records one entry of code region r by the wave with its active-lane count -- out[r] entries,
 // out[16 + r] entries with <= 16 active lanes, out[32 + r] with <= 8, out[48 + r] the sum of

@@ -7,6 +7,7 @@ A pixel's stream depends only on (seed, x, y) (path_tracer.cu:36-42), so the sti
 bit-identical to a monolithic render (tests/test_multi_gpu_cpu.py on the oracle,
 tests/test_gpu_multirank.py through libcpt.so).
 """
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -16,14 +17,18 @@ from . import tiling
 class TileGather:
     """Buffers and the collective for one rank's share of a row-tiled frame."""
 
-    def __init__(self, width, height, world, rank, device, backend="nccl"):
+    def __init__(self, width, height, world, rank, device, backend="nccl", parts=None):
+        """parts: every rank's rows (a partition of the frame's rows, the same list on every
+        rank); default: the interleaved 8-row blocks (tiling.partition_rows)."""
         self.width, self.height, self.world, self.rank = width, height, world, rank
         self.backend = backend
-        self.rows = tiling.partition_rows(height, world, rank)
-        self.max_rows = tiling.max_rows(height, world)
+        if parts is None:
+            parts = [tiling.partition_rows(height, world, r) for r in range(world)]
+        self.rows = np.asarray(parts[rank], dtype=np.int32)
+        self.max_rows = max(int(p.size) for p in parts)
         self.send = torch.zeros((self.max_rows * width, 4), dtype=torch.float32, device=device)
         self.gathered = torch.zeros((world * self.max_rows * width, 4), dtype=torch.float32, device=device)
-        self.stitch_idx = torch.from_numpy(tiling.stitch_index(height, width, world)).to(device)
+        self.stitch_idx = torch.from_numpy(tiling.parts_stitch_index(parts, height)).to(device)
         self.device = torch.device(device)
 
     def __call__(self, renderer):

@@ -175,6 +175,17 @@ class Renderer:
             f |= CPT_SCHEDULE_CONSOLIDATE if consolidate else CPT_SCHEDULE_NO_CONSOLIDATE
         self._check(self._L.cpt_render(self._ctx, _p(c), spp, max_depth, f))
 
+    def tile_costs(self, cam, passes, max_depth, ordered=True):
+        """The cost schedule's pilot alone (cpt_tile_costs): each 8x8 tile's work over `passes`
+        passes from the current RNG states (nothing written back), [tiles_y, tiles_x] uint32."""
+        c = np.ascontiguousarray(np.array(cam, dtype=CAMERA_DTYPE))
+        ty, tx = (self.n_rows + 7) // 8, (self.width + 7) // 8
+        out = np.zeros((ty, tx), dtype=np.uint32)
+        f = CPT_TRAVERSAL_ORDERED if ordered else 0
+        f |= CPT_TRAVERSAL_PLAIN_LEAVES if ordered == "plain" else 0
+        self._check(self._L.cpt_tile_costs(self._ctx, _p(c), int(passes), int(max_depth), f, _p(out), out.size))
+        return out
+
     def synchronize(self):
         self._check(self._L.cpt_synchronize(self._ctx))
 
@@ -265,6 +276,13 @@ class Renderer:
         self._check(self._L.cpt_get_raw_counters(self._ctx, _p(out)))
         return [int(x) for x in out]
 
+    def debug_timeline(self):
+        """DIAGNOSTIC: the lane-occupancy timeline of a CPT_TIMELINE build (cpt_debug_timeline):
+        ([4096, 4] uint64 bins, first tick the queue ran dry); clears it."""
+        out = np.zeros(4 * 4096 + 4, dtype=np.uint64)
+        self._check(self._L.cpt_debug_timeline(self._ctx, _p(out), out.size))
+        return out[: 4 * 4096].reshape(4096, 4), int(out[4 * 4096])
+
     def diag_counters(self):
         """DIAGNOSTIC: the 16 stamp slots of a CPT_STAMPS build (cpt_stamps.hpp)."""
         out = np.zeros(16, dtype=np.uint64)
@@ -282,6 +300,14 @@ class Renderer:
         out = np.zeros(4, dtype=np.int32)
         self._check(self._L.cpt_get_walk_info(self._ctx, _p(out)))
         return dict(zip(("n_bvh", "n_walk", "n_wide", "n_unb"), (int(x) for x in out)))
+
+    def measure_read_pattern(self, bytes_per_lane, nbytes=1 << 30, iters=1):
+        """DIAGNOSTIC: GB/s of a streaming read in one of the display kernel's access shapes
+        (cpt_measure_read_pattern: 4, 12 or 16 bytes per lane)."""
+        out = ctypes.c_float(0.0)
+        self._check(self._L.cpt_measure_read_pattern(self._ctx, int(bytes_per_lane), int(nbytes), int(iters),
+                                                     ctypes.byref(out)))
+        return out.value
 
     def measure_read_bandwidth(self, nbytes=4 << 30, iters=10):
         """HBM streaming-read ceiling in GB/s (cpt_measure_read_bandwidth)."""

@@ -2,7 +2,8 @@
 
 Each rank renders the global rows of its interleaved 8-row blocks (block b -> rank
 b % world): the sky-heavy top rows and the object-heavy bottom rows are dealt evenly, so the
-ranks' work is balanced without a pilot pass.  A pixel's XORWOW stream depends only on
+ranks' work is balanced without a pilot pass.  Or (lpt_owner) the blocks are dealt by the work a
+short pilot of the whole frame measures, heaviest first to the least-loaded rank.  A pixel's XORWOW stream depends only on
 (seed, x, y) (path_tracer.cu:36-42), so any row partition gives results bit-identical to a
 monolithic render.  After the render, the fp32 accumulator tiles are gathered into one
 framebuffer with a single all-gather (RCCL over xGMI on MI355X; gloo in the CPU tests).
@@ -24,6 +25,46 @@ def weak_scaled_size(width: int, height: int, world: int) -> tuple:
 def partition_rows(height: int, world: int, rank: int, block: int = BLOCK_ROWS) -> np.ndarray:
     ys = np.arange(height, dtype=np.int32)
     return ys[(ys // block) % world == rank]
+
+
+def lpt_owner(block_costs, world: int) -> np.ndarray:
+    """Cost-balanced partition of row blocks (longest processing time first): blocks heaviest
+    first (ties by block index), each to the rank with the least cost so far (ties to the lowest
+    rank).  A pure function of the costs, so every rank computes the same partition from the same
+    pilot without exchanging anything.  Returns the owning rank of each block."""
+    costs = np.asarray(block_costs, dtype=np.int64)
+    order = sorted(range(costs.size), key=lambda b: (-int(costs[b]), b))
+    load = [0] * world
+    owner = np.empty(costs.size, dtype=np.int32)
+    for b in order:
+        r = min(range(world), key=lambda k: (load[k], k))
+        owner[b] = r
+        load[r] += int(costs[b])
+    return owner
+
+
+def rows_of_owner(height: int, owner, rank: int, block: int = BLOCK_ROWS) -> np.ndarray:
+    """The rows of the blocks `owner` gives to `rank` (ascending)."""
+    ys = np.arange(height, dtype=np.int32)
+    return ys[np.asarray(owner)[ys // block] == rank]
+
+
+def block_costs_from_tiles(tile_costs, block: int = BLOCK_ROWS) -> np.ndarray:
+    """Per row block cost from the pilot's per 8x8 tile costs (Renderer.tile_costs of the whole
+    frame): a block of 8 rows is one row of tiles."""
+    assert block == 8, "the pilot's tiles are 8 rows high"
+    return np.asarray(tile_costs, dtype=np.int64).sum(axis=1)
+
+
+def parts_stitch_index(parts, height: int) -> np.ndarray:
+    """Row gather index for any partition (parts[r] = rank r's rows, each rank's tile padded to
+    the largest): framebuffer row y = gathered row idx[y]."""
+    mr = max(int(p.size) for p in parts)
+    idx = np.full(height, -1, dtype=np.int64)
+    for r, rows in enumerate(parts):
+        idx[rows] = r * mr + np.arange(rows.size)
+    assert (idx >= 0).all(), "the partition must cover every row"
+    return idx
 
 
 def max_rows(height: int, world: int, block: int = BLOCK_ROWS) -> int:

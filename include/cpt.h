@@ -265,6 +265,13 @@ int cpt_read_aux(cpt_ctx* ctx, float* normal3, float* depth); /* either may be N
  * With cpt_write_rng, a render (and the display path) resumes bit for bit. */
 int cpt_write_accum(cpt_ctx* ctx, const float* rgba);
 int cpt_write_aux(cpt_ctx* ctx, const float* normal3, const float* depth);
+/* The cost schedule's pilot alone (for cost-balanced row partitions across ranks, tiling.py):
+ * `passes` passes from the context's current RNG states (nothing is written back), each 8x8 tile's
+ * work -- segments + node visits + primitive tests, the walk of `flags`' CPT_TRAVERSAL_* bits --
+ * into out[tile] (tiles row-major over the context's rows: ((n_rows+7)/8) x ((width+7)/8);
+ * n_out at least that).  Synchronous. */
+int cpt_tile_costs(cpt_ctx* ctx, const cpt_camera* cam, int passes, int max_depth, uint32_t flags, uint32_t* out,
+                   size_t n_out);
 /* Device-to-device copy of the accumulator (e.g. into an RCCL send buffer), ordered against the
  * caller's HIP stream `caller_stream` (NULL: the null stream) without blocking the host: the
  * context's stream first waits for the work queued on caller_stream so far (a fill of dst, a
@@ -301,6 +308,12 @@ int cpt_reset_stats(cpt_ctx* ctx);
  * winner certificate and took the reference walk (CPT_RENDER_STATS | CPT_TRAVERSAL_ORDERED);
  * 6 = 4-wide node visits read from global memory, i.e. past the LDS image's first 512 nodes). */
 int cpt_get_raw_counters(cpt_ctx* ctx, uint64_t* out8);
+/* DIAGNOSTIC (a library built with CPT_TIMELINE; CPT_ERR_STATE otherwise): the megakernel's
+ * lane-occupancy timeline since the last call, n words (<= 4 x 4096 + 4): per 1.31 ms bin of
+ * the device's 100 MHz clock (a ring of 4096 bins) busy-lane x ticks, wave x 64 x ticks, busy-lane
+ * x ticks after the pixel queue ran dry, of level-0 waves; then the first tick a wave saw the
+ * queue dry.  Clears it (tools/timeline.py). */
+int cpt_debug_timeline(cpt_ctx* ctx, uint64_t* out, int n);
 /* DIAGNOSTIC: the 16 wave-time stamp slots of a CPT_STAMPS build (cpt_stamps.hpp; all zero in
  * the shipped library), summed over the renders since the last cpt_reset_stats. */
 int cpt_get_diag_counters(cpt_ctx* ctx, uint64_t* out16);
@@ -364,6 +377,11 @@ int cpt_reset_display(cpt_ctx* ctx);
  * the box): `iters` grid-stride 16-B-per-lane read passes over a fresh `bytes`-byte buffer
  * (use >> 256 MiB so the Infinity Cache cannot serve it), GB/s from HIP events. */
 int cpt_measure_read_bandwidth(cpt_ctx* ctx, size_t bytes, int iters, float* gbps);
+/* DIAGNOSTIC: the same streaming read in the display kernel's access shapes, bytes_per_lane 4 (one
+ * float per lane), 12 (three consecutive floats per lane) or 16 (one float4), one kernel
+ * (k_read_pattern<bpl>) per shape: the known byte counts a rocprofv3 FETCH_SIZE pass is calibrated
+ * against (tools/fetch_calibration.py). */
+int cpt_measure_read_pattern(cpt_ctx* ctx, int bytes_per_lane, size_t bytes, int iters, float* gbps);
 /* Host-only test hook (no GPU): the cap-disk bound a cylinder leaf carries (cpt_capi.cpp
  * cap_disk_bound), the largest float c with  sqrtf(q) < radius  <=>  q <= c  for every float
  * q; the kernels decide the reference's cap test (object.cu:52-77) with it. */

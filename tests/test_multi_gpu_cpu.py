@@ -91,3 +91,69 @@ def test_weak_scaled_sizes():
         assert abs(w / h - 16 / 9) < 0.01
         rows = [tiling.partition_rows(h, n, r).size for r in range(n)]
         assert sum(rows) == h and max(rows) - min(rows) <= tiling.BLOCK_ROWS
+
+
+def _worker_parts(rank, world, port, W, H, spp, depth, owner, q):
+    """As _worker, with a cost-balanced partition (tiling.lpt_owner) and the parts stitch index."""
+    import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sky = texture_io.load_cptex()
+    objs = scenes.scene_s1000()
+    cam = oracle.camera_get_copy(scenes.camera_for(W, H))
+    parts = [tiling.rows_of_owner(H, owner, r) for r in range(world)]
+    rows = parts[rank]
+    rng = oracle.init_rng(1234, W, rows)
+    acc, _, _, _ = oracle.render(objs, cam, sky, rows, spp, depth, rng)
+    mr = max(p.size for p in parts)
+    send = torch.zeros((mr * W, 4), dtype=torch.float32)
+    send[: rows.size * W] = torch.from_numpy(acc)
+    gathered = torch.zeros((world * mr * W, 4), dtype=torch.float32)
+    dist.all_gather_into_tensor(gathered, send)
+    if rank == 0:
+        idx = tiling.parts_stitch_index(parts, H)
+        q.put(gathered.numpy().reshape(world * mr, W, 4)[idx].reshape(H * W, 4))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_balanced_partition_render_equals_monolithic(oracle_mod, sky):
+    """A cost-balanced row partition (blocks of uneven cost, so the ranks hold different row
+    counts) stitched through parts_stitch_index equals the monolithic render bit for bit."""
+    W, H, spp, depth, world = 24, 44, 2, 8, 2
+    costs = [50, 3, 40, 7, 9, 1]            # 6 blocks of 8 rows (the last one 4 rows)
+    owner = tiling.lpt_owner(costs, world)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_parts, args=(r, world, port, W, H, spp, depth, owner, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    fb = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    objs = scenes.scene_s1000()
+    cam = oracle_mod.camera_get_copy(scenes.camera_for(W, H))
+    rows = np.arange(H, dtype=np.int32)
+    mono, _, _, _ = oracle_mod.render(objs, cam, sky, rows, spp, depth, oracle_mod.init_rng(1234, W, rows))
+    np.testing.assert_array_equal(fb.view(np.uint32), mono.view(np.uint32))
+
+
+def test_lpt_owner():
+    """Longest-processing-time assignment: every block owned once, deterministic, and the
+    heaviest rank within the largest block of the lightest one (the LPT bound)."""
+    rng = np.random.default_rng(3)
+    for world in (1, 2, 3, 8):
+        costs = rng.integers(1, 1000, 270)
+        owner = tiling.lpt_owner(costs, world)
+        assert owner.min() >= 0 and owner.max() < world
+        assert np.array_equal(owner, tiling.lpt_owner(costs.copy(), world))
+        loads = np.bincount(owner, weights=costs, minlength=world)
+        assert loads.max() - loads.min() <= costs.max()
+        parts = [tiling.rows_of_owner(2160, owner, r) for r in range(world)]
+        assert np.array_equal(np.sort(np.concatenate(parts)), np.arange(2160))
+        idx = tiling.parts_stitch_index(parts, 2160)
+        assert np.unique(idx).size == 2160
+    # ties: blocks of equal cost go to ranks in index order
+    assert list(tiling.lpt_owner([5, 5, 5, 5], 2)) == [0, 1, 0, 1]
