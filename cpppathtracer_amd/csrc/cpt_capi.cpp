@@ -388,6 +388,17 @@ static void fill_params(cpt_ctx* c, const cpt_camera* cam, int spp, int max_dept
     p.publish_wait_log2 = c->publish_wait_log2;
 }
 
+// The cost schedule's pilot: min(CPT_PILOT_MAX, max(1, spp / CPT_PILOT_DIV)) passes, ranking the 8x8
+// tiles by their heaviest pixel.  Round 6 (interleaved, profiles/r06/keymax/): with the max key,
+// up to 16 passes at one per 128 spp against round 5's 4 at one per 512: C4 2182-2198 vs 2065-2072
+// Mpaths/s (8 passes at one per 256: 2159-2175), C5 N = 8 slowest rank 2101 vs 2388 ms; C2 / C3
+// unchanged.
+#ifndef CPT_PILOT_MAX
+#define CPT_PILOT_MAX 16
+#endif
+#ifndef CPT_PILOT_DIV
+#define CPT_PILOT_DIV 128
+#endif
 int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32_t flags) {
     if (!c || !cam) return CPT_ERR_INVALID_ARG;
     if (spp < 0 || max_depth < 0 || max_depth > (int)cpt::MAX_RECURSION_DEPTH_SET)
@@ -448,8 +459,8 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
             prev_schedule = true;
         }
         if ((flags & CPT_SCHEDULE_COST) && spp > 0 && c->n_rows > 0) {
-            // pilot: 1 pass per 512 (1..4), then the tiles sorted heaviest first
-            const int passes = std::min(4, std::max(1, spp / 512));
+            // pilot: 1 pass per 128 (1..16), then the tiles sorted by their heaviest pixel, first
+            const int passes = std::min(CPT_PILOT_MAX, std::max(1, spp / CPT_PILOT_DIV));
             const size_t n_tiles = (size_t)((c->width + 7) / 8) * ((c->n_rows + 7) / 8);
             const size_t bytes = cpt::tile_schedule_scratch_bytes(c->width, c->n_rows);
             if (c->cap_sched < bytes) {

@@ -36,7 +36,7 @@ namespace cpt {
 //
 // PROBE (the cost schedule's pilot, DESIGN.md §Cost schedule): the same passes from the same
 // RNG states, but nothing is written back except each pixel's work (segments + node visits +
-// primitive tests) added to its tile's cost.
+// primitive tests), whose maximum over the tile's pixels is the tile's cost.
 // ======================================================================================
 // TAIL CONSOLIDATION (LDS walk, p.resume != nullptr).  Once the pixel
 // queue is drained, chains finish and the waves thin out, but every wave keeps its SIMD slot
@@ -90,9 +90,6 @@ __device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int&
 }
 
 // Scheduling constants (SUSPEND_AT, STATIC_FIRST, DEFER_MISS_ROUND, CPT_LDS_BLOCK): cpt_tuning.hpp.
-#ifndef CPT_TILE_KEY_MAX
-#define CPT_TILE_KEY_MAX 0
-#endif
 
 // LDST: the 4-wide walk tree's compact image (its first LDS_TREE_NODES nodes: the top of the
 // tree) is staged in LDS once per workgroup, and the walk reads those nodes there (a lane's
@@ -570,11 +567,10 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             const KParams& p = kernarg_params();   // cold fields (see the refill)
             if (PROBE) {
                 // ---- pilot: the pixel's work goes to its tile's cost ----------------------
-#if CPT_TILE_KEY_MAX   // A/B: a tile's key is its heaviest pixel's pilot work
+                // the tile's key is its heaviest pixel's work, not the tile's sum (round 6): one long
+                // chain in an otherwise light tile must start with the first tiles, not in the tail
+                // (tools/timeline.py: C5 N = 8, the rank's last quarter ran a few hundred such chains)
                 atomicMax(&p.tile_cost[L.tile], cnt.segments + cnt.nodes + cnt.prims - work_at_take);
-#else
-                atomicAdd(&p.tile_cost[L.tile], cnt.segments + cnt.nodes + cnt.prims - work_at_take);
-#endif
             } else {
                 // ---- pixel finished: write back (path_tracer.cu:172-174) -----------------
                 execdiag::lanes(p.stats + 64, 11);
