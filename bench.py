@@ -68,6 +68,10 @@ def parse_args(argv=None):
                     help="megakernel pixel dequeue order: 8x8 tiles heaviest first from a pilot pass "
                          "(CPT_SCHEDULE_COST), or tiles in row-major order; auto: cost from 64 passes up "
                          "(the pilot is one pass: a quarter of C1's 4-pass frame, C1 1043 vs 1556 Mpaths/s)")
+    ap.add_argument("--partition", default="interleaved", choices=["interleaved", "balanced"],
+                    help="N > 1: each rank's rows -- interleaved 8-row blocks (block b to rank b mod N), or the "
+                         "blocks dealt by a 4-pass pilot of the whole frame, heaviest first to the least-loaded "
+                         "rank (tiling.lpt_owner; every rank computes the same partition at setup)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong (default): the config's image (C4: 1920x1080, the metric's resolution) at every N; "
                          "weak: pixels per GPU fixed (image grows by sqrt(N))")
@@ -253,6 +257,8 @@ def run(args):
     sky = texture_io.load_cptex()
     cam = camera_get_copy(scenes.camera_for(W, H))
     rows = tiling.partition_rows(H, world, rank)
+    parts = None
+    partition_pilot_ms = None
 
     def _all_reduce(x, op=dist.ReduceOp.SUM):
         if backend == "nccl":
@@ -272,6 +278,17 @@ def run(args):
     r.set_stream(stream.cuda_stream)
     r.set_scene(objs)
     r.set_env(sky)
+    if args.partition == "balanced" and world > 1:
+        # setup, not timed: a pilot of the whole frame, identical on every rank (same scene, camera,
+        # seed), gives each 8-row block's work; every rank deals the blocks the same way
+        t_p = time.perf_counter()
+        r.set_frame(W, H)
+        r.init_rng(cfg["seed"])
+        owner = tiling.lpt_owner(tiling.block_costs_from_tiles(r.tile_costs(cam, 4, depth, ordered=args.walk == "ordered")),
+                                 world)
+        parts = [tiling.rows_of_owner(H, owner, k) for k in range(world)]
+        rows = parts[rank]
+        partition_pilot_ms = round((time.perf_counter() - t_p) * 1e3, 2)
     r.set_frame(W, H, rows)
     t_init = time.perf_counter()
     r.init_rng(cfg["seed"])
@@ -279,7 +296,7 @@ def run(args):
     t_init = time.perf_counter() - t_init
 
     npix_local = rows.size * W
-    gather = multigpu.TileGather(W, H, world, rank, dev, backend) if use_pg else None
+    gather = multigpu.TileGather(W, H, world, rank, dev, backend, parts=parts) if use_pg else None
     kernel_events = []
     ordered = args.walk == "ordered"
     schedule = args.schedule if args.path == "megakernel" else "tiles"
@@ -443,10 +460,14 @@ def run(args):
                 # strong (default since round 4): the config's own frame at every N; weak: pixels per
                 # GPU fixed.  N > 1 values of rounds 1-3 were weak-scaled
                 "scaling": args.scaling,
-                "parallelism": f"row-tiled x{world} (interleaved {tiling.BLOCK_ROWS}-row blocks){collective}",
+                "parallelism": (f"row-tiled x{world} (interleaved {tiling.BLOCK_ROWS}-row blocks){collective}"
+                                if parts is None else
+                                f"row-tiled x{world} ({tiling.BLOCK_ROWS}-row blocks dealt by a pilot's cost){collective}"),
             },
             "rng_init_ms": round(t_init * 1e3, 2),
         }
+        if partition_pilot_ms is not None:
+            out["partition_pilot_ms"] = partition_pilot_ms   # setup, outside the timed steps
         if other:
             out[f"{other.pop('mode')}_scaling"] = other
         if st is not None:

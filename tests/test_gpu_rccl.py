@@ -186,3 +186,20 @@ def test_tilegather_copy_ordered_against_torch_stream(sky):
         g.send.fill_(float("nan"))                     # a late writer of `send` on torch's stream
         got = g(r).reshape(H * W, 4).cpu().numpy()
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_bench_two_ranks_balanced_partition():
+    """bench.py --gpus 2 --partition balanced, the two ranks sharing this box's GPU (gloo host
+    copies): every rank deals the 8-row blocks by the same whole-frame pilot (tiling.lpt_owner),
+    the stitched frame's walk parity count is 0 and the line names the partition."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--config", "c4", "--width", "256",
+           "--height", "120", "--spp", "8", "--steps", "1", "--warmup", "1", "--partition", "balanced",
+           "--no-cpu-baseline", "--no-hbm-probe", "--no-strong-check"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", CPT_BENCH_BACKEND="gloo")
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 2
+    assert "pilot's cost" in out["config"]["parallelism"]
+    assert out["roofline"]["walk_vs_reference_pixels_differing"] == 0
+    assert out["partition_pilot_ms"] > 0
