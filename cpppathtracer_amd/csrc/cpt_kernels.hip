@@ -1436,6 +1436,8 @@ __global__ void __launch_bounds__(64) k_tile_draws(const uint32_t* __restrict__ 
         draws = (d - d_prev[pix]) * INV;
         d_prev[pix] = d;
     }
+    // (the sum: keying 1-spp tiles by their heaviest pixel's draws, as the cost pilot does, was
+    // slower here, 1.59-1.62 vs 1.57-1.59 ms per pass, profiles/r06/ab_prevmax.log)
     const uint64_t sum = wave_sum(draws);
     if (k == 0) cost[tile] = (uint32_t)(sum < 0xffffffffull ? sum : 0xffffffffull);
 }
