@@ -23,9 +23,7 @@
 // C4 DispatchRay loop, three interleaved rounds (profiles/r05/ab_dispatch_order_every.log): every
 // render 1.71-1.72 ms per pass, every 4th 1.66-1.68, every 8th 1.65-1.66; the 1-spp render itself
 // is unchanged (1.42-1.43), so the staler order costs nothing measurable.
-#ifndef CPT_PREV_ORDER_EVERY
-#define CPT_PREV_ORDER_EVERY 8
-#endif
+constexpr int PREV_ORDER_EVERY = 8;
 
 static_assert(sizeof(cpt_material) == 40, "cpt_material must match Material (40 B)");
 static_assert(sizeof(cpt_object) == 72, "cpt_object must match Object (72 B)");
@@ -388,17 +386,12 @@ static void fill_params(cpt_ctx* c, const cpt_camera* cam, int spp, int max_dept
     p.publish_wait_log2 = c->publish_wait_log2;
 }
 
-// The cost schedule's pilot: min(CPT_PILOT_MAX, max(1, spp / CPT_PILOT_DIV)) passes, ranking the 8x8
+// The cost schedule's pilot: min(PILOT_MAX, max(1, spp / PILOT_DIV)) passes, ranking the 8x8
 // tiles by their heaviest pixel.  Round 6 (interleaved, profiles/r06/keymax/): with the max key,
 // up to 16 passes at one per 128 spp against round 5's 4 at one per 512: C4 2182-2198 vs 2065-2072
 // Mpaths/s (8 passes at one per 256: 2159-2175), C5 N = 8 slowest rank 2101 vs 2388 ms; C2 / C3
 // unchanged.
-#ifndef CPT_PILOT_MAX
-#define CPT_PILOT_MAX 16
-#endif
-#ifndef CPT_PILOT_DIV
-#define CPT_PILOT_DIV 128
-#endif
+constexpr int PILOT_MAX = 16, PILOT_DIV = 128;
 int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32_t flags) {
     if (!c || !cam) return CPT_ERR_INVALID_ARG;
     if (spp < 0 || max_depth < 0 || max_depth > (int)cpt::MAX_RECURSION_DEPTH_SET)
@@ -460,7 +453,7 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
         }
         if ((flags & CPT_SCHEDULE_COST) && spp > 0 && c->n_rows > 0) {
             // pilot: 1 pass per 128 (1..16), then the tiles sorted by their heaviest pixel, first
-            const int passes = std::min(CPT_PILOT_MAX, std::max(1, spp / CPT_PILOT_DIV));
+            const int passes = std::min(PILOT_MAX, std::max(1, spp / PILOT_DIV));
             const size_t n_tiles = (size_t)((c->width + 7) / 8) * ((c->n_rows + 7) / 8);
             const size_t bytes = cpt::tile_schedule_scratch_bytes(c->width, c->n_rows);
             if (c->cap_sched < bytes) {
@@ -497,10 +490,10 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
         HIP_TRY(c, hipEventRecord(c->ev_main, s));
         HIP_TRY(c, cpt::launch_megakernel(p, (flags & CPT_RENDER_STATS) != 0, aux, s));
         HIP_TRY(c, hipEventRecord(c->ev_stop, s));
-        if (prev_schedule && (!c->prev_order_valid || ++c->prev_since_order >= CPT_PREV_ORDER_EVERY)) {
+        if (prev_schedule && (!c->prev_order_valid || ++c->prev_since_order >= PREV_ORDER_EVERY)) {
             // the next render's order from this one's draws (after the timed events: the render's
             // own time is the kernel's; the stream runs this before the caller's next work).
-            // Refreshed every CPT_PREV_ORDER_EVERY renders: the draws then span those renders (the
+            // Refreshed every PREV_ORDER_EVERY renders: the draws then span those renders (the
             // RNG's d word counts them all), and the order, a heuristic, costs ~65 us to rebuild
             const size_t n_tiles = (size_t)((c->width + 7) / 8) * ((c->n_rows + 7) / 8);
             const size_t bytes = cpt::tile_schedule_scratch_bytes(c->width, c->n_rows);

@@ -413,9 +413,6 @@ __device__ __forceinline__ void sincos_2pi(float phi, double& s, double& c, bool
     ok = phi >= 0.0f && phi <= 6.28318548f && sure_f32(s) && sure_f32(c);
 }
 
-#ifndef CPT_FM   // A/B: bit 0 the lobe's short forms, bit 1 the sky fetch's (0 = round 5's full sequences)
-#define CPT_FM 3
-#endif
 __device__ const double g_at_tab[2 * (FM_AT_N + 1)] = CPT_FM_AT_TABLE_INIT;   // {atan(k/32), pi/2 - atan(k/32)}
 
 // atan(n / m) for n >= 0, m > 0 (else ok = false): with k = round(32 min(n/m, m/n)) from a float
@@ -453,7 +450,6 @@ __device__ __forceinline__ double atan_ratio(double n, double m, bool& ok) {
 // Miss's atanf(d.y / d.x) (path_tracer.cu:120): (float)dm::atan((double)x) through fm::atan_ratio
 // (|x| over 1), the full sequence where its guard fails (test_miss_atan_asin_exhaustive).
 __device__ __forceinline__ float miss_atanf(float x) {
-    if (!(CPT_FM & 2)) return dm::atanf_(x);
     bool ok;
     const double a = fm::atan_ratio(__builtin_fabs((double)x), 1.0, ok);
     float f = (float)(x < 0.0f ? -a : a);
@@ -465,7 +461,6 @@ __device__ __forceinline__ float miss_atanf(float x) {
 // fm::atan_ratio takes |z| over the same square root directly, so neither the quotient's divide
 // nor a second atan reduction runs; the full sequence where the guard fails (z = +-1, 0, NaN).
 __device__ __forceinline__ float miss_asinf(float z) {
-    if (!(CPT_FM & 2)) return dm::asinf_(z);
     const double x = (double)z;
     bool ok;
     const double a = fm::atan_ratio(__builtin_fabs(x), __builtin_sqrt((1.0 - x) * (1.0 + x)), ok);
@@ -479,7 +474,6 @@ __device__ __forceinline__ float miss_asinf(float z) {
 // checked on the host against the oracle and on the device (test_lobe_pow_exhaustive); the
 // other exponents through fm::pow_unit, the dm:: sequence where its guard fails.
 __device__ __forceinline__ float lobe_pow(float x, double y) {
-    if (!(CPT_FM & 1)) return (float)dm::pow((double)x, y);
     if (y == 0.5 && x >= 0x1p-42f) return sqrt_nn(x);
     bool ok;
     const double d = fm::pow_unit(x, y, ok);
@@ -491,7 +485,6 @@ __device__ __forceinline__ float lobe_pow(float x, double y) {
 // sinf / cosf of the lobe's phi = (float)(2 pi x_2) in [0, 2 pi] (material.cu:26-27,47-48):
 // fm::sincos_2pi, dm::sincosf_ where its guard fails (test_lobe_sincos_exhaustive).
 __device__ __forceinline__ void lobe_sincos(float phi, float* s_out, float* c_out) {
-    if (!(CPT_FM & 1)) return dm::sincosf_(phi, s_out, c_out);
     double s, c;
     bool ok;
     fm::sincos_2pi(phi, s, c, ok);

@@ -97,8 +97,8 @@ __device__ __forceinline__ bool decode_pixel(const KParams& p, uint32_t id, int&
 // step of the walk); a larger tree's other nodes come from the image in global memory.
 // One LDS workgroup per CU: 16 waves, 4 per SIMD (the image, the 16-bit stacks and the pending
 // sky fetches take 156 KB of the CU's 160 KB), which caps the kernel at 128 VGPRs.
-template <bool LDST> constexpr int mk_block() { return LDST ? CPT_LDS_BLOCK : 256; }
-template <bool LDST> constexpr int mk_waves() { return LDST ? CPT_LDS_BLOCK / 256 : CPT_WAVES_PER_SIMD; }
+template <bool LDST> constexpr int mk_block() { return LDST ? LDS_BLOCK : 256; }
+template <bool LDST> constexpr int mk_waves() { return LDST ? LDS_BLOCK / 256 : WAVES_PER_SIMD; }
 
 // HYB (LDST): the wide tree has more nodes than the LDS image holds; the rest are read from
 // global memory (cpt_path.hpp load_wide_node).
@@ -173,11 +173,10 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     const bool stat = STATIC_FIRST && LDST && !PROBE && p.lanes == 64 && p.tile_order != nullptr;
     const uint32_t n_static = gridDim.x * (uint32_t)BLK;
     bool first_take = true;
-    // CPT_TAKE_BATCH: the wave's reserved ids [res_id, res_end), the counter position it last
-    // saw, and whether the counter has run past the image (all wave-uniform)
+    // batched takes: the wave's reserved ids [res_id, res_end), the counter position it last saw,
+    // and whether the counter has run past the image (all wave-uniform)
     uint32_t res_id = 0, res_end = 0, res_seen = 0;
     bool counter_done = false;
-    (void)res_id; (void)res_end; (void)res_seen; (void)counter_done;
     stamps::init();
     timeline::State tl;
     timeline::init(tl);
@@ -185,7 +184,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         stamps::lap(5);
         stamps::count(8);
         timeline::round(tl, __ballot(busy), exhausted, level);
-        if (cons && !retiring && level > 0 && exhausted && vq[3] == 0u && vq[2] <= level * (uint32_t)CPT_CONS_RETIRE_PER_LEVEL) retiring = true;
+        if (cons && !retiring && level > 0 && exhausted && vq[3] == 0u && vq[2] <= level * (uint32_t)CONS_RETIRE_PER_LEVEL) retiring = true;
         bool begin = false;   // a lane took a chain: start its next pass
         // ---- take handed-over chains into idle lanes (consolidation) ---------------------
         if (cons && !retiring && exhausted) {
@@ -263,57 +262,44 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                     if (n_static >= n_work) exhausted = true;
                     lane_id = base + lane_rank(need);
                 }
-#if CPT_TAKE_BATCH
                 else if (p.replicate == 1) {
-                    // Batched take: the wave draws a tile's worth of ids (CPT_TAKE_BATCH = 64) from
-                    // the counter and serves its idle lanes from that range over the next rounds,
-                    // so the device atomic on the one counter every wave of the grid contends for
-                    // is issued once per 64 takes instead of once per round (at 1 spp a wave
-                    // takes ~11 pixels every round: 2.43 -> 1.43 ms per 1-spp C4 render,
-                    // DESIGN.md §The reference's per-pass loop).  Near the end of the image (less
-                    // than one id per lane of the grid left) it draws only what it needs, so no
-                    // wave sits on unstarted pixels while others run dry.  Pixels are independent
-                    // chains, so the order they are taken in does not change the image.
+                    // Batched take: the wave draws a tile's worth of ids (TAKE_BATCH = 64) from the
+                    // counter and serves its idle lanes from that range over the next rounds, so the
+                    // device atomic on the one counter every wave of the grid contends for is issued
+                    // once per 64 takes instead of once per round (at 1 spp a wave takes ~11 pixels
+                    // every round: 2.43 -> 1.43 ms per 1-spp C4 render).  Pixels
+                    // are independent chains, so the order they are taken in does not change the image.
                     const uint32_t n_need = wave_count(need);
                     const uint32_t avail = res_end - res_id;
                     const uint32_t off = stat ? n_static : 0u;
                     uint32_t nb = 0, ncnt = 0;
                     if (n_need > avail && !counter_done) {
                         const uint32_t want = n_need - avail;
-                        // long chains (spp >= 64): smaller ranges, since a wave's unstarted ids then hold
-                        // back long chains other waves' idle lanes could run
-                        const uint32_t bsz = p.spp >= 64 ? (uint32_t)CPT_TAKE_BATCH_LONG : (uint32_t)CPT_TAKE_BATCH;
-                        // the consolidating kernel (frames of <= 4 pixels per lane) takes exactly what it needs.
-                        // Near the end of the image (less than one id per lane of the grid left) a
-                        // wave draws only what it needs.  `res_seen` is the counter as this wave saw
-                        // it at its last draw; a wave on long chains draws rarely, so with
-                        // CPT_TAKE_FRESH its leader reads the counter's current value first (one
-                        // relaxed load per draw, i.e. per ~64 takes at spp >= 64).
+                        // `res_seen` is the counter as this wave saw it at its last draw; a wave on
+                        // long chains (spp >= 64) draws rarely, so its leader reads the counter's
+                        // current value first, until its last draw fell inside the tail (the counter
+                        // only grows, so a wave once in the tail stays there)
                         uint32_t seen = res_seen;
-#if CPT_TAKE_FRESH
-                        // (CPT_TAKE_FRESH 2: only while this wave's last draw left more than the tail:
-                        // the counter only grows, so a wave once in the tail stays there)
-                        if (p.spp >= 64 && (CPT_TAKE_FRESH == 1 || res_seen + n_static < n_work)) {
+                        if (p.spp >= 64 && res_seen + n_static < n_work) {
                             uint32_t cur = 0;
                             if (lane == leader) cur = __hip_atomic_load(p.work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             seen = __builtin_amdgcn_readfirstlane(__shfl(cur, leader)) + off;
                         }
-#endif
-                        uint32_t bsz_k = CONS ? (uint32_t)CPT_TAKE_BATCH_CONS_SIZE : bsz;
+                        uint32_t bsz = (uint32_t)TAKE_BATCH;
                         const uint32_t left_ids = n_work > seen ? n_work - seen : 0u;
-#if CPT_TAKE_TAPER
-                        // long chains: the range shrinks with what is left (guided scheduling), so
-                        // the ids waves hold unstarted never amount to more than 1/TAPER of a round
-                        // of the grid's lanes
+                        // long chains: the range shrinks with what is left (guided scheduling), so the
+                        // ids waves hold unstarted never amount to more than 1/TAKE_TAPER of a round of
+                        // the grid's lanes; short chains draw exactly what they need once less than
+                        // one id per lane of the grid is left
                         if (p.spp >= 64) {
-                            const uint64_t t = (uint64_t)bsz_k * left_ids / ((uint64_t)n_static * CPT_TAKE_TAPER);
-                            bsz_k = t < bsz_k ? (uint32_t)t : bsz_k;
+                            const uint64_t t = (uint64_t)bsz * left_ids / ((uint64_t)n_static * TAKE_TAPER);
+                            bsz = t < bsz ? (uint32_t)t : bsz;
                         }
                         const bool batch_ok = p.spp >= 64 || left_ids > n_static;
-#else
-                        const bool batch_ok = left_ids > n_static;
-#endif
-                        const uint32_t grab = (!CONS || CPT_TAKE_BATCH_CONS) && batch_ok && bsz_k > want ? bsz_k : want;
+                        // the consolidating kernel (frames of <= 4 pixels per lane) takes exactly what
+                        // it needs: there a wave's unstarted ids hold back chains other waves' idle
+                        // lanes could run
+                        const uint32_t grab = !CONS && batch_ok && bsz > want ? bsz : want;
                         if (lane == leader) nb = atomicAdd(p.work, grab);
                         nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader)) + off;
                         ncnt = grab;
@@ -332,7 +318,6 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                     }
                     if (counter_done && res_id >= res_end) exhausted = true;
                 }
-#endif
                 else {
                     // DIAGNOSTIC p.replicate > 1: every taken pixel runs on that many lanes, as
                     // identical copies (tools/lane_latency.py); 1 in normal use
@@ -393,10 +378,10 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         }
         stamps::lap(0);
         if (!__any(busy)) {
-            // (a wave whose takes all fell outside the frame takes again while ids remain: with
-            // CPT_TAKE_BATCH it may still hold reserved ids, which no other wave would render)
+            // (a wave whose takes all fell outside the frame takes again while ids remain: it may
+            // still hold reserved ids, which no other wave would render)
             if (!cons || retiring) {
-                if (CPT_TAKE_BATCH && !exhausted) continue;
+                if (!exhausted) continue;
                 break;
             }
             if (exhausted) {

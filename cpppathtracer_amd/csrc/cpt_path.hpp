@@ -917,31 +917,9 @@ __device__ __forceinline__ int trace_wide(const KParams& p, __amdgpu_buffer_rsrc
 // the binary octant orders testing each leaf where the walk meets it.
 // Returns 1 hit, 0 miss, or 2 when the walk was suspended (only with suspend_at > 0; the
 // lane calls again in a later round with the same ray and `ws`).
-// The walks a C4 frame never (or almost never) takes -- the reference-order fallback after a failed
-// certificate (1.4e-4 of segments), the NaN-ray walk, and in the LDS kernels the binary octant walk
-// of trees without a wide image -- out of line (CPT_COLD_NOINLINE), so the timed kernel's hot code
-// is smaller (instruction cache).  One copy per (STATS, FAST, CONS).
-template <bool STATS, bool FAST, bool CONS>
-__device__ __noinline__ int trace_cold(__amdgpu_buffer_rsrc_t rsrc, uint32_t base, int n, RayK ray, Hit* h, int* code,
-                                       Counters* cnt) {
-    const BufSrc src{rsrc, base};
-    Hit hh;
-    int cc = -1;
-    Counters c = *cnt;
-    const int r = trace<STATS, FAST, CONS>(src, n, ray, hh, cc, c);
-    *cnt = c;
-    *h = hh;
-    *code = cc;
-    return r;
-}
-
 template <bool STATS, bool FAST, bool CONS = false>
 __device__ __forceinline__ int trace_any(__amdgpu_buffer_rsrc_t rsrc, uint32_t base, int n, const RayK& ray, Hit& h,
-                                         int& code, Counters& cnt, bool cold) {
-#if CPT_COLD_NOINLINE
-    if (cold) return trace_cold<STATS, FAST, CONS>(rsrc, base, n, ray, &h, &code, &cnt);
-#endif
-    (void)cold;
+                                         int& code, Counters& cnt) {
     return trace<STATS, FAST, CONS>(BufSrc{rsrc, base}, n, ray, h, code, cnt);
 }
 
@@ -961,14 +939,14 @@ __device__ __forceinline__ int trace_segment(const KParams& p, const RayK& rk, b
         }
         if (!wide) {
             const uint32_t base = walk_order(p, rk.d, n) * (uint32_t)sizeof(Node);
-            r = trace_any<STATS, true, true>(rsrc, base, n, rk, h, code, cnt, LDST);
+            r = trace_any<STATS, true, true>(rsrc, base, n, rk, h, code, cnt);
         }
         if (__builtin_expect(r >= 0, 1)) return r;
         if (STATS) cnt.fallbacks++;
     }
     const RayK rs = with_slab(rk);
-    if (__builtin_expect(finite, 1)) return trace_any<STATS, true>(rsrc, 0u, p.n_nodes, rs, h, code, cnt, LDST) > 0 ? 1 : 0;
-    return trace_any<STATS, false>(rsrc, 0u, p.n_nodes, rs, h, code, cnt, LDST) > 0 ? 1 : 0;
+    if (__builtin_expect(finite, 1)) return trace_any<STATS, true>(rsrc, 0u, p.n_nodes, rs, h, code, cnt) > 0 ? 1 : 0;
+    return trace_any<STATS, false>(rsrc, 0u, p.n_nodes, rs, h, code, cnt) > 0 ? 1 : 0;
 }
 
 // The same without suspension (a walk always completes).

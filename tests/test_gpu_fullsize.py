@@ -88,7 +88,7 @@ def test_fullsize_configs_timed_kernel_rows_match_oracle(gpu, oracle_mod, sky, c
     """BASELINE.json's C2 / C3 / C4 at full size through the instantiation bench.py times
     (ordered walk, cost schedule, no counters), 8 passes: six evenly spaced rows and their
     XORWOW end states equal the oracle's bit for bit.  At 64 passes the long-chain take applies
-    (ranges shrinking with the ids left, cpt_tuning.hpp CPT_TAKE_TAPER): every pixel of the frame
+    (ranges shrinking with the ids left, cpt_tuning.hpp TAKE_TAPER): every pixel of the frame
     must then have been taken exactly once, so every pass count is spp."""
     cfg = scenes.CONFIGS[config]
     W, H, depth = cfg["width"], cfg["height"], cfg["depth"]
