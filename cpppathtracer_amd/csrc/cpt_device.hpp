@@ -514,7 +514,7 @@ __device__ __forceinline__ float uniform(Xorwow& s) {
 }
 
 // ------------------------------------------------------------------------------------
-// Scene data in HBM (DESIGN.md §Data layout)
+// Scene data in HBM (DESIGN.md §The path and its boundary)
 // ------------------------------------------------------------------------------------
 // BVH node, 32 B, right-first preorder ("skip-link" order): the node after n in memory is
 // its right child (the child the reference's DFS pops first, bvh.cu:201-202).  The eight

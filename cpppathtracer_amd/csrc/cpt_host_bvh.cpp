@@ -306,7 +306,7 @@ int build(HostBvh& t, const std::vector<cpt_object>& O, std::vector<int>& idx, i
 }  // namespace sah
 
 // ------------------------------------------------------------------------------------
-// 4-wide walk tree (DESIGN.md §Wide walk).  The binary SAH walk tree is collapsed into
+// 4-wide walk tree (DESIGN.md §Ordered walk, Execution).  The binary SAH walk tree is collapsed into
 // nodes of up to four children: starting from a node's two children, the internal child
 // with the largest box is replaced by its own two children until there are four (or only
 // leaves).  Appended to `out` (after the eight binary octant orders): the compact image,

@@ -267,7 +267,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                     // counter and serves its idle lanes from that range over the next rounds, so the
                     // device atomic on the one counter every wave of the grid contends for is issued
                     // once per 64 takes instead of once per round (at 1 spp a wave takes ~11 pixels
-                    // every round: 2.43 -> 1.43 ms per 1-spp C4 render).  Pixels
+                    // every round: 2.43 -> 1.43 ms per 1-spp C4 render, DESIGN.md §Lane refill).  Pixels
                     // are independent chains, so the order they are taken in does not change the image.
                     const uint32_t n_need = wave_count(need);
                     const uint32_t avail = res_end - res_id;
@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                         const bool batch_ok = p.spp >= 64 || left_ids > n_static;
                         // the consolidating kernel (frames of <= 4 pixels per lane) takes exactly what
                         // it needs: there a wave's unstarted ids hold back chains other waves' idle
-                        // lanes could run
+                        // lanes could run (DESIGN.md §Lane refill)
                         const uint32_t grab = !CONS && batch_ok && bsz > want ? bsz : want;
                         if (lane == leader) nb = atomicAdd(p.work, grab);
                         nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader)) + off;

@@ -616,7 +616,7 @@ __device__ __forceinline__ int trace(const SRC& nodes, int n_nodes, const RayK& 
 // stopped at a parked leaf (cpt_tuning.hpp).
 
 // ======================================================================================
-// The ordered walk on the 4-wide walk tree (DESIGN.md §Wide walk).  One iteration reads a
+// The ordered walk on the 4-wide walk tree (DESIGN.md §Ordered walk, Execution).  One iteration reads a
 // 112-B node of the tree's compact image (cpt_capi.cpp linearise_wide) and tests its four
 // children's boxes with the conservative octant-form slab; the nearest hit child is taken
 // next, the other hits go onto a per-lane stack in LDS (far ones first).  Leaves are parked

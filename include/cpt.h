@@ -145,8 +145,8 @@ typedef struct cpt_ctx cpt_ctx;
  * (CPT_RENDER_STATS) are then this walk's counts, not the reference's. */
 #define CPT_TRAVERSAL_ORDERED 0x200u
 /* With CPT_TRAVERSAL_ORDERED: test each leaf where the walk meets it.  By default the ordered
- * walk parks a leaf and runs the parked leaves of a wave together (DESIGN.md §Postponed
- * leaves); the closest hits are the same, but the node/prim counts then depend on which rays
+ * walk parks a leaf and runs the parked leaves of a wave together (DESIGN.md §Ordered walk,
+ * parked leaves); the closest hits are the same, but the node/prim counts then depend on which rays
  * share a wave.  This flag makes them a per-ray property (the oracle's diagnostic walk). */
 #define CPT_TRAVERSAL_PLAIN_LEAVES 0x400u
 /* Megakernel pixel schedule: a short pilot render (1..4 passes from the current RNG states,

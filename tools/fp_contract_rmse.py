@@ -1,4 +1,4 @@
-"""How far does FMA contraction move the integrator's output?  (DIAGNOSTIC)
+"""How far does FMA contraction move the integrator's output?  (DIAGNOSTIC, DESIGN.md §Oracle and parity status)
 
 The reference was compiled by nvcc without --use_fast_math, so a*b+c was contracted into FMA
 (SURVEY.md 8(a) numeric semantics).  The shipped oracle and libcpt.so are both built with
