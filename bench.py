@@ -63,7 +63,7 @@ def parse_args(argv=None):
                     help="BVH node order: the reference's right-first DFS, or near-first per ray octant "
                          "(CPT_TRAVERSAL_ORDERED, same closest hits; DESIGN.md §Ordered walk)")
     ap.add_argument("--consolidate", default="auto", choices=["auto", "on", "off"],
-                    help="megakernel tail consolidation (auto: on for ranks of <= 4 pixels per lane, spp >= 512)")
+                    help="megakernel tail consolidation (auto: on for ranks of more than 1 and at most 4 pixels per lane, spp >= 512)")
     ap.add_argument("--schedule", default="auto", choices=["auto", "cost", "tiles"],
                     help="megakernel pixel dequeue order: 8x8 tiles heaviest first from a pilot pass "
                          "(CPT_SCHEDULE_COST), or tiles in row-major order; auto: cost from 64 passes up "
@@ -304,11 +304,11 @@ def run(args):
         schedule = "cost" if spp >= 64 else "tiles"
     consolidate = {"auto": None, "on": True, "off": False}[args.consolidate]
     # the library's rule (cpt_capi.cpp): the LDS-walk megakernel consolidates its tail when the
-    # rank holds at most 4 pixels per lane of the persistent grid (1024 lanes per CU) and the
-    # chains have at least 512 passes
+    # rank holds more than 1 and at most 4 pixels per lane of the persistent grid (1024 lanes per
+    # CU) and the chains have at least 512 passes
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     consolidating = (args.path == "megakernel" and ordered and spp > 1 and
-                     (consolidate if consolidate is not None else spp >= 512 and npix_local <= 4 * 1024 * cus))
+                     (consolidate if consolidate is not None else spp >= 512 and 1024 * cus < npix_local <= 4 * 1024 * cus))
 
     def step(timed=False):
         r.render(cam, spp, depth, path=args.path, ordered=ordered, schedule=schedule, consolidate=consolidate)

@@ -470,16 +470,21 @@ int cpt_render(cpt_ctx* c, const cpt_camera* cam, int spp, int max_depth, uint32
         }
         // Tail consolidation (cpt_kernels.hip): one slab of hand-over slots per workgroup of the
         // persistent grid (one LDS workgroup of 1024 lanes per CU), 3 x 256 chains each.  By
-        // default for frames of at most 4 pixels per lane and chains of at least 512 passes:
-        // with more pixels the tail is a small part of the render, with short chains the
-        // hand-overs do not pay, and the plain kernel's tighter code wins (DESIGN.md §Multi-GPU;
-        // C2 at 0.9 pixels per lane and 256 spp: 23.2 vs 21.9 Gpaths/s without).
+        // default for frames of more than 1 and at most 4 pixels per lane and chains of at least
+        // 512 passes: with more pixels the tail is a small part of the render, with short chains
+        // the hand-overs do not pay, and the plain kernel's tighter code wins (DESIGN.md
+        // §Multi-GPU; C2 at 0.9 pixels per lane and 256 spp: 23.2 vs 21.9 Gpaths/s without).  At
+        // one pixel per lane no lane takes a second chain and the plain kernel wins too (C4 at
+        // N = 8, slowest rank: 309 vs 322 ms in r06, 314-318 vs 322 in r05, 304 vs 325 with
+        // this rule; profiles/r06/reh_cons_r06z.log, r06/cert/reh_c4_cons_rule.log,
+        // profiles/r05/reh_cons_off_vs_auto.log).
         int cus = 0;
         HIP_TRY(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         cus = std::max(cus, 1);
+        const size_t frame_px = (size_t)c->n_rows * c->width, grid_lanes = 1024u * (size_t)cus;
         const bool cons = (flags & CPT_SCHEDULE_CONSOLIDATE) ||
-                          (!(flags & CPT_SCHEDULE_NO_CONSOLIDATE) && spp >= 512 &&
-                           (size_t)c->n_rows * c->width <= 4u * 1024u * (size_t)cus);
+                          (!(flags & CPT_SCHEDULE_NO_CONSOLIDATE) && spp >= 512 && frame_px > grid_lanes &&
+                           frame_px <= 4u * grid_lanes);
         if (cons && spp > 1) {
             const size_t cap = 3u * 256u * (size_t)cus;
             int rc;

@@ -154,8 +154,8 @@ class Renderer:
         heaviest first; same results, DESIGN.md §Cost schedule) or "previous"
         (CPT_SCHEDULE_PREVIOUS: heaviest first by the previous such render's per-tile RNG draws,
         no pilot; for repeated renders of few passes, the DispatchRay loop).
-        consolidate: None (the library's default: on for frames of <= 4 pixels per lane and
-        spp >= 512), True or
+        consolidate: None (the library's default: on for frames of more than 1 and at most 4
+        pixels per lane and spp >= 512), True or
         False (CPT_SCHEDULE_[NO_]CONSOLIDATE): the megakernel's tail consolidation, same results."""
         if path not in PATHS:
             raise ValueError(f"path must be one of {PATHS}")

@@ -159,7 +159,8 @@ typedef struct cpt_ctx cpt_ctx;
 /* Megakernel tail consolidation: once the pixel queue is drained, the
  * waves of a workgroup hand their chains over at pass boundaries so that each SIMD runs fewer,
  * fuller waves while chains finish.  Identical results.  By default it runs when spp >= 512 and
- * the frame holds at most 4 pixels per lane of the persistent grid (a strong-scaled row tile);
+ * the frame holds more than 1 and at most 4 pixels per lane of the persistent grid (a
+ * strong-scaled row tile on 2-7 GPUs at 1080p);
  * these flags force it on or off (on needs spp > 1).  Only the 4-wide walk consolidates
  * (CPT_TRAVERSAL_ORDERED with a 4-wide walk tree, cpt_get_walk_info [2] > 0).  A hand-over that
  * cannot complete ends the render with CPT_ERR_DEVICE, never with silently missing pixels. */

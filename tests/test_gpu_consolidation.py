@@ -1,5 +1,5 @@
-"""Tail consolidation (k_megakernel<..., CONS>, cpt_kernels.hip): the default kernel of every
-N >= 2 rank.  Its hand-overs must either finish every chain bit for bit or end the render with
+"""Tail consolidation (k_megakernel<..., CONS>, cpt_kernels.hip): the default kernel of
+ranks holding more than 1 and at most 4 pixels per lane (N = 2..7 at 1080p, C5 at N = 8).  Its hand-overs must either finish every chain bit for bit or end the render with
 an error -- never with silently missing pixels (cpt.h CPT_ERR_DEVICE; the reference at least
 logs its CUDA errors, path_tracer.cu:279-283).
 """

@@ -220,8 +220,8 @@ def _kw(path):
 def _timed(path):
     """"<path>+timed": the instantiation bench.py times — no STATS counters, and for the
     megakernel the cost schedule (pilot pass + heaviest-tiles-first order).  "+cons" forces the
-    tail-consolidating megakernel, which the library picks by itself for ranks of <= 4 pixels per
-    lane at >= 512 spp (strong-scaled row tiles); these small test renders would otherwise run
+    tail-consolidating megakernel, which the library picks by itself for ranks of more than 1 and
+    at most 4 pixels per lane at >= 512 spp (strong-scaled row tiles); these small test renders would otherwise run
     the plain one, the kernel the N = 1 bench times."""
     return "+timed" in path
 
