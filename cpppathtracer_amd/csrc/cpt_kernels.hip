@@ -258,6 +258,9 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                     // the wave's first tile by level: the heaviest tiles (cost order) go to the
                     // level-0 waves (one per SIMD), the lightest to level 3, so every SIMD holds
                     // one heavy wave that runs alone once its lighter neighbours finish
+                    // (pairing the heaviest level-0 waves with the lightest of the other levels
+                    // instead lost: C4 N = 4 / 8 slowest rank 389-409 / 316-318 vs 323-338 /
+                    // 308-310 ms, profiles/r06/ab_reh_snake.log)
                     base = (level * (gridDim.x * 4u) + blockIdx.x * 4u + ((threadIdx.x >> 6) & 3u)) * 64u;
                     if (n_static >= n_work) exhausted = true;
                     lane_id = base + lane_rank(need);
