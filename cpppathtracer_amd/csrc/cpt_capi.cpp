@@ -1107,7 +1107,7 @@ int cpt_measure_read_pattern(cpt_ctx* c, int bytes_per_lane, size_t bytes, int i
 }
 
 int cpt_selftest_qdiv(cpt_ctx* c, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len) {
-    if (!c || !out || out_len < 1 || which < 0 || which > 13) return CPT_ERR_INVALID_ARG;
+    if (!c || !out || out_len < 1 || which < 0 || which > 16) return CPT_ERR_INVALID_ARG;
     HIP_TRY(c, hipSetDevice(c->device));
     unsigned long long* d = nullptr;
     HIP_TRY(c, hipMalloc((void**)&d, out_len * sizeof(unsigned long long)));

@@ -878,6 +878,66 @@ __device__ __forceinline__ bool dn_near_midpoint(double e) {
     return !normal_f || (d < 512 && d > -512);
 }
 
+// The winner certificate's quotient-free form (cpt_path.hpp cert_inside) against the exact slab
+// test it stands in for (slab_reject<true> with exact quotients), on case i of a counter-hashed
+// stream (seed, i): a box (sphere-like, or a platform's +-5e30 x/z slab), a ray (3% of axes with
+// d == 0) and a distance t either within 16 float ulps of one of the six planes' exact quotients
+// (the only place the two can disagree) or anywhere in (0, 200].  which = 14 counts the cases
+// the certificate passes and the exact test rejects (0 expected); 15 counts the cases it
+// certifies, 16 the cases the exact test passes (the test checks the form decides most of them).
+__device__ __forceinline__ uint64_t cert_mix(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ float cert_unit(uint64_t& st) {
+    st = cert_mix(st);
+    return (float)(uint32_t)(st >> 40) * 0x1p-24f;
+}
+__device__ bool cert_case(uint64_t seed, uint64_t i, int which) {
+    uint64_t st = cert_mix(seed ^ cert_mix(i));
+    float c[3], e[3], o[3], d[3];
+    for (int k = 0; k < 3; ++k) {
+        c[k] = -30.f + 60.f * cert_unit(st);
+        const float u = cert_unit(st);
+        e[k] = 1e-3f + 10.f * u * u * u;
+        o[k] = -60.f + 120.f * cert_unit(st);
+        d[k] = cert_unit(st) - 0.5f;
+    }
+    const float inv = 1.0f / __builtin_sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    for (int k = 0; k < 3; ++k) d[k] = cert_unit(st) < 0.03f ? 0.0f : d[k] * inv;
+    Node box{};
+    box.a0 = c[0] - e[0]; box.a1 = c[1] - e[1]; box.a2 = c[2] - e[2];
+    box.b0 = c[0] + e[0]; box.b1 = c[1] + e[1]; box.b2 = c[2] + e[2];
+    if (cert_unit(st) < 0.1f) {   // a platform's box: unbounded in x and z, +-1e-4 in y
+        box.a0 = box.a2 = -5e30f; box.b0 = box.b2 = 5e30f;
+        box.a1 = c[1] - 1e-4f; box.b1 = c[1] + 1e-4f;
+    }
+    float t;
+    if (cert_unit(st) < 0.5f) {
+        const int ax = (int)(cert_unit(st) * 3.f) % 3;
+        const bool lo_side = cert_unit(st) < 0.5f;
+        const float pa[3] = {box.a0, box.a1, box.a2}, pb[3] = {box.b0, box.b1, box.b2};
+        const float q = ((lo_side ? pa[ax] : pb[ax]) - o[ax]) / d[ax];
+        const int k = (int)(cert_unit(st) * 33.f) - 16;
+        t = __int_as_float(__float_as_int(q) + (q >= 0.f ? k : -k));
+    } else {
+        t = 200.f * cert_unit(st);
+    }
+    const float tmin = 1e-3f;
+    if (!(t > tmin && t < DEFAULT_RAY_TMAX)) return false;   // not a winner's distance
+    Ray r;
+    r.o = mk(o[0], o[1], o[2]);
+    r.d = mk(d[0], d[1], d[2]);
+    r.tmin = tmin;
+    r.tmax = DEFAULT_RAY_TMAX;
+    const RayK rk = make_rayk(r);
+    const bool cert = cert_inside(box, rk, t);
+    const bool exact = !slab_reject<true>(box, with_slab(rk), t);
+    return which == 14 ? cert && !exact : (which == 15 ? cert : exact);
+}
+
 // Exhaustive checks of the lobe's short transcendentals (cpt_device.hpp lobe_pow, lobe_sincos)
 // against the full dm:: sequences, over the float patterns [0, n) (cpt_selftest_qdiv):
 // which = 8: lobe_pow(x, y) vs (float)dm::pow(x, y), y = the double with the bits of `seed`;
@@ -891,7 +951,9 @@ __global__ void k_selftest_fm(int which, uint64_t n, uint64_t seed, unsigned lon
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const float x = __uint_as_float((uint32_t)i);
         bool flag;
-        if (which == 8) {
+        if (which >= 14) {
+            flag = cert_case(seed, i, which);
+        } else if (which == 8) {
             flag = __float_as_uint(lobe_pow(x, y)) != __float_as_uint((float)dm::pow((double)x, y));
         } else if (which == 9) {
             bool ok;

@@ -409,6 +409,10 @@ int cpt_math_batch(cpt_ctx* ctx, int op, const float* a, const float* b, float* 
  * counts the guard's fallbacks there; which = 12: the sky fetch's short atanf and asinf
  * (miss_atanf, miss_asinf) against the full sequences for the float patterns [0, n); which = 13:
  * counts the patterns where either guard falls back (asinf: on [-1, 1]).
+ * which = 14: the ordered walk's quotient-free winner certificate (cert_inside) against the exact
+ * slab test on n hashed cases from `seed` (boxes, rays, distances within 16 ulps of a plane):
+ * out[0] counts the cases it certifies and the exact test rejects (0 expected); which = 15 counts
+ * the certified cases and which = 16 the cases the exact test passes.
  * out[0] receives the mismatch count (0 expected), out[1..out_len) up to out_len-1 failing
  * pairs as (a bits << 32 | d bits). */
 int cpt_selftest_qdiv(cpt_ctx* ctx, int which, uint64_t n, uint64_t seed, uint64_t* out, int out_len);

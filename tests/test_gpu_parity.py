@@ -159,6 +159,22 @@ def test_miss_atan_asin_exhaustive(gpu):
     assert fell - 2 * 0x00800000 - (1 << 24) < 1e-5 * (1 << 32), fell
 
 
+def test_winner_certificate_quotient_free(gpu):
+    """The ordered walk's quotient-free winner certificate (cpt_path.hpp cert_inside, round 6) as
+    compiled for the device never certifies a box the exact slab test rejects (bvh.cu:181-200 with
+    the exact quotients, slab_reject<true>): 2^32 hashed cases, half of them with the distance
+    within 16 ulps of a box plane's exact quotient (where it must stay inconclusive) and the rest
+    at random distances; both sides are exercised (r06: 19.8 M of the 108 M passing cases
+    certified).  tests/test_certificate.py restates it on the host and checks that hits well
+    inside their box are certified."""
+    n = 1 << 32
+    bad, ids = gpu.selftest_qdiv(14, n, seed=20261018)
+    assert bad == 0, ids
+    certified, _ = gpu.selftest_qdiv(15, n, seed=20261018)
+    passing, _ = gpu.selftest_qdiv(16, n, seed=20261018)
+    assert passing > 1e7 and certified > 0.1 * passing, (certified, passing)
+
+
 # ------------------------------------------------------------------------------- rng
 @pytest.mark.parametrize("w,rows", [(64, list(range(64))), (3840, [0, 1, 7, 1079, 2159]),
                                     (333, [5, 3, 200, 3])])
