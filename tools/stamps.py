@@ -1,7 +1,7 @@
 """Wave-time breakdown of the megakernel from a CPT_STAMPS diagnostic build (cpt_stamps.hpp;
 never the timed library).
 
-    python tools/stamps.py [config] [spp] [--rows=a:b] [--width=W] [--schedule=cost|tiles|previous]   (CPT_LIB_PATH = the stamped build)
+    python tools/stamps.py [config] [spp] [--rows=a:b] [--width=W] [--schedule=cost|tiles|previous] [--consolidate=on|off]   (CPT_LIB_PATH = the stamped build)
 
 Build the diagnostic library with
     python -c "from cpppathtracer_amd import build as b; b.build(out='build/diag/stamps.so', defines={'CPT_STAMPS': 1})"
@@ -24,7 +24,10 @@ spp = int(args[1]) if len(args) > 1 else 8
 rows = None
 width = cfg["width"]
 schedule = "cost"
+consolidate = None
 for a in sys.argv[1:]:
+    if a.startswith("--consolidate="):
+        consolidate = {"on": True, "off": False}[a[14:]]
     if a.startswith("--schedule="):
         schedule = a[11:]
     if a.startswith("--width="):
@@ -45,7 +48,7 @@ if schedule == "previous":   # the DispatchRay loop's order: from a previous ren
     r.render(cam, spp, cfg["depth"], sync=True, ordered=True, schedule="previous")
     r.init_rng(1234)
     r.reset_stats()
-r.render(cam, spp, cfg["depth"], stats=True, sync=True, ordered=True, schedule=schedule)
+r.render(cam, spp, cfg["depth"], stats=True, sync=True, ordered=True, schedule=schedule, consolidate=consolidate)
 c = r.diag_counters()
 st = dict(zip(["segments", "nodes", "prims", "hits", "misses"], r.raw_counters()[:5]))
 tot = sum(c[:8]) + c[11] + c[12]
