@@ -186,62 +186,6 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         timeline::round(tl, __ballot(busy), exhausted, level);
         if (cons && !retiring && level > 0 && exhausted && vq[3] == 0u && vq[2] <= level * (uint32_t)CONS_RETIRE_PER_LEVEL) retiring = true;
         bool begin = false;   // a lane took a chain: start its next pass
-        // ---- take handed-over chains into idle lanes (consolidation) ---------------------
-        if (cons && !retiring && exhausted) {
-            const uint64_t need = __ballot(!busy && lane < p.lanes);
-            if (need && vq[1] != vq[0]) {
-                const int leader = __ffsll((unsigned long long)need) - 1;
-                uint32_t h = 0, n = 0;
-                if (lane == leader) {
-                    for (int tries = 0; tries < 16; ++tries) {
-                        h = vq[0];
-                        uint32_t t = vq[1];
-                        t = t < (uint32_t)QS ? t : (uint32_t)QS;   // slots past the cap are never written
-                        const uint32_t want = (uint32_t)__popcll(need);
-                        n = t > h ? (t - h < want ? t - h : want) : 0u;
-                        if (n == 0 || atomicCAS(&s_q[0], h, h + n) == h) break;
-                        n = 0;
-                    }
-                }
-                h = __shfl(h, leader);
-                n = __shfl(n, leader);
-                const uint32_t rank = lane_rank(need);
-                bool lost = false;
-                if (((need >> lane) & 1ull) && rank < n) {
-                    const uint32_t slot = h + rank;
-                    // the slot was allocated before it was written: wait for its publication
-                    const volatile uint8_t* fl = s_qflag + slot;
-                    for (uint32_t w = 0; *fl == 0 && w < publish_wait; ++w) __builtin_amdgcn_s_sleep(1);
-                    lost = *fl == 0;
-                }
-                if (lost) {
-                    // never published: the chain is abandoned (its pixel is not written) and
-                    // the render reports CPT_DEVERR_PUBLISH_TIMEOUT instead of reading the slot
-                    atomicOr(p.error, CPT_DEVERR_PUBLISH_TIMEOUT);
-                    atomicSub(&s_q[2], 1u);
-                } else if (((need >> lane) & 1ull) && rank < n) {
-                    const uint32_t slot = h + rank;
-                    const uint32_t* e = reinterpret_cast<const uint32_t*>(qslab + 5 * (size_t)slot);
-                    auto ld4 = [&](int q) {
-                        return make_uint4(ld_coherent(e + 4 * q), ld_coherent(e + 4 * q + 1), ld_coherent(e + 4 * q + 2),
-                                          ld_coherent(e + 4 * q + 3));
-                    };
-                    const uint4 e0 = ld4(0), e1 = ld4(1), e2 = ld4(2), e3 = AUX ? ld4(3) : make_uint4(0u, 0u, 0u, 0u);
-                    const uint32_t left = ld_coherent(e + 16);
-                    L.pix = e0.x; L.xy = e0.y; L.s.v0 = e0.z; L.s.v1 = e0.w;
-                    L.s.v2 = e1.x; L.s.v3 = e1.y; L.s.v4 = e1.z; L.s.d = e1.w;
-                    L.sum = mk(__uint_as_float(e2.x), __uint_as_float(e2.y), __uint_as_float(e2.z));
-                    L.passes = __uint_as_float(e2.w);
-                    if (AUX) {
-                        first_normal = mk(__uint_as_float(e3.x), __uint_as_float(e3.y), __uint_as_float(e3.z));
-                        first_depth = __uint_as_float(e3.w);
-                    }
-                    L.left = (int)left;
-                    busy = true;
-                    begin = true;
-                }
-            }
-        }
         // ---- refill idle lanes with new pixels (wave-aggregated dequeue) ----------------
         if (!exhausted && !retiring) {
             // cold fields reloaded here from the kernarg segment rather than held in SGPRs
@@ -375,6 +319,96 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                 }
             }
         }
+        // ---- take handed-over chains into idle lanes (consolidation) ---------------------
+        if (cons && !retiring && exhausted) {
+            const uint64_t need = __ballot(!busy && lane < p.lanes);
+            // (After the refill: a wave whose last take this round exhausted the counter with every
+            // lane idle joins the keepers at once.)
+            // A keeper with no chain left waits here, in this block, until it holds a handed-over
+            // chain or its workgroup is done (no wave still taking, no chain live; a chain in
+            // flight is never more than a pass away from its hand-over or its end).  Waiting by
+            // going round the loop instead -- a back edge with every lane idle -- made the
+            // register allocator spill 26 VGPRs in this kernel.
+            const bool idle_wave = !__any(busy);
+            bool quit = false;
+            for (;;) {
+                if (idle_wave) {
+                    while (vq[1] == vq[0]) {   // nothing allocated to take
+                        if (vq[3] == 0u && vq[2] == 0u) { quit = true; break; }
+                        if (++idle_spins > keeper_spins) {
+                            // never hang the device on a lost count, but never end silently either:
+                            // chains of this workgroup may be left unfinished
+                            if (lane == 0) atomicOr(p.error, CPT_DEVERR_KEEPER_TIMEOUT);
+                            quit = true;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(16);
+                    }
+                    if (quit) break;
+                }
+                if (need && vq[1] != vq[0]) {
+                    const int leader = __ffsll((unsigned long long)need) - 1;
+                    uint32_t h = 0, n = 0;
+                    if (lane == leader) {
+                        for (int tries = 0; tries < 16; ++tries) {
+                            h = vq[0];
+                            uint32_t t = vq[1];
+                            t = t < (uint32_t)QS ? t : (uint32_t)QS;   // slots past the cap are never written
+                            const uint32_t want = (uint32_t)__popcll(need);
+                            n = t > h ? (t - h < want ? t - h : want) : 0u;
+                            if (n == 0 || atomicCAS(&s_q[0], h, h + n) == h) break;
+                            n = 0;
+                        }
+                    }
+                    h = __shfl(h, leader);
+                    n = __shfl(n, leader);
+                    const uint32_t rank = lane_rank(need);
+                    bool lost = false;
+                    if (((need >> lane) & 1ull) && rank < n) {
+                        const uint32_t slot = h + rank;
+                        // the slot was allocated before it was written: wait for its publication
+                        const volatile uint8_t* fl = s_qflag + slot;
+                        for (uint32_t w = 0; *fl == 0 && w < publish_wait; ++w) __builtin_amdgcn_s_sleep(1);
+                        lost = *fl == 0;
+                    }
+                    if (lost) {
+                        // never published: the chain is abandoned (its pixel is not written) and
+                        // the render reports CPT_DEVERR_PUBLISH_TIMEOUT instead of reading the slot
+                        atomicOr(p.error, CPT_DEVERR_PUBLISH_TIMEOUT);
+                        atomicSub(&s_q[2], 1u);
+                    } else if (((need >> lane) & 1ull) && rank < n) {
+                        const uint32_t slot = h + rank;
+                        const uint32_t* e = reinterpret_cast<const uint32_t*>(qslab + 5 * (size_t)slot);
+                        auto ld4 = [&](int q) {
+                            return make_uint4(ld_coherent(e + 4 * q), ld_coherent(e + 4 * q + 1), ld_coherent(e + 4 * q + 2),
+                                              ld_coherent(e + 4 * q + 3));
+                        };
+                        const uint4 e0 = ld4(0), e1 = ld4(1), e2 = ld4(2), e3 = AUX ? ld4(3) : make_uint4(0u, 0u, 0u, 0u);
+                        const uint32_t left = ld_coherent(e + 16);
+                        L.pix = e0.x; L.xy = e0.y; L.s.v0 = e0.z; L.s.v1 = e0.w;
+                        L.s.v2 = e1.x; L.s.v3 = e1.y; L.s.v4 = e1.z; L.s.d = e1.w;
+                        L.sum = mk(__uint_as_float(e2.x), __uint_as_float(e2.y), __uint_as_float(e2.z));
+                        L.passes = __uint_as_float(e2.w);
+                        if (AUX) {
+                            first_normal = mk(__uint_as_float(e3.x), __uint_as_float(e3.y), __uint_as_float(e3.z));
+                            first_depth = __uint_as_float(e3.w);
+                        }
+                        L.left = (int)left;
+                        busy = true;
+                        begin = true;
+                    }
+                }
+                // one pass for a wave with chains; an idle wave whose take lost the race (or whose
+                // chains were never published) tries again
+                if (!idle_wave || __any(busy)) break;
+                if (++idle_spins > keeper_spins) {
+                    if (lane == 0) atomicOr(p.error, CPT_DEVERR_KEEPER_TIMEOUT);
+                    quit = true;
+                    break;
+                }
+            }
+            if (quit) break;
+        }
         if (begin) {
             execdiag::lanes(p.stats + 64, 10);
             start_pass();
@@ -383,23 +417,10 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         if (!__any(busy)) {
             // (a wave whose takes all fell outside the frame takes again while ids remain: it may
             // still hold reserved ids, which no other wave would render)
-            if (!cons || retiring) {
-                if (!exhausted) continue;
-                break;
-            }
-            if (exhausted) {
-                // a keeper with nothing to do: wait for hand-overs while any chain is live (a
-                // chain in flight is never more than a pass away from its hand-over or its end)
-                if (vq[3] == 0u && vq[2] == 0u) break;
-                if (++idle_spins > keeper_spins) {
-                    // never hang the device on a lost count, but never end silently either:
-                    // chains of this workgroup may be left unfinished
-                    if (lane == 0) atomicOr(p.error, CPT_DEVERR_KEEPER_TIMEOUT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(16);
-            }
-            continue;   // taken ids past the frame's rows: take again
+            // (a keeper of a consolidating workgroup never gets here idle: it waits in the take
+            // above until its workgroup is done; an idle wave here holds no chain)
+            if (!exhausted) continue;
+            break;
         }
         Hit h;
         int code = -1;
