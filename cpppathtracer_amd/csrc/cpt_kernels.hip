@@ -127,8 +127,10 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
     v3 att = mk1(1.f), rad = mk1(0.f);
     uint32_t depth = 0;
     bool first = true;
-    v3 nrm_acc = mk1(0.f), first_normal = mk1(0.f);
-    float dep_acc = 0.f, first_depth = 0.f;
+    // AUX: the first hit's normal of the lane's latest pass (path_tracer.cu:160-163: summed into
+    // zeroed accumulators on the pass's first segment only, so 0 + n); its depth is always
+    // DEFAULT_RAY_TMAX (a18: TraceRay took the ray by value), written as that constant
+    v3 first_normal = mk1(0.f);
 
     // a lane's pending sky fetch: direction, the pass's radiance and attenuation so far
     __shared__ float pending_q[DEFER_MISS_ROUND > 0 ? 9 * BLK : 1];
@@ -165,8 +167,6 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
         rad = mk1(0.f);
         depth = 0;
         first = true;
-        nrm_acc = mk1(0.f);
-        dep_acc = 0.f;
     };
     // STATIC_FIRST (LDS walk): each wave's first tile is placed by level (see the refill); the
     // counter then hands out the tiles after the first gridDim.x * BLK pixels
@@ -294,7 +294,6 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                         L.passes = acc.w;
                         L.left = p.spp;
                         first_normal = mk1(0.f);
-                        first_depth = 0.f;
                         if (PROBE) work_at_take = cnt.segments + cnt.nodes + cnt.prims;
                         if (max_depth == 0) {
                             // while (0 < 0) never runs: each pass is RayGen's draws and zero radiance
@@ -391,7 +390,6 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                         L.passes = __uint_as_float(e2.w);
                         if (AUX) {
                             first_normal = mk(__uint_as_float(e3.x), __uint_as_float(e3.y), __uint_as_float(e3.z));
-                            first_depth = __uint_as_float(e3.w);
                         }
                         L.left = (int)left;
                         busy = true;
@@ -520,10 +518,9 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             if (!hit) depth = MAX_RECURSION_DEPTH_SET;   // termination sentinel (path_tracer.cu:121)
             rad = rad + att * sh.radiance;
             att = att * sh.attenuation;
-            if (AUX && first) {
-                nrm_acc = nrm_acc + attr_normal;
-                dep_acc += DEFAULT_RAY_TMAX;           // TraceRay took the ray by value (a18)
-            }
+            // the pass's first segment: its normal (0 + n, as the reference's zeroed sum; a pass
+            // ends at a pass boundary only, so first_normal is the finished pass's at every read)
+            if (AUX && first) first_normal = mk1(0.f) + attr_normal;
             first = false;
             ray.d = normalize_u(sh.bounce);
             ray.tmin = BOUNCE_RAY_TMIN;
@@ -532,7 +529,6 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
             if (!(depth < max_depth)) {
                 if (!deferred) L.sum = L.sum + rad;
                 L.passes += 1.0f;
-                if (AUX) { first_normal = nrm_acc; first_depth = dep_acc; }
                 if (--L.left > 0) {
                     if (retiring) hand_over = true;   // the next pass runs in a keeper wave
                     else {
@@ -559,7 +555,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                                                 __float_as_uint(L.sum.x), __float_as_uint(L.sum.y), __float_as_uint(L.sum.z),
                                                 __float_as_uint(L.passes), __float_as_uint(first_normal.x),
                                                 __float_as_uint(first_normal.y), __float_as_uint(first_normal.z),
-                                                __float_as_uint(first_depth), (uint32_t)L.left, 0u, 0u, 0u};
+                                                0u, (uint32_t)L.left, 0u, 0u, 0u};
 #pragma unroll
                         for (int k = 0; k < 17; ++k)
                             if (AUX || k < 12 || k == 16) st_coherent(e + k, w[k]);
@@ -588,7 +584,7 @@ __global__ void __launch_bounds__(mk_block<LDST>(), mk_waves<LDST>()) k_megakern
                     p.normal[3 * (size_t)L.pix + 0] = first_normal.x;
                     p.normal[3 * (size_t)L.pix + 1] = first_normal.y;
                     p.normal[3 * (size_t)L.pix + 2] = first_normal.z;
-                    p.depth[L.pix] = first_depth;
+                    p.depth[L.pix] = max_depth > 0 ? DEFAULT_RAY_TMAX : 0.f;   // a18
                 }
                 p.rng[L.pix] = L.s.v0;
                 p.rng[npix + L.pix] = L.s.v1;
