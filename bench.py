@@ -559,7 +559,7 @@ def run(args):
 # ---------------------------------------------------------------------------------------
 # --dispatch K: the reference's own per-pass loop (PipelineLoop, path_tracer.cu:256-306)
 # ---------------------------------------------------------------------------------------
-DISPLAY_BYTES_PER_PIXEL = 60   # k_denoise_rows (k_denoise_mix under CPT_DN_TILE=1): accum 16 + normal 12 + depth 4 + mix 12 read + 12 written + BGRA 4
+DISPLAY_BYTES_PER_PIXEL = 60   # k_denoise_rows: accum 16 + normal 12 + depth 4 + mix 12 read + 12 written + BGRA 4
 
 
 def dispatch_bench(args):
